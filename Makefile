@@ -1,0 +1,40 @@
+# Build of the MI355X backend (gfx950) and of the CPU oracle.
+#   make            -> hpx_amd/libhpxhip.so + oracle/_build/liboracle.so
+#   make lib        -> the HIP library only
+#   make oracle     -> the oracle only (g++, no ROCm needed)
+#   make cxxtests   -> C++ tests of the header-only HPX-API layer
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+BUILD    := build
+
+HIPFLAGS := -O3 --offload-arch=$(ARCH) -fPIC -std=c++17 -ffp-contract=off \
+            -Wall -Wno-unused-result -Wno-unused-function -Iinclude
+LIB      := hpx_amd/libhpxhip.so
+KSRC     := runtime elementwise reduce scan copy_if sort stencil
+KOBJ     := $(KSRC:%=$(BUILD)/csrc/%.o)
+KHDR     := $(wildcard hpx_amd/csrc/*.hpp) include/hpxhip.h
+
+ORACLE   := oracle/_build/liboracle.so
+OFLAGS   := -O2 -fPIC -std=c++17 -ffp-contract=off -Wall -pthread
+
+.PHONY: all lib oracle clean cxxtests
+
+all: lib oracle
+
+lib: $(LIB)
+oracle: $(ORACLE)
+
+$(BUILD)/csrc/%.o: hpx_amd/csrc/%.hip $(KHDR)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(KOBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(KOBJ)
+
+$(ORACLE): oracle/oracle.cpp oracle/oracle.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(OFLAGS) -shared -o $@ oracle/oracle.cpp
+
+clean:
+	rm -rf $(BUILD) $(LIB) oracle/_build

@@ -1,0 +1,229 @@
+// common.hpp -- device-side building blocks shared by every hpx_amd kernel.
+//
+// MI355X (gfx950, CDNA4) only: wave64, DPP row/wave controls of the GFX9
+// family, agent-scope `sc1` hand-offs between workgroups (the XCD L2s are not
+// coherent with each other).  Nothing here is a CUDA idiom recompiled: the
+// wave primitives are DPP sequences, the inter-workgroup protocol follows
+// the write-through (sc1) + drained flag form of the MI355X microarchitecture
+// guide (Guideline 16, table row 1).
+//
+// The binary operators mirror the functors HPX's algorithms accept
+// (std::plus, std::multiplies, min/max, bit ops; see e.g.
+// hpx/parallel/algorithms/reduce.hpp:200, inclusive_scan.hpp:288) plus the
+// identity element every GPU tree/scan needs for inactive lanes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <type_traits>
+
+namespace hpxhip {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------------------
+// Wrapping integer arithmetic (HPX relies on the host's two's-complement
+// behaviour; device code must not give the optimiser signed-overflow UB).
+template <typename T>
+__host__ __device__ __forceinline__ T wrap_add(T a, T b) {
+    if constexpr (std::is_integral_v<T>) {
+        using U = std::make_unsigned_t<T>;
+        return static_cast<T>(static_cast<U>(a) + static_cast<U>(b));
+    } else {
+        return a + b;
+    }
+}
+template <typename T>
+__host__ __device__ __forceinline__ T wrap_mul(T a, T b) {
+    if constexpr (std::is_integral_v<T>) {
+        using U = std::make_unsigned_t<T>;
+        return static_cast<T>(static_cast<U>(a) * static_cast<U>(b));
+    } else {
+        return a * b;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Binary operators with identities.  The semantics are the std:: functors'
+// (std::min is `(b < a) ? b : a`, std::max is `(a < b) ? b : a`).
+struct op_plus {
+    template <typename T> __host__ __device__ __forceinline__ T operator()(T a, T b) const { return wrap_add(a, b); }
+    template <typename T> __host__ __device__ static constexpr T identity() { return T(0); }
+};
+struct op_multiplies {
+    template <typename T> __host__ __device__ __forceinline__ T operator()(T a, T b) const { return wrap_mul(a, b); }
+    template <typename T> __host__ __device__ static constexpr T identity() { return T(1); }
+};
+struct op_min {
+    template <typename T> __host__ __device__ __forceinline__ T operator()(T a, T b) const { return (b < a) ? b : a; }
+    template <typename T> __host__ __device__ static constexpr T identity() {
+        if constexpr (std::is_floating_point_v<T>) return std::numeric_limits<T>::infinity();
+        else return std::numeric_limits<T>::max();
+    }
+};
+struct op_max {
+    template <typename T> __host__ __device__ __forceinline__ T operator()(T a, T b) const { return (a < b) ? b : a; }
+    template <typename T> __host__ __device__ static constexpr T identity() {
+        if constexpr (std::is_floating_point_v<T>) return -std::numeric_limits<T>::infinity();
+        else return std::numeric_limits<T>::lowest();
+    }
+};
+struct op_bit_and {
+    template <typename T> __host__ __device__ __forceinline__ T operator()(T a, T b) const { return a & b; }
+    template <typename T> __host__ __device__ static constexpr T identity() { return static_cast<T>(~T(0)); }
+};
+struct op_bit_or {
+    template <typename T> __host__ __device__ __forceinline__ T operator()(T a, T b) const { return a | b; }
+    template <typename T> __host__ __device__ static constexpr T identity() { return T(0); }
+};
+struct op_bit_xor {
+    template <typename T> __host__ __device__ __forceinline__ T operator()(T a, T b) const { return a ^ b; }
+    template <typename T> __host__ __device__ static constexpr T identity() { return T(0); }
+};
+
+// ---------------------------------------------------------------------------
+// 16-byte vector of T (one `global_load_dwordx4` per lane).
+template <typename T, int N>
+struct alignas(sizeof(T) * N) vec {
+    T v[N];
+};
+
+template <typename T>
+struct vec_width {
+    static constexpr int value = 16 / sizeof(T);
+};
+
+// ---------------------------------------------------------------------------
+// Bit casts between T and 32-bit lanes (DPP moves 32 bits per lane).
+template <typename T>
+__device__ __forceinline__ void to_words(T x, uint32_t (&w)[(sizeof(T) + 3) / 4]) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4/8-byte types only");
+    __builtin_memcpy(w, &x, sizeof(T));
+}
+template <typename T>
+__device__ __forceinline__ T from_words(const uint32_t (&w)[(sizeof(T) + 3) / 4]) {
+    T x;
+    __builtin_memcpy(&x, w, sizeof(T));
+    return x;
+}
+
+// update_dpp on an arbitrary 4/8-byte type; lanes whose source is invalid or
+// masked off receive `old`.
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf, typename T>
+__device__ __forceinline__ T dpp(T old, T src) {
+    constexpr int W = (sizeof(T) + 3) / 4;
+    uint32_t o[W], s[W], r[W];
+    to_words(old, o);
+    to_words(src, s);
+#pragma unroll
+    for (int i = 0; i < W; ++i)
+        r[i] = __builtin_amdgcn_update_dpp(o[i], s[i], CTRL, ROW_MASK, BANK_MASK, false);
+    return from_words<T>(r);
+}
+
+template <typename T>
+__device__ __forceinline__ T readlane(T x, int lane) {
+    constexpr int W = (sizeof(T) + 3) / 4;
+    uint32_t s[W], r[W];
+    to_words(x, s);
+#pragma unroll
+    for (int i = 0; i < W; ++i) r[i] = __builtin_amdgcn_readlane(s[i], lane);
+    return from_words<T>(r);
+}
+
+template <typename T>
+__device__ __forceinline__ T shfl(T x, int src_lane) {
+    constexpr int W = (sizeof(T) + 3) / 4;
+    uint32_t s[W], r[W];
+    to_words(x, s);
+#pragma unroll
+    for (int i = 0; i < W; ++i) r[i] = __builtin_amdgcn_ds_bpermute(src_lane << 2, s[i]);
+    return from_words<T>(r);
+}
+
+// DPP controls (GFX9 family, valid on gfx950).
+enum : int {
+    DPP_ROW_SHR1 = 0x111,
+    DPP_ROW_SHR2 = 0x112,
+    DPP_ROW_SHR3 = 0x113,
+    DPP_ROW_SHR4 = 0x114,
+    DPP_ROW_SHR8 = 0x118,
+    DPP_WAVE_SHR1 = 0x138,
+    DPP_ROW_BCAST15 = 0x142,
+    DPP_ROW_BCAST31 = 0x143,
+};
+
+// Inclusive wave64 scan: lane l receives x_0 (+) ... (+) x_l.
+// 7 DPP steps: three row_shr from the original value, row_shr:4/8 inside the
+// 16-lane rows, then row_bcast:15/31 across rows.
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_inclusive_scan(T x, Op op) {
+    const T id = Op::template identity<T>();
+    T s = op(x, dpp<DPP_ROW_SHR1>(id, x));
+    s = op(s, dpp<DPP_ROW_SHR2>(id, x));
+    s = op(s, dpp<DPP_ROW_SHR3>(id, x));
+    s = op(s, dpp<DPP_ROW_SHR4, 0xf, 0xe>(id, s));
+    s = op(s, dpp<DPP_ROW_SHR8, 0xf, 0xc>(id, s));
+    s = op(s, dpp<DPP_ROW_BCAST15, 0xa, 0xf>(id, s));
+    s = op(s, dpp<DPP_ROW_BCAST31, 0xc, 0xf>(id, s));
+    return s;
+}
+
+// Exclusive companion of an inclusive wave scan (lane 0 gets the identity).
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_shift_right(T incl) {
+    return dpp<DPP_WAVE_SHR1>(Op::template identity<T>(), incl);
+}
+
+// Wave64 reduction: every lane receives the total.
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_reduce(T x, Op op) {
+    return readlane(wave_inclusive_scan(x, op), kWave - 1);
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// ---------------------------------------------------------------------------
+// Inter-workgroup hand-off words (agent scope).  Producer: payload stored
+// with sc1 (`relaxed, agent` atomic store), then `s_waitcnt vmcnt(0)`, then
+// the flag stored the same way by the same lane.  Consumer: relaxed sc1 poll,
+// and only after the poll matched, sc1 loads of the payload.
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+    if constexpr (sizeof(T) == 8) {
+        uint64_t u;
+        __builtin_memcpy(&u, &v, 8);
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        uint32_t u;
+        __builtin_memcpy(&u, &v, 4);
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+    T v;
+    if constexpr (sizeof(T) == 8) {
+        uint64_t u = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_memcpy(&v, &u, 8);
+    } else {
+        uint32_t u = __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_memcpy(&v, &u, 4);
+    }
+    return v;
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Compiler-only ordering: keep payload loads below the poll that licensed them.
+__device__ __forceinline__ void order_after_poll() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); }
+
+// Bounded spin: every look-back wait gives up after this many polls and
+// raises the device error word instead of hanging the GPU.
+constexpr uint32_t kSpinLimit = 1u << 24;
+
+// Device error word (per library instance); set by a kernel that gave up a
+// spin, read back by hpxhip_device_error().
+enum : uint32_t { HPXHIP_DEVERR_NONE = 0, HPXHIP_DEVERR_LOOKBACK_TIMEOUT = 1 };
+
+}  // namespace hpxhip

@@ -1,0 +1,297 @@
+// elementwise.hip -- fill / copy / for_each / transform (unary, binary).
+//
+// Replaces the reference's one-thread-per-element closure launch
+// (hpx/compute/cuda/default_executor.hpp:87-136 -> detail/launch.hpp:32-137,
+// block = 1024, 32-bit index, scalar access) with a gfx950 streaming kernel:
+//   * 16-byte vector accesses (global_load_dwordx4 / global_store_dwordx4);
+//   * each thread keeps UNROLL independent vectors in flight per array;
+//   * grid-stride over a grid sized to fill 256 CUs (8 blocks x 256 threads
+//     per CU), 64-bit indexing throughout;
+//   * a head (to reach 16-B alignment) and a tail handled inside the same
+//     launch, so any iterator offset works; ranges whose arrays cannot all
+//     be aligned together fall back to the scalar (V = 1) instantiation.
+// FP expressions are compiled with -ffp-contract=off so x + y*s0 rounds
+// exactly like the host functor in stream.cpp:257 (bit-exact parity).
+#include "internal.hpp"
+
+using namespace hpxhip;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;
+
+// Geometry: vector part of [0, nvec) processed grid-stride, each thread
+// handling vectors i, i+S, ..., i+(U-1)S per iteration (coalesced per
+// instruction: a wave touches 64 consecutive 16-B vectors).
+struct span3 {
+    uint64_t head;  // scalar elements before the vector part
+    uint64_t nvec;  // vectors of V elements
+    uint64_t tail;  // scalar elements after the vector part
+};
+
+inline unsigned grid_for(uint64_t work_items) {
+    const uint64_t per_block = static_cast<uint64_t>(kThreads) * kUnroll;
+    uint64_t blocks = (work_items + per_block - 1) / per_block;
+    const uint64_t cap = static_cast<uint64_t>(current_device_info().cus) * 8;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) blocks = 1;
+    return static_cast<unsigned>(blocks);
+}
+
+// out[i] = (TO) f((C) in[i])
+template <typename TI, typename C, typename TO, typename F, int V>
+__global__ __launch_bounds__(kThreads) void k_unary(const TI* in, TO* out, span3 sp, F f) {
+    using VI = vec<TI, V>;
+    using VO = vec<TO, V>;
+    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+
+    // Head and tail: scalar, first threads of the grid.
+    if (tid < sp.head) out[tid] = static_cast<TO>(f(static_cast<C>(in[tid])));
+    const uint64_t tail0 = sp.head + sp.nvec * V;
+    if (tid < sp.tail) out[tail0 + tid] = static_cast<TO>(f(static_cast<C>(in[tail0 + tid])));
+
+    const VI* vin = reinterpret_cast<const VI*>(in + sp.head);
+    VO* vout = reinterpret_cast<VO*>(out + sp.head);
+    for (uint64_t i = tid; i < sp.nvec; i += stride * kUnroll) {
+        VI x[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint64_t j = i + u * stride;
+            if (j < sp.nvec) x[u] = vin[j];
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint64_t j = i + u * stride;
+            if (j < sp.nvec) {
+                VO y;
+#pragma unroll
+                for (int e = 0; e < V; ++e) y.v[e] = static_cast<TO>(f(static_cast<C>(x[u].v[e])));
+                vout[j] = y;
+            }
+        }
+    }
+}
+
+// out[i] = (TO) f((C) a[i], (C) b[i])
+template <typename TI, typename C, typename TO, typename F, int V>
+__global__ __launch_bounds__(kThreads) void k_binary(const TI* a, const TI* b, TO* out, span3 sp, F f) {
+    using VI = vec<TI, V>;
+    using VO = vec<TO, V>;
+    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+
+    if (tid < sp.head) out[tid] = static_cast<TO>(f(static_cast<C>(a[tid]), static_cast<C>(b[tid])));
+    const uint64_t tail0 = sp.head + sp.nvec * V;
+    if (tid < sp.tail)
+        out[tail0 + tid] = static_cast<TO>(f(static_cast<C>(a[tail0 + tid]), static_cast<C>(b[tail0 + tid])));
+
+    const VI* va = reinterpret_cast<const VI*>(a + sp.head);
+    const VI* vb = reinterpret_cast<const VI*>(b + sp.head);
+    VO* vout = reinterpret_cast<VO*>(out + sp.head);
+    for (uint64_t i = tid; i < sp.nvec; i += stride * kUnroll) {
+        VI x[kUnroll], y[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint64_t j = i + u * stride;
+            if (j < sp.nvec) {
+                x[u] = va[j];
+                y[u] = vb[j];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint64_t j = i + u * stride;
+            if (j < sp.nvec) {
+                VO z;
+#pragma unroll
+                for (int e = 0; e < V; ++e)
+                    z.v[e] = static_cast<TO>(f(static_cast<C>(x[u].v[e]), static_cast<C>(y[u].v[e])));
+                vout[j] = z;
+            }
+        }
+    }
+}
+
+// data[i] = value
+template <typename T, int V>
+__global__ __launch_bounds__(kThreads) void k_fill(T* out, span3 sp, T value) {
+    using VT = vec<T, V>;
+    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+    if (tid < sp.head) out[tid] = value;
+    const uint64_t tail0 = sp.head + sp.nvec * V;
+    if (tid < sp.tail) out[tail0 + tid] = value;
+    VT y;
+#pragma unroll
+    for (int e = 0; e < V; ++e) y.v[e] = value;
+    VT* vout = reinterpret_cast<VT*>(out + sp.head);
+    for (uint64_t i = tid; i < sp.nvec; i += stride) vout[i] = y;
+}
+
+// Split [0, n) into head/vector/tail for the given pointers (all must share
+// the same misalignment); returns false if they cannot be vectorised together.
+template <int V>
+bool make_span(uint64_t n, size_t esize, span3* sp, std::initializer_list<const void*> ptrs) {
+    uint64_t head = UINT64_MAX;
+    bool first = true;
+    for (const void* p : ptrs) {
+        uint64_t h = head_to_align16(p, esize);
+        if (h == UINT64_MAX) return false;
+        if (first) {
+            head = h;
+            first = false;
+        } else if (h != head) {
+            return false;
+        }
+    }
+    if (head > n) head = n;
+    sp->head = head;
+    sp->nvec = (n - head) / V;
+    sp->tail = n - head - sp->nvec * V;
+    return true;
+}
+
+template <typename TI, typename C, typename TO, typename F>
+int launch_unary(const TI* in, TO* out, uint64_t n, F f, hipStream_t s) {
+    constexpr int VW = 16 / (sizeof(TI) > sizeof(TO) ? sizeof(TI) : sizeof(TO));
+    constexpr int V = VW < 1 ? 1 : VW;
+    span3 sp;
+    if ((sizeof(TI) == sizeof(TO)) && make_span<V>(n, sizeof(TI), &sp, {in, out})) {
+        hipLaunchKernelGGL((k_unary<TI, C, TO, F, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail)),
+                           dim3(kThreads), 0, s, in, out, sp, f);
+    } else {
+        sp = span3{0, n, 0};
+        hipLaunchKernelGGL((k_unary<TI, C, TO, F, 1>), dim3(grid_for(n)), dim3(kThreads), 0, s, in, out, sp, f);
+    }
+    HPXHIP_CHECK_LAUNCH();
+    return 0;
+}
+
+template <typename TI, typename C, typename TO, typename F>
+int launch_binary(const TI* a, const TI* b, TO* out, uint64_t n, F f, hipStream_t s) {
+    constexpr int VW = 16 / (sizeof(TI) > sizeof(TO) ? sizeof(TI) : sizeof(TO));
+    constexpr int V = VW < 1 ? 1 : VW;
+    span3 sp;
+    if ((sizeof(TI) == sizeof(TO)) && make_span<V>(n, sizeof(TI), &sp, {a, b, out})) {
+        hipLaunchKernelGGL((k_binary<TI, C, TO, F, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail)),
+                           dim3(kThreads), 0, s, a, b, out, sp, f);
+    } else {
+        sp = span3{0, n, 0};
+        hipLaunchKernelGGL((k_binary<TI, C, TO, F, 1>), dim3(grid_for(n)), dim3(kThreads), 0, s, a, b, out,
+                           sp, f);
+    }
+    HPXHIP_CHECK_LAUNCH();
+    return 0;
+}
+
+// (in, compute, out) combinations that are built: compute == in or F64;
+// out == in or == compute.
+template <typename TI, typename F>
+int with_compute_out(int compute_dt, int out_dt, F&& f) {
+    return with_wide_dtype<TI>(compute_dt, [&](auto ct) -> int {
+        using C = typename decltype(ct)::type;
+        if (out_dt == dtype_of<TI>()) return f(ct, tag<TI>{});
+        if (out_dt == dtype_of<C>()) return f(ct, tag<C>{});
+        return HPXHIP_ERROR_UNSUPPORTED;
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+int hpxhip_fill(int dtype, const void* value, void* data, uint64_t n, hpxhip_stream stream) {
+    if (n == 0) return 0;
+    if (!value || !data) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    return with_dtype(dtype, [&](auto t) -> int {
+        using T = typename decltype(t)::type;
+        constexpr int V = 16 / sizeof(T);
+        T v;
+        __builtin_memcpy(&v, value, sizeof(T));
+        span3 sp;
+        if (!make_span<V>(n, sizeof(T), &sp, {data})) {
+            sp = span3{0, n, 0};
+            hipLaunchKernelGGL((k_fill<T, 1>), dim3(grid_for(n)), dim3(kThreads), 0, s, static_cast<T*>(data), sp, v);
+        } else {
+            hipLaunchKernelGGL((k_fill<T, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail)), dim3(kThreads), 0, s,
+                               static_cast<T*>(data), sp, v);
+        }
+        HPXHIP_CHECK_LAUNCH();
+        return 0;
+    });
+}
+
+int hpxhip_copy(int dtype, const void* in, void* out, uint64_t n, hpxhip_stream stream) {
+    if (n == 0) return 0;
+    if (!in || !out) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    return with_dtype(dtype, [&](auto t) -> int {
+        using T = typename decltype(t)::type;
+        return launch_unary<T, T, T>(static_cast<const T*>(in), static_cast<T*>(out), n,
+                                     unary_fn<HPXHIP_U_IDENTITY, T>{T(0), T(0)}, s);
+    });
+}
+
+int hpxhip_for_each(int dtype, int unary_kind, const void* scalars, void* data, uint64_t n,
+                    hpxhip_stream stream) {
+    if (n == 0) return 0;
+    if (!data) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    return with_dtype(dtype, [&](auto t) -> int {
+        using T = typename decltype(t)::type;
+        return with_unary<T>(unary_kind, scalars, [&](auto f) -> int {
+            return launch_unary<T, T, T>(static_cast<const T*>(data), static_cast<T*>(data), n, f, s);
+        });
+    });
+}
+
+int hpxhip_transform(int in_dtype, int compute_dtype, int out_dtype, int unary_kind, const void* scalars,
+                     const void* in, void* out, uint64_t n, hpxhip_stream stream) {
+    if (n == 0) return 0;
+    if (!in || !out) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    return with_dtype(in_dtype, [&](auto ti) -> int {
+        using TI = typename decltype(ti)::type;
+        return with_compute_out<TI>(compute_dtype, out_dtype, [&](auto ct, auto ot) -> int {
+            using C = typename decltype(ct)::type;
+            using TO = typename decltype(ot)::type;
+            return with_unary<C>(unary_kind, scalars, [&](auto f) -> int {
+                return launch_unary<TI, C, TO>(static_cast<const TI*>(in), static_cast<TO*>(out), n, f, s);
+            });
+        });
+    });
+}
+
+int hpxhip_transform_binary(int in_dtype, int compute_dtype, int out_dtype, int binary_kind,
+                            const void* scalars, const void* in1, const void* in2, void* out, uint64_t n,
+                            hpxhip_stream stream) {
+    if (n == 0) return 0;
+    if (!in1 || !in2 || !out) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    return with_dtype(in_dtype, [&](auto ti) -> int {
+        using TI = typename decltype(ti)::type;
+        return with_compute_out<TI>(compute_dtype, out_dtype, [&](auto ct, auto ot) -> int {
+            using C = typename decltype(ct)::type;
+            using TO = typename decltype(ot)::type;
+            return with_binary<C>(binary_kind, scalars, [&](auto f) -> int {
+                return launch_binary<TI, C, TO>(static_cast<const TI*>(in1), static_cast<const TI*>(in2),
+                                                static_cast<TO*>(out), n, f, s);
+            });
+        });
+    });
+}
+
+}  // extern "C"
