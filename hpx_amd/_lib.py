@@ -25,6 +25,7 @@ U_IDENTITY, U_SCALE, U_ADD_SCALAR, U_AFFINE, U_NEGATE, U_ABS, U_SQUARE = range(7
 B_ADD, B_TRIAD, B_SUB, B_MUL, B_AXPY, B_MIN, B_MAX = range(7)
 P_LT, P_LE, P_GT, P_GE, P_EQ, P_NE, P_NOT_LT, P_BITS = range(8)
 H2H, H2D, D2H, D2D, DEFAULT = range(5)
+GEN_IOTA, GEN_BITS, GEN_RANGE, GEN_UNIT = range(4)
 ALGO_REDUCE, ALGO_SCAN, ALGO_COPY_IF, ALGO_SORT, ALGO_SORT_BY_KEY = range(5)
 
 SUCCESS = 0
@@ -111,6 +112,7 @@ SIGNATURES = {
     "hpxhip_memcpy_peer_async": [_vp, _i, _vp, _i, _sz, _vp],
     "hpxhip_memset_async": [_vp, _i, _sz, _vp],
     "hpxhip_scratch_bytes": [_i, _i, _i, _u64, ctypes.POINTER(_sz)],
+    "hpxhip_generate": [_i, _i, _u64, ctypes.c_int64, ctypes.c_int64, _vp, _u64, _vp],
     "hpxhip_fill": [_i, _vp, _vp, _u64, _vp],
     "hpxhip_copy": [_i, _vp, _vp, _u64, _vp],
     "hpxhip_for_each": [_i, _i, _vp, _vp, _u64, _vp],

@@ -1,0 +1,372 @@
+"""hpx::parallel algorithms over hip device iterators.
+
+Each function keeps the reference's name, argument order and return
+convention (value for ``seq``/``par``, ``future`` for ``par(task)``) and
+calls one whole-algorithm entry point of the C ABI (include/hpxhip.h):
+
+  for_each / for_each_n      hpx/parallel/algorithms/for_each.hpp:369-552
+  fill / fill_n              fill.hpp:86,159
+  copy / copy_n              copy.hpp:88-114,209 (+ util/transfer.hpp for
+                             host<->device ranges, cuda/transfer.hpp:188-348)
+  copy_if                    copy.hpp:401-494,585
+  transform (1, 2, 2')       transform.hpp:138-182,411-461,643-694,304/625/862
+  reduce                     reduce.hpp:200/271/344
+  transform_reduce           transform_reduce.hpp:254; binary: transform_reduce_binary.hpp:323/432
+  inclusive_scan             inclusive_scan.hpp:288/320/409/511/591
+  exclusive_scan             exclusive_scan.hpp:292/374
+  transform_inclusive_scan   transform_inclusive_scan.hpp:320/445
+  transform_exclusive_scan   transform_exclusive_scan.hpp:317
+  sort / sort_by_key         sort.hpp:364, sort_by_key.hpp:42-78
+  generate (splitmix/iota)   generate.hpp (device generator functors)
+
+A policy must be rebound to a hip executor (``par.on(hip_exec)``) or all
+iterators must be device iterators of one target (then that target's
+stream is used).  There is no host fallback: host ranges are only accepted
+as the source/destination of ``copy`` (a transfer).
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _lib as L
+from . import functional as F
+from .compute import (default_executor, dtype_code, iterator, np_dtype, target)
+from .execution import policy as _policy
+from .future import future, make_ready_future
+
+
+# ------------------------------------------------------------------ helpers
+class _slots:
+    """Per-target ring of small device result slots + pinned host mirrors."""
+    N = 256
+
+    def __init__(self, tgt: target):
+        self.dev = ctypes.c_void_p()
+        L.call("hpxhip_malloc", tgt.device, ctypes.byref(self.dev), 16 * self.N)
+        self.host = ctypes.c_void_p()
+        L.call("hpxhip_malloc_host", ctypes.byref(self.host), 16 * self.N)
+        self.i = 0
+        self.lock = threading.Lock()
+
+    def next(self):
+        with self.lock:
+            self.i = (self.i + 1) % self.N
+            return self.dev.value + 16 * self.i, self.host.value + 16 * self.i
+
+
+_slot_lock = threading.Lock()
+
+
+def _slots_for(tgt: target) -> _slots:
+    s = getattr(tgt, "_hpx_slots", None)
+    if s is None:
+        with _slot_lock:
+            s = getattr(tgt, "_hpx_slots", None)
+            if s is None:
+                s = _slots(tgt)
+                tgt._hpx_slots = s
+    return s
+
+
+def _read_host(addr: int, dtype: int):
+    return np.frombuffer((ctypes.c_char * 8).from_address(addr), dtype=np_dtype(dtype), count=1)[0].item()
+
+
+def _exec_of(pol) -> tuple:
+    if not isinstance(pol, _policy):
+        raise TypeError(f"first argument must be an execution policy, got {pol!r}")
+    return pol.executor
+
+
+def _context(pol, *iters):
+    """-> (stream, target, is_task) for a policy and its device iterators."""
+    ex = _exec_of(pol)
+    devs = [it for it in iters if isinstance(it, iterator)]
+    if ex is not None:
+        if not isinstance(ex, default_executor):
+            raise TypeError(f"hpx_amd algorithms run on hip executors, got {type(ex).__name__}")
+        tgt = ex.target()
+        stream = ex.stream_for_call()
+    else:
+        if not devs:
+            raise TypeError("policy has no hip executor and no device iterators: host algorithms "
+                            "are HPX's own, hpx_amd provides the hip executor path")
+        tgt = devs[0].target()
+        stream = tgt.stream
+    for it in devs:
+        if it.target().device != tgt.device:
+            raise ValueError(f"iterator on device {it.target().device} used with target on device {tgt.device}")
+    return stream, tgt, pol.is_task
+
+
+def _check_range(first, last):
+    if not isinstance(first, iterator) or not isinstance(last, iterator):
+        raise TypeError("expected device iterators (hpx_amd.compute.iterator)")
+    n = last - first
+    if n < 0:
+        raise ValueError("last precedes first")
+    return n
+
+
+def _finish(is_task, stream, tgt, value_thunk):
+    """Return the algorithm result: a value (sync) or a future (task)."""
+    if is_task:
+        return future.on_stream(stream, thunk=value_thunk)
+    L.call("hpxhip_stream_synchronize", stream)
+    from .compute import device_error_check
+    device_error_check(tgt.device)
+    return value_thunk()
+
+
+def _vp(addr):
+    return ctypes.c_void_p(addr)
+
+
+def _fill_raw(stream, dtype, addr, n, value):
+    buf = L.scalar_buf(dtype, value)
+    L.call("hpxhip_fill", dtype, buf, _vp(addr), n, stream)
+
+
+def _acc_dtype(elem: int, init) -> int:
+    """HPX's T is the init's type: float init over integers -> double."""
+    if isinstance(init, np.generic):
+        return dtype_code(init.dtype)
+    if isinstance(init, float) and elem not in (L.F32, L.F64):
+        return L.F64
+    return elem
+
+
+def _compute_dtype(elem: int, fn) -> int:
+    c = getattr(fn, "compute", None)
+    return dtype_code(c) if c else elem
+
+
+# ------------------------------------------------------------- for_each etc
+def generate(pol, first, last, kind: str = "splitmix", seed: int = 0x5EED, lo: int = 0, hi: int = 0):
+    """hpx::parallel::generate with a counter-based generator functor:
+    kind = 'iota' (lo + i), 'bits', 'range' ([lo, hi]) or 'unit' ([0,1))."""
+    kinds = {"iota": L.GEN_IOTA, "bits": L.GEN_BITS, "splitmix": L.GEN_BITS, "range": L.GEN_RANGE,
+             "unit": L.GEN_UNIT}
+    n = _check_range(first, last)
+    stream, tgt, is_task = _context(pol, first)
+    L.call("hpxhip_generate", first.dtype, kinds[kind], seed, lo, hi, _vp(first.address), n, stream)
+    return _finish(is_task, stream, tgt, lambda: last)
+
+
+def fill(pol, first, last, value):
+    n = _check_range(first, last)
+    stream, tgt, is_task = _context(pol, first)
+    _fill_raw(stream, first.dtype, first.address, n, value)
+    return _finish(is_task, stream, tgt, lambda: None)
+
+
+def fill_n(pol, first, count, value):
+    return fill(pol, first, first + count, value) if count > 0 else _finish(
+        pol.is_task, *_context(pol, first)[:2], lambda: first)
+
+
+def for_each(pol, first, last, f):
+    """for_each.hpp:540: applies f in place; returns last (future for task)."""
+    f = F.require(f, F.Unary, "for_each")
+    n = _check_range(first, last)
+    stream, tgt, is_task = _context(pol, first)
+    sc = L.scalars_buf(first.dtype, f.scalars)
+    L.call("hpxhip_for_each", first.dtype, f.kind, sc, _vp(first.address), n, stream)
+    return _finish(is_task, stream, tgt, lambda: last)
+
+
+def for_each_n(pol, first, count, f):
+    return for_each(pol, first, first + max(0, count), f)
+
+
+# ---------------------------------------------------------------- copy etc
+def copy(pol, first, last, dest):
+    """copy.hpp:209.  Device->device runs the copy kernel; device<->host
+    ranges (numpy arrays) are transfers (util/transfer.hpp -> memcpy)."""
+    if isinstance(first, np.ndarray) and isinstance(dest, iterator):
+        arr = np.ascontiguousarray(first if last is None else first[:last])
+        stream, tgt, is_task = _context(pol, dest)
+        if np_dtype(dest.dtype) != arr.dtype:
+            raise TypeError("host/device dtype mismatch")
+        L.call("hpxhip_memcpy_async", _vp(dest.address), arr.ctypes.data_as(ctypes.c_void_p), arr.nbytes,
+               L.H2D, stream)
+        keep = arr  # noqa: F841 (alive until synchronised)
+        end = dest + arr.size
+        return _finish(is_task, stream, tgt, lambda: (keep, end)[1])
+    n = _check_range(first, last)
+    if isinstance(dest, np.ndarray):
+        stream, tgt, is_task = _context(pol, first)
+        if dest.size < n or not dest.flags.c_contiguous or np_dtype(first.dtype) != dest.dtype:
+            raise TypeError("destination array too small, non-contiguous or of another dtype")
+        L.call("hpxhip_memcpy_async", dest.ctypes.data_as(ctypes.c_void_p), _vp(first.address),
+               n * first.vec.value_size, L.D2H, stream)
+        return _finish(is_task, stream, tgt, lambda: dest)
+    stream, tgt, is_task = _context(pol, first, dest)
+    if first.dtype != dest.dtype:
+        return transform(pol, first, last, dest, F.identity())
+    L.call("hpxhip_copy", first.dtype, _vp(first.address), _vp(dest.address), n, stream)
+    return _finish(is_task, stream, tgt, lambda: (last, dest + n))
+
+
+def copy_n(pol, first, count, dest):
+    return copy(pol, first, first + count, dest)
+
+
+def copy_if(pol, first, last, dest, pred):
+    """copy.hpp:585: stable compaction; returns (last, dest_end)."""
+    pred = F.require(pred, F.Predicate, "copy_if")
+    n = _check_range(first, last)
+    stream, tgt, is_task = _context(pol, first, dest)
+    if first.dtype != dest.dtype:
+        raise TypeError("copy_if: source and destination dtypes differ")
+    dev, host = _slots_for(tgt).next()
+    arg = L.scalar_buf(first.dtype, pred.arg)
+    L.call("hpxhip_copy_if", first.dtype, pred.kind, arg, _vp(first.address), _vp(dest.address), n,
+           _vp(dev), stream, None, 0)
+    L.call("hpxhip_memcpy_async", _vp(host), _vp(dev), 8, L.D2H, stream)
+    return _finish(is_task, stream, tgt, lambda: (last, dest + _read_host(host, L.U64)))
+
+
+# --------------------------------------------------------------- transform
+def transform(pol, *args):
+    """transform.hpp overloads:
+         (first, last, dest, f)                    unary      (304)
+         (first1, last1, first2, dest, f)          binary     (625)
+         (first1, last1, first2, last2, dest, f)   binary2    (862; min length)
+    Returns (in_last, out_last) like the reference's tagged pair."""
+    if len(args) == 4:
+        first, last, dest, f = args
+        f = F.require(f, F.Unary, "transform")
+        n = _check_range(first, last)
+        stream, tgt, is_task = _context(pol, first, dest)
+        cdt = _compute_dtype(first.dtype, f)
+        sc = L.scalars_buf(cdt, f.scalars)
+        L.call("hpxhip_transform", first.dtype, cdt, dest.dtype, f.kind, sc, _vp(first.address),
+               _vp(dest.address), n, stream)
+        return _finish(is_task, stream, tgt, lambda: (last, dest + n))
+    if len(args) == 5:
+        first1, last1, first2, dest, f = args
+        n = _check_range(first1, last1)
+    elif len(args) == 6:
+        first1, last1, first2, last2, dest, f = args
+        n = min(_check_range(first1, last1), _check_range(first2, last2))  # transform.hpp:683-685
+    else:
+        raise TypeError("transform: unsupported overload")
+    f = F.require(f, F.Binary, "transform")
+    stream, tgt, is_task = _context(pol, first1, first2, dest)
+    if first1.dtype != first2.dtype:
+        raise TypeError("transform: both input ranges must have the same dtype")
+    cdt = _compute_dtype(first1.dtype, f)
+    sc = L.scalars_buf(cdt, f.scalars)
+    L.call("hpxhip_transform_binary", first1.dtype, cdt, dest.dtype, f.kind, sc, _vp(first1.address),
+           _vp(first2.address), _vp(dest.address), n, stream)
+    return _finish(is_task, stream, tgt, lambda: (first1 + n, first2 + n, dest + n))
+
+
+# -------------------------------------------------------------- reductions
+def reduce(pol, first, last, init=None, op=F.plus):
+    """reduce.hpp:200/271/344: init defaults to T(), op to std::plus."""
+    return transform_reduce(pol, first, last, 0 if init is None else init, op, F.identity())
+
+
+def transform_reduce(pol, *args):
+    """transform_reduce.hpp:254 (first, last, init, red_op, conv_op) and
+    transform_reduce_binary.hpp:323/432 (first1, last1, first2, init[, red_op, conv_op])."""
+    if len(args) >= 4 and isinstance(args[2], iterator):
+        first1, last1, first2, init = args[:4]
+        red = args[4] if len(args) > 4 else F.plus
+        conv = args[5] if len(args) > 5 else F.multiply()
+        red = F.require(red, F.BinaryOp, "transform_reduce")
+        conv = F.require(conv, F.Binary, "transform_reduce")
+        n = _check_range(first1, last1)
+        stream, tgt, is_task = _context(pol, first1, first2)
+        adt = _acc_dtype(first1.dtype, init)
+        dev, host = _slots_for(tgt).next()
+        L.call("hpxhip_transform_reduce_binary", first1.dtype, adt, red.kind, conv.kind,
+               L.scalars_buf(adt, conv.scalars), L.scalar_buf(adt, init), _vp(first1.address),
+               _vp(first2.address), n, _vp(dev), stream, None, 0)
+    else:
+        first, last, init, red, conv = args
+        red = F.require(red, F.BinaryOp, "transform_reduce")
+        conv = F.require(conv, F.Unary, "transform_reduce")
+        n = _check_range(first, last)
+        stream, tgt, is_task = _context(pol, first)
+        adt = _acc_dtype(first.dtype, init)
+        dev, host = _slots_for(tgt).next()
+        L.call("hpxhip_transform_reduce", first.dtype, adt, red.kind, conv.kind,
+               L.scalars_buf(adt, conv.scalars), L.scalar_buf(adt, init), _vp(first.address), n,
+               _vp(dev), stream, None, 0)
+    L.call("hpxhip_memcpy_async", _vp(host), _vp(dev), 8, L.D2H, stream)
+    return _finish(is_task, stream, tgt, lambda: _read_host(host, adt))
+
+
+# -------------------------------------------------------------------- scans
+def _scan(pol, first, last, dest, op, init, inclusive, conv, prefix_dev=None):
+    op = F.require(op, F.BinaryOp, "scan")
+    conv = F.require(conv, F.Unary, "scan")
+    n = _check_range(first, last)
+    stream, tgt, is_task = _context(pol, first, dest)
+    if first.dtype != dest.dtype:
+        raise TypeError("scan: source and destination dtypes differ")
+    dt = first.dtype
+    L.call("hpxhip_scan", dt, op.kind, 1 if inclusive else 0, conv.kind, L.scalars_buf(dt, conv.scalars),
+           L.scalar_buf(dt, init), None if prefix_dev is None else _vp(prefix_dev), _vp(first.address),
+           _vp(dest.address), n, stream, None, 0)
+    return _finish(is_task, stream, tgt, lambda: dest + n)
+
+
+def inclusive_scan(pol, first, last, dest, *args):
+    """Overloads (op, init) 288, (init, op) 320, (init) 409, (op) 511, () 591.
+    Without init the reference uses value_type() (inclusive_scan.hpp:526,606)."""
+    op, init = F.plus, 0
+    if len(args) == 2:
+        if isinstance(args[0], F.BinaryOp):
+            op, init = args
+        else:
+            init, op = args
+    elif len(args) == 1:
+        if isinstance(args[0], F.BinaryOp):
+            op = args[0]
+        else:
+            init = args[0]
+    elif args:
+        raise TypeError("inclusive_scan: unsupported overload")
+    return _scan(pol, first, last, dest, op, init, True, F.identity())
+
+
+def exclusive_scan(pol, first, last, dest, init, op=F.plus):
+    """exclusive_scan.hpp:292 (init, op) / 374 (init)."""
+    return _scan(pol, first, last, dest, op, init, False, F.identity())
+
+
+def transform_inclusive_scan(pol, first, last, dest, op, conv, init=0):
+    """transform_inclusive_scan.hpp:320 (op, conv, init) / 445 (op, conv)."""
+    return _scan(pol, first, last, dest, op, init, True, conv)
+
+
+def transform_exclusive_scan(pol, first, last, dest, init, op, conv):
+    """transform_exclusive_scan.hpp:317 (init, op, conv)."""
+    return _scan(pol, first, last, dest, op, init, False, conv)
+
+
+# --------------------------------------------------------------------- sort
+def sort(pol, first, last, comp=F.less):
+    """sort.hpp:364; comp = std::less (default) or std::greater."""
+    comp = F.require(comp, F.Compare, "sort")
+    n = _check_range(first, last)
+    stream, tgt, is_task = _context(pol, first)
+    L.call("hpxhip_sort", first.dtype, _vp(first.address), n, 1 if comp.descending else 0, stream, None, 0)
+    return _finish(is_task, stream, tgt, lambda: last)
+
+
+def sort_by_key(pol, key_first, key_last, value_first, comp=F.less):
+    """sort_by_key.hpp:42-78 (stable here); returns (key_last, value_last)."""
+    comp = F.require(comp, F.Compare, "sort_by_key")
+    n = _check_range(key_first, key_last)
+    stream, tgt, is_task = _context(pol, key_first, value_first)
+    L.call("hpxhip_sort_by_key", key_first.dtype, value_first.dtype, _vp(key_first.address),
+           _vp(value_first.address), n, 1 if comp.descending else 0, stream, None, 0)
+    return _finish(is_task, stream, tgt, lambda: (key_last, value_first + n))

@@ -17,130 +17,13 @@
 // from the sequential left fold (tolerance in DESIGN.md).
 #include "internal.hpp"
 #include "lookback.hpp"
+#include "scan_kernel.hpp"
 
 using namespace hpxhip;
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / kWave;
-constexpr int kRounds = 8;
-
-template <typename T>
-constexpr uint64_t tile_elems() {
-    return static_cast<uint64_t>(kThreads) * kRounds * (16 / sizeof(T));
-}
-
-template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED>
-__global__ __launch_bounds__(kThreads) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init,
-                                                    const T* prefix_dev, uint32_t* counter, tile_state<T> st) {
-    constexpr int V = 16 / sizeof(T);
-    constexpr uint64_t TILE = tile_elems<T>();
-    constexpr uint64_t WAVE_ELEMS = TILE / kWaves;
-    using VT = vec<T, V>;
-
-    __shared__ uint32_t s_tile;
-    __shared__ T s_wave_total[kWaves];
-    __shared__ T s_prefix;
-
-    if (threadIdx.x == 0)
-        s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint64_t tile = s_tile;
-    const int wave = threadIdx.x / kWave;
-    const int lane = lane_id();
-    const T id = Op::template identity<T>();
-
-    const uint64_t tile_base = tile * TILE;
-    const uint64_t wbase = tile_base + wave * WAVE_ELEMS;
-    const bool full = tile_base + TILE <= n;
-
-    // ---- load (all rounds in flight) and convert
-    VT x[kRounds];
-    if (ALIGNED && full) {
-        const VT* src = reinterpret_cast<const VT*>(in + wbase);
-#pragma unroll
-        for (int r = 0; r < kRounds; ++r) x[r] = src[r * kWave + lane];
-#pragma unroll
-        for (int r = 0; r < kRounds; ++r)
-#pragma unroll
-            for (int e = 0; e < V; ++e) x[r].v[e] = conv(x[r].v[e]);
-    } else {
-#pragma unroll
-        for (int r = 0; r < kRounds; ++r)
-#pragma unroll
-            for (int e = 0; e < V; ++e) {
-                const uint64_t i = wbase + (static_cast<uint64_t>(r) * kWave + lane) * V + e;
-                x[r].v[e] = i < n ? conv(in[i]) : id;
-            }
-    }
-
-    // ---- per-round lane scan + wave scan; x becomes the wave-local result
-    T carry = id;
-#pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-        T local[V];
-        T run = id;
-#pragma unroll
-        for (int e = 0; e < V; ++e) {
-            const T nxt = op(run, x[r].v[e]);
-            local[e] = INCL ? nxt : run;
-            run = nxt;
-        }
-        const T incl = wave_inclusive_scan(run, op);
-        const T excl = wave_shift_right<T, Op>(incl);
-        const T pre = op(carry, excl);
-#pragma unroll
-        for (int e = 0; e < V; ++e) x[r].v[e] = op(pre, local[e]);
-        carry = op(carry, readlane(incl, kWave - 1));
-    }
-    if (lane == 0) s_wave_total[wave] = carry;
-    __syncthreads();
-
-    T wave_prefix = id;
-    T agg = id;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-        if (w < wave) wave_prefix = op(wave_prefix, s_wave_total[w]);
-        agg = op(agg, s_wave_total[w]);
-    }
-
-    // ---- decoupled look-back (wave 0)
-    if (wave == 0) {
-        T p;
-        if (tile == 0) {
-            p = prefix_dev ? *prefix_dev : init;
-            if (lane == 0) st.publish(0, op(p, agg), TILE_INCLUSIVE);
-        } else {
-            if (lane == 0) st.publish(tile, agg, TILE_AGGREGATE);
-            p = st.exclusive_prefix(tile, op);
-            if (lane == 0) st.publish(tile, op(p, agg), TILE_INCLUSIVE);
-        }
-        if (lane == 0) s_prefix = p;
-    }
-    __syncthreads();
-    const T pre = op(s_prefix, wave_prefix);
-
-    // ---- store
-    if (ALIGNED && full) {
-        VT* dst = reinterpret_cast<VT*>(out + wbase);
-#pragma unroll
-        for (int r = 0; r < kRounds; ++r) {
-            VT y;
-#pragma unroll
-            for (int e = 0; e < V; ++e) y.v[e] = op(pre, x[r].v[e]);
-            dst[r * kWave + lane] = y;
-        }
-    } else {
-#pragma unroll
-        for (int r = 0; r < kRounds; ++r)
-#pragma unroll
-            for (int e = 0; e < V; ++e) {
-                const uint64_t i = wbase + (static_cast<uint64_t>(r) * kWave + lane) * V + e;
-                if (i < n) out[i] = op(pre, x[r].v[e]);
-            }
-    }
-}
+using namespace hpxhip::scan_detail;
 
 template <typename T>
 struct scan_layout {

@@ -206,6 +206,16 @@ int hpxhip_scratch_bytes(int algo, int dtype, int aux_dtype, uint64_t n, size_t*
 /* ------------------------------------------------ elementwise (for_each) */
 /* fill.hpp:86: data[i] = *value (value: host pointer to one dtype element). */
 int hpxhip_fill(int dtype, const void* value, void* data, uint64_t n, hpxhip_stream stream);
+/* generate.hpp (hpx::parallel::generate / iota-style initialisation of the
+   reference tests, e.g. std::iota in transform_reduce.cpp:29):
+     GEN_IOTA : data[i] = lo + i
+     GEN_BITS : data[i] = bits of splitmix64(seed ^ i) (upper 32 bits for 4-byte types)
+     GEN_RANGE: data[i] = lo + splitmix64(seed ^ i) % (hi - lo + 1)   (integers)
+     GEN_UNIT : data[i] = (splitmix64(seed ^ i) >> 11) * 2^-53 in [0,1)
+                (float: >> 40, * 2^-24)                                  */
+enum hpxhip_gen { HPXHIP_GEN_IOTA = 0, HPXHIP_GEN_BITS = 1, HPXHIP_GEN_RANGE = 2, HPXHIP_GEN_UNIT = 3 };
+int hpxhip_generate(int dtype, int kind, uint64_t seed, int64_t lo, int64_t hi, void* data, uint64_t n,
+                    hpxhip_stream stream);
 /* copy.hpp:88-114: out[i] = in[i]. */
 int hpxhip_copy(int dtype, const void* in, void* out, uint64_t n, hpxhip_stream stream);
 /* for_each.hpp:369: data[i] = f(data[i]) in place (for_each_compute.cu `i += 5`). */

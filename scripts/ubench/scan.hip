@@ -1,0 +1,57 @@
+// Microbenchmark: the shipped scan kernel (scan_kernel.hpp) at several tile
+// shapes, with and without the look-back (ablation), 2^30 int64.
+#include "../../hpx_amd/csrc/scan_kernel.hpp"
+#include "../../hpx_amd/csrc/internal.hpp"
+#include <cstdio>
+#include <vector>
+#include <algorithm>
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+using namespace hpxhip;
+using namespace hpxhip::scan_detail;
+using T = int64_t;
+using Conv = unary_fn<HPXHIP_U_IDENTITY, T>;
+
+int main() {
+  const uint64_t N = 1ull << 30;
+  T *in, *out; char* ws; uint32_t* err;
+  CK(hipMalloc(&in, N * 8)); CK(hipMalloc(&out, N * 8)); CK(hipMalloc(&ws, 64 << 20)); CK(hipMalloc(&err, 64));
+  CK(hipMemset(in, 1, N * 8)); CK(hipMemset(err, 0, 64));
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  auto run = [&](const char* name, auto launch) {
+    launch(); CK(hipDeviceSynchronize());
+    std::vector<float> t;
+    for (int r = 0; r < 15; ++r) { CK(hipEventRecord(e0)); launch(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1)); t.push_back(ms); }
+    std::sort(t.begin(), t.end());
+    const double B = 16.0 * N;
+    printf("%-34s min %7.3f ms med %7.3f ms  %7.1f GB/s (med %7.1f)\n", name, t[0], t[7], B / t[0] / 1e6, B / t[7] / 1e6);
+  };
+  auto variant = [&](auto rounds_c, auto threads_c, auto lb_c, const char* name) {
+    constexpr int R = decltype(rounds_c)::value;
+    constexpr int TH = decltype(threads_c)::value;
+    constexpr bool LB = decltype(lb_c)::value;
+    const uint64_t tile = tile_elems<T, R, TH>();
+    const uint64_t ntiles = (N + tile - 1) / tile;
+    const size_t flags_off = 256, agg_off = align_up(flags_off + ntiles * 4, 256);
+    const size_t incl_off = align_up(agg_off + ntiles * 8, 256);
+    tile_state<T> st{reinterpret_cast<uint32_t*>(ws + flags_off), reinterpret_cast<T*>(ws + agg_off),
+                     reinterpret_cast<T*>(ws + incl_off), err};
+    run(name, [&] {
+      CK(hipMemsetAsync(ws, 0, agg_off, 0));
+      k_scan<T, Conv, op_plus, true, true, R, TH, LB><<<ntiles, TH>>>(in, out, N, Conv{0, 0}, op_plus{}, T(0), nullptr,
+                                                                   reinterpret_cast<uint32_t*>(ws), st);
+    });
+  };
+#define V_(R, TH, LB, NAME) variant(std::integral_constant<int, R>{}, std::integral_constant<int, TH>{}, std::integral_constant<bool, LB>{}, NAME)
+  V_(8, 256, true, "T256 R8 lookback");
+  V_(16, 256, true, "T256 R16 lookback");
+  V_(8, 512, true, "T512 R8 lookback");
+  V_(16, 512, true, "T512 R16 lookback");
+  V_(4, 1024, true, "T1024 R4 lookback");
+  V_(8, 1024, true, "T1024 R8 lookback");
+  V_(8, 1024, false, "T1024 R8 no-lookback");
+  V_(16, 1024, true, "T1024 R16 lookback");
+  V_(16, 512, false, "T512 R16 no-lookback");
+  uint32_t h = 0; CK(hipMemcpy(&h, err, 4, hipMemcpyDeviceToHost)); printf("deverr %u\n", h);
+  return 0;
+}
