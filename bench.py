@@ -1,0 +1,268 @@
+"""bench.py -- headline benchmark of the MI355X backend for HPX's data-parallel
+algorithm layer.
+
+metric (BASELINE.json): achieved GB/s (% HBM peak) for triad/reduce/scan/sort
+at 2^30, 1-8 MI355X.
+
+One *step* = one pass of the hot path over 2^30 elements per GPU (weak
+scaling; configs[1] of BASELINE.json plus the STREAM triad leg):
+    STREAM triad      a = b + 3.0*c            2^30 doubles   24 B/elem
+    transform_reduce  sum(x), init 0           2^30 int64      8 B/elem
+    inclusive_scan    y = scan(x, plus, 0)     2^30 int64     16 B/elem
+through the segmented algorithms over a partitioned_vector with one
+partition per GPU (N = 1: the plain hip-executor algorithms; N > 1: segment
+totals/carries exchanged with one RCCL all-gather of 8 B per GPU).
+value = algorithmic bytes of all GPUs / max-over-ranks wall time of K steps.
+
+Also reported (outside the timed region, rank 0): sort of 2^30 uint64 keys
+(136 B/key LSD model), copy_if, f64 reduce/scan, the 1d_stencil heat
+solver, the per-kernel HIP-event timings, the roofline of the dominant
+kernel, and the HPX-par host baseline (oracle restatement) on a 2^27 sample.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+class Events:
+    """HIP events on the library's stream (torch.cuda.Event would only see
+    torch's current stream)."""
+
+    def __init__(self, L, count):
+        self.L = L
+        self.ev = []
+        for _ in range(count):
+            h = ctypes.c_void_p()
+            L.call("hpxhip_event_create", ctypes.byref(h))
+            self.ev.append(h)
+        self.i = 0
+
+    def record(self, stream):
+        e = self.ev[self.i]
+        self.i += 1
+        self.L.call("hpxhip_event_record", e, stream)
+        return e
+
+    def ms(self, a, b):
+        f = ctypes.c_float()
+        self.L.call("hpxhip_event_elapsed_ms", a, b, ctypes.byref(f))
+        return f.value
+
+
+def pct(gbs):
+    return round(100.0 * gbs / HBM_PEAK_GBS, 2)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--logn", type=int, default=30)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--cpu-logn", type=int, default=27)
+    args = ap.parse_args()
+
+    import hpx_amd as hpx
+    from hpx_amd import _lib as L
+    from hpx_amd import execution as ex, functional as F, segmented as S
+
+    comm, tgt = S.init_distributed()
+    rank, world = comm.rank, comm.size
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    stream = tgt.stream
+    pol = ex.par.on(hpx.default_executor(tgt))
+    seg = S.algorithms
+
+    n_local = 1 << args.logn
+    n = n_local * world
+    a = S.partitioned_vector(n, np.float64, comm=comm, tgt=tgt)
+    b = S.partitioned_vector(n, np.float64, comm=comm, tgt=tgt)
+    c = S.partitioned_vector(n, np.float64, comm=comm, tgt=tgt)
+    x = S.partitioned_vector(n, np.int64, comm=comm, tgt=tgt)
+    y = S.partitioned_vector(n, np.int64, comm=comm, tgt=tgt)
+    seg.generate(pol, b.begin(), b.end(), "unit", 1)
+    seg.generate(pol, c.begin(), c.end(), "unit", 2)
+    seg.generate(pol, x.begin(), x.end(), "range", 0x5EED, -(1 << 20), 1 << 20)
+    tgt.synchronize()
+
+    triad = F.triad_step(3.0)
+    ev = Events(L, 6 * (args.steps + args.warmup) + 8)
+    marks = []
+
+    def step(timed):
+        e0 = ev.record(stream) if timed else None
+        seg.transform_binary(pol, b.begin(), b.end(), c.begin(), a.begin(), triad)
+        e1 = ev.record(stream) if timed else None
+        r = seg.reduce(pol, x.begin(), x.end(), 0, F.plus)
+        e2 = ev.record(stream) if timed else None
+        seg.inclusive_scan(pol, x.begin(), x.end(), y.begin(), F.plus, 0)
+        e3 = ev.record(stream) if timed else None
+        if timed:
+            marks.append((e0, e1, e2, e3))
+        return r
+
+    for _ in range(args.warmup):
+        step(False)
+    tgt.synchronize()
+    comm.barrier()
+    tgt.synchronize()
+    t0 = time.perf_counter()
+    r = None
+    for _ in range(args.steps):
+        r = step(True)
+    tgt.synchronize()
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{tgt.device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel HIP-event timings (segment-local kernels + their collectives)
+    k_triad = np.mean([ev.ms(m[0], m[1]) for m in marks])
+    k_reduce = np.mean([ev.ms(m[1], m[2]) for m in marks])
+    k_scan = np.mean([ev.ms(m[2], m[3]) for m in marks])
+
+    # cheap self-check: last inclusive-scan value == reduce result (int64 exact)
+    if len(y.local) and rank == world - 1:
+        last_local = y.local[len(y.local) - 1]
+        assert last_local == r, f"scan/reduce mismatch {last_local} != {r}"
+    from oracle import oracle as O  # checker only
+    for i in [0, 1, n_local // 3, n_local - 1]:
+        bb = O.generate(np.float64, "unit", 1, 1, offset=a.lo + i)[0]
+        cc = O.generate(np.float64, "unit", 1, 2, offset=a.lo + i)[0]
+        assert a.local[i] == bb + cc * 3.0, "triad parity"
+
+    bytes_step = (24 + 8 + 16) * n_local
+    value = world * bytes_step * args.steps / elapsed / 1e9
+    ms_step = 1000.0 * elapsed / args.steps
+    triad_gbs = 24 * n_local / (k_triad * 1e-3) / 1e9
+    out = {
+        "metric": "achieved GB/s (% HBM peak) for triad/reduce/scan/sort at 2^30, 1-8 MI355X",
+        "value": round(value, 1),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64+int64",
+        "data": "synthetic (splitmix64 of the global index, seeded)",
+        "config": {"workload": "STREAM triad (f64) + transform_reduce (int64) + inclusive_scan (int64) per step",
+                   "elements_per_gpu": n_local, "global_elements": n, "partitioning": f"partitioned_vector x{world}",
+                   "bytes_per_step_per_gpu": bytes_step, "pct_hbm_peak": pct(value / world)},
+        "kernels_ms": {"triad": round(k_triad, 4), "transform_reduce": round(k_reduce, 4),
+                       "inclusive_scan": round(k_scan, 4)},
+        "kernels_gbs": {"triad": round(triad_gbs, 1),
+                        "transform_reduce": round(8 * n_local / (k_reduce * 1e-3) / 1e9, 1),
+                        "inclusive_scan": round(16 * n_local / (k_scan * 1e-3) / 1e9, 1)},
+        "roofline": {"kernel": "triad (transform_binary f64)", "bound": "hbm", "achieved": round(triad_gbs, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(triad_gbs / HBM_PEAK_GBS, 4),
+                     "traffic": None, "bytes_per_launch": 24 * n_local},
+    }
+    for v in (a, b, c):
+        v.local.free()
+    if rank == 0 and not args.no_extras:
+        out["extras"] = extras(hpx, L, ex, F, tgt, pol, x, y, n_local, world)
+    x.local.free()
+    y.local.free()
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_logn)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def timed(L, tgt, fn, reps=3):
+    ev = Events(L, 2 * reps + 2)
+    fn()
+    tgt.synchronize()
+    best = 1e30
+    for _ in range(reps):
+        e0 = ev.record(tgt.stream)
+        fn()
+        e1 = ev.record(tgt.stream)
+        tgt.synchronize()
+        best = min(best, ev.ms(e0, e1))
+    return best
+
+
+def extras(hpx, L, ex, F, tgt, pol, x, y, n_local, world):
+    from hpx_amd import parallel as P
+    res = {}
+    # f64 reduce / scan on the same vectors reinterpreted (values don't matter for speed)
+    xv, yv = x.local, y.local
+    n = n_local
+    ms = timed(L, tgt, lambda: P.copy_if(pol, xv.begin(), xv.end(), yv.begin(), F.not_less_than(0)))
+    res["copy_if_int64"] = {"ms": round(ms, 4), "gbs_model_12B": round(12 * n / ms / 1e6, 1),
+                            "pct_peak": pct(12 * n / ms / 1e6)}
+    # sort of 2^30 uint64 keys (8 GiB + 8 GiB workspace)
+    keys = hpx.vector(n, dtype=np.uint64, tgt=tgt)
+    regen = lambda: P.generate(pol, keys.begin(), keys.end(), "bits", 7)  # noqa: E731
+    ms_gen = timed(L, tgt, regen, reps=2)
+    ms_sort = timed(L, tgt, lambda: (regen(), P.sort(pol, keys.begin(), keys.end())), reps=2) - ms_gen
+    ok = P.reduce(pol, keys.begin(), keys.begin() + 1, 0, F.plus) <= P.reduce(pol, keys.begin() + 1, keys.begin() + 2, 0, F.plus)
+    res["sort_uint64"] = {"ms": round(ms_sort, 3), "gkeys_per_s": round(n / ms_sort / 1e6, 3),
+                          "gbs_model_136B": round(136 * n / ms_sort / 1e6, 1),
+                          "pct_peak": pct(136 * n / ms_sort / 1e6), "sorted_head_check": bool(ok)}
+    keys.free()
+    # 1d_stencil heat: 2^32 points on one GPU (two 32 GiB buffers), 10 steps
+    from hpx_amd import stencil
+    nx = 1 << 32 if world == 1 else n
+    st = stencil.stepper(nx, tgt)
+    nt = 10
+    ms = timed(L, tgt, lambda: st.do_work(nt), reps=2)
+    res["stencil_heat"] = {"points": nx, "steps": nt, "ms": round(ms, 3),
+                           "gpoint_steps_per_s": round(nx * nt / ms / 1e6, 2),
+                           "gbs_model_16B": round(16 * nx * nt / ms / 1e6, 1), "pct_peak": pct(16 * nx * nt / ms / 1e6)}
+    for v in st.U:
+        v.free()
+    return res
+
+
+def cpu_baseline(logn):
+    """HPX-par restatement (oracle) of the same step on the host cores, on a
+    2^logn sample: triad + reduce + inclusive scan."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    n = 1 << logn
+    t_triad = O.par_triad(n, threads, reps=3)
+    x = O.generate(np.int64, "range", n, 0x5EED, -(1 << 20), 1 << 20)
+    t_red, _ = O.par_reduce_i64(x, threads, reps=3)
+    t_scan, _ = O.par_scan_i64(x, threads, reps=3)
+    gbs = (24 + 8 + 16) * n / (t_triad + t_red + t_scan) / 1e9
+    return {"value": round(gbs, 2), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"2^{logn} elements: triad f64 + reduce int64 + inclusive_scan int64, best of 3, "
+                      f"HPX par chunking (4*cores chunks) on {threads} std::threads",
+            "triad_gbs": round(24 * n / t_triad / 1e9, 2), "reduce_gbs": round(8 * n / t_red / 1e9, 2),
+            "scan_gbs": round(16 * n / t_scan / 1e9, 2)}
+
+
+if __name__ == "__main__":
+    main()

@@ -113,6 +113,7 @@ SIGNATURES = {
     "hpxhip_memset_async": [_vp, _i, _sz, _vp],
     "hpxhip_scratch_bytes": [_i, _i, _i, _u64, ctypes.POINTER(_sz)],
     "hpxhip_generate": [_i, _i, _u64, ctypes.c_int64, ctypes.c_int64, _vp, _u64, _vp],
+    "hpxhip_generate_at": [_i, _i, _u64, _u64, ctypes.c_int64, ctypes.c_int64, _vp, _u64, _vp],
     "hpxhip_fill": [_i, _vp, _vp, _u64, _vp],
     "hpxhip_copy": [_i, _vp, _vp, _u64, _vp],
     "hpxhip_for_each": [_i, _i, _vp, _vp, _u64, _vp],

@@ -210,10 +210,11 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(kThreads) void k_generate(T* out, uint64_t n, int kind, uint64_t seed, int64_t lo,
-                                                        uint64_t span) {
+__global__ __launch_bounds__(kThreads) void k_generate(T* out, uint64_t n, uint64_t base, int kind, uint64_t seed,
+                                                        int64_t lo, uint64_t span) {
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
-    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) {
+    for (uint64_t j = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; j < n; j += stride) {
+        const uint64_t i = base + j;  // global index
         T v;
         if (kind == HPXHIP_GEN_IOTA) {
             v = static_cast<T>(lo + static_cast<int64_t>(i));
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(kThreads) void k_generate(T* out, uint64_t n, int k
                 else v = static_cast<T>(static_cast<float>(z >> 40) * 0x1.0p-24f);
             }
         }
-        out[i] = v;
+        out[j] = v;
     }
 }
 
@@ -241,8 +242,8 @@ __global__ __launch_bounds__(kThreads) void k_generate(T* out, uint64_t n, int k
 
 extern "C" {
 
-int hpxhip_generate(int dtype, int kind, uint64_t seed, int64_t lo, int64_t hi, void* data, uint64_t n,
-                    hpxhip_stream stream) {
+int hpxhip_generate_at(int dtype, int kind, uint64_t seed, uint64_t index_base, int64_t lo, int64_t hi, void* data,
+                       uint64_t n, hpxhip_stream stream) {
     if (n == 0) return 0;
     if (!data || kind < HPXHIP_GEN_IOTA || kind > HPXHIP_GEN_UNIT) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -252,10 +253,15 @@ int hpxhip_generate(int dtype, int kind, uint64_t seed, int64_t lo, int64_t hi, 
     return with_dtype(dtype, [&](auto t) -> int {
         using T = typename decltype(t)::type;
         hipLaunchKernelGGL((k_generate<T>), dim3(grid_for(n / 4 + 1)), dim3(kThreads), 0, s, static_cast<T*>(data), n,
-                           kind, seed, lo, span);
+                           index_base, kind, seed, lo, span);
         HPXHIP_CHECK_LAUNCH();
         return 0;
     });
+}
+
+int hpxhip_generate(int dtype, int kind, uint64_t seed, int64_t lo, int64_t hi, void* data, uint64_t n,
+                    hpxhip_stream stream) {
+    return hpxhip_generate_at(dtype, kind, seed, 0, lo, hi, data, n, stream);
 }
 
 int hpxhip_fill(int dtype, const void* value, void* data, uint64_t n, hpxhip_stream stream) {

@@ -1,0 +1,427 @@
+"""hpx::partitioned_vector and the segmented algorithms over the GPUs of a node.
+
+Reference:
+  * partitioned_vector: hpx/components/containers/partitioned_vector/
+    partitioned_vector_decl.hpp:146-405, partitioned_vector_impl.hpp:317-395
+    (N elements in `num_parts` partitions of ceil(N/num_parts), last shorter,
+    impl.hpp:325);
+  * segmented for_each/transform: segmented_algorithms/for_each.hpp:40-213
+    (per-segment dispatch, no combine);
+  * segmented reduce: segmented_algorithms/reduce.hpp:112-209 + detail/
+    reduce.hpp:31-63 (S_k per segment, then init (op) S_0 (op) ... in
+    segment order, reduce.hpp:191-207);
+  * segmented scans: segmented_algorithms/detail/scan.hpp:527-696 (segment
+    totals, carries in segment order, per-segment scan with init = carry).
+
+MI355X design: one process per GPU (torchrun), one partition per rank.  The
+reference ships partitions to localities with AGAS actions and combines
+per-segment results with futures on the caller; here every rank runs the
+whole-algorithm kernel on its partition and the tiny per-segment results
+(8 B each) are exchanged with one RCCL all-gather (torch.distributed,
+backend "nccl" = RCCL over xGMI).  Every rank then folds them in segment
+order ON THE DEVICE (hpxhip_fold), so the carry of a scan never leaves the
+GPU.  No data-path collective: only segment totals/counts move.
+
+The orchestration is written against two small interfaces so that the
+multi-rank logic is testable on CPU with gloo (tests/test_segmented_gloo.py):
+``comm`` (rank, size, all-gather of a small device buffer, barrier, halo
+send/recv) and ``engine`` (the per-partition kernels).  The product engine
+is :class:`HipEngine` (the C ABI); there is no host fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib as L
+from . import functional as F
+from .compute import dtype_code, np_dtype, target, vector
+
+
+# ------------------------------------------------------------- partitioning
+def partition_bounds(n: int, parts: int, k: int):
+    """[begin, end) of partition k (partitioned_vector_impl.hpp:325-372)."""
+    part = -(-n // parts) if parts else 0
+    b = min(n, k * part)
+    return b, min(n, b + part)
+
+
+# ----------------------------------------------------------------- comms
+class LocalComm:
+    """World of one rank (no collectives)."""
+    rank = 0
+    size = 1
+
+    def __init__(self, tgt: target | None = None):
+        self.tgt = tgt or target(0)
+        self._buf = None
+
+    def slots(self, nbytes: int):
+        """(send_ptr, recv_ptr) device buffers for one all-gather."""
+        if self._buf is None:
+            self._buf = vector(64, dtype=np.uint64, tgt=self.tgt)
+        return self._buf.data(), self._buf.data()  # recv[0] == send
+
+    def allgather(self, nbytes: int, stream):
+        return None
+
+    def barrier(self):
+        pass
+
+    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream):
+        # ring of one: left neighbour's last point is my last, right's first is my first
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_left), ctypes.c_void_p(send_right), 8, L.D2D, stream)
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_right), ctypes.c_void_p(send_left), 8, L.D2D, stream)
+
+
+class TorchComm:
+    """One rank per GPU over torch.distributed (backend "nccl" = RCCL on ROCm).
+
+    The small exchange buffers are torch device tensors; the library's kernels
+    write into them and the collectives run on the library's stream
+    (torch.cuda.ExternalStream), so stream order replaces host syncs."""
+
+    def __init__(self, tgt: target):
+        import torch
+        import torch.distributed as dist
+        self.torch = torch
+        self.dist = dist
+        self.tgt = tgt
+        self.rank = dist.get_rank()
+        self.size = dist.get_world_size()
+        self.device = torch.device("cuda", tgt.device)
+        self._send = torch.zeros(8, dtype=torch.int64, device=self.device)
+        self._recv = torch.zeros(8 * self.size, dtype=torch.int64, device=self.device)
+        self._halo = torch.zeros(4, dtype=torch.float64, device=self.device)
+
+    def _stream(self, stream):
+        return self.torch.cuda.ExternalStream(stream.value if hasattr(stream, "value") else int(stream),
+                                              device=self.device)
+
+    def slots(self, nbytes: int):
+        return self._send.data_ptr(), self._recv.data_ptr()
+
+    def allgather(self, nbytes: int, stream):
+        """recv[r*8 : r*8+nbytes] <- rank r's send[0:nbytes] (8-byte words)."""
+        words = max(1, nbytes // 8)
+        with self.torch.cuda.stream(self._stream(stream)):
+            out = self._recv.view(self.size, 8)[:, :words]
+            if words == 8:
+                self.dist.all_gather_into_tensor(self._recv, self._send)
+            else:
+                tmp = self.torch.empty(self.size * words, dtype=self.torch.int64, device=self.device)
+                self.dist.all_gather_into_tensor(tmp, self._send[:words].contiguous())
+                out.copy_(tmp.view(self.size, words))
+        return None
+
+    def barrier(self):
+        self.dist.barrier()
+
+    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream):
+        """Ring halo: my first point goes to the left neighbour (its right
+        halo), my last point to the right neighbour (its left halo)."""
+        torch, dist = self.torch, self.dist
+        left, right = (self.rank - 1) % self.size, (self.rank + 1) % self.size
+        with torch.cuda.stream(self._stream(stream)):
+            h = self._halo
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(h.data_ptr()), ctypes.c_void_p(send_left), 8, L.D2D, stream)
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(h.data_ptr() + 8), ctypes.c_void_p(send_right), 8, L.D2D,
+                   stream)
+            ops = [dist.P2POp(dist.isend, h[0:1], left), dist.P2POp(dist.isend, h[1:2], right),
+                   dist.P2POp(dist.irecv, h[2:3], left), dist.P2POp(dist.irecv, h[3:4], right)]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_left), ctypes.c_void_p(h.data_ptr() + 16), 8, L.D2D,
+                   stream)
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_right), ctypes.c_void_p(h.data_ptr() + 24), 8, L.D2D,
+                   stream)
+
+
+# ------------------------------------------------------------------ engine
+class HipEngine:
+    """Per-partition kernels (C ABI)."""
+
+    def __init__(self, tgt: target):
+        self.tgt = tgt
+
+    @property
+    def stream(self):
+        return self.tgt.stream
+
+    def reduce_into(self, vec, lo, hi, op, conv, acc_dt, out_ptr):
+        """out_ptr <- identity (op) conv(x[lo]) ... (op) conv(x[hi-1])."""
+        ident = _identity(op.kind, acc_dt)
+        L.call("hpxhip_transform_reduce", vec.dtype, acc_dt, op.kind, conv.kind, L.scalars_buf(acc_dt, conv.scalars),
+               L.scalar_buf(acc_dt, ident), ctypes.c_void_p(vec.data() + lo * vec.value_size), hi - lo,
+               ctypes.c_void_p(out_ptr), self.stream, None, 0)
+
+    def fold(self, dt, op, init, values_ptr, count, out_ptr):
+        L.call("hpxhip_fold", dt, op.kind, L.scalar_buf(dt, init), ctypes.c_void_p(values_ptr), count,
+               ctypes.c_void_p(out_ptr), self.stream)
+
+    def scan(self, src, lo, hi, dst, dlo, op, conv, inclusive, prefix_ptr):
+        dt = src.dtype
+        L.call("hpxhip_scan", dt, op.kind, 1 if inclusive else 0, conv.kind, L.scalars_buf(dt, conv.scalars),
+               L.scalar_buf(dt, 0), ctypes.c_void_p(prefix_ptr), ctypes.c_void_p(src.data() + lo * src.value_size),
+               ctypes.c_void_p(dst.data() + dlo * dst.value_size), hi - lo, self.stream, None, 0)
+
+    def read(self, ptr, dt):
+        out = np.empty(1, np_dtype(dt))
+        L.call("hpxhip_memcpy_async", out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ptr), out.itemsize, L.D2H,
+               self.stream)
+        L.call("hpxhip_stream_synchronize", self.stream)
+        return out[0].item()
+
+    def copy_if(self, src, lo, hi, dst, dlo, pred, count_ptr):
+        L.call("hpxhip_copy_if", src.dtype, pred.kind, L.scalar_buf(src.dtype, pred.arg),
+               ctypes.c_void_p(src.data() + lo * src.value_size), ctypes.c_void_p(dst.data() + dlo * dst.value_size),
+               hi - lo, ctypes.c_void_p(count_ptr), self.stream, None, 0)
+
+
+def _identity(kind, dt):
+    isint = np_dtype(dt).kind in "iu"
+    info = np.iinfo(np_dtype(dt)) if isint else None
+    return {L.PLUS: 0, L.MULTIPLIES: 1,
+            L.MIN: (info.max if isint else float("inf")), L.MAX: (info.min if isint else float("-inf")),
+            L.BIT_AND: (-1 if np_dtype(dt).kind == "i" else (info.max if isint else 0)), L.BIT_OR: 0,
+            L.BIT_XOR: 0}[kind]
+
+
+# -------------------------------------------------------- partitioned_vector
+class partitioned_vector:
+    """hpx::partitioned_vector<T> with one partition per rank (container_layout
+    over the ranks, partitioned_vector_impl.hpp:317-395)."""
+
+    def __init__(self, n: int, dtype=np.float64, value=None, comm=None, tgt: target | None = None):
+        self.tgt = tgt or (comm.tgt if comm is not None and hasattr(comm, "tgt") else target(0))
+        self.comm = comm or LocalComm(self.tgt)
+        self.n = int(n)
+        self.dtype = dtype_code(dtype)
+        self.rank, self.parts = self.comm.rank, self.comm.size
+        self.lo, self.hi = partition_bounds(self.n, self.parts, self.rank)
+        self.local = vector(self.hi - self.lo, dtype=self.dtype, value=value, tgt=self.tgt)
+
+    def size(self) -> int:
+        return self.n
+
+    def __len__(self):
+        return self.n
+
+    def get_num_partitions(self) -> int:
+        return self.parts
+
+    def segment_bounds(self, k: int):
+        return partition_bounds(self.n, self.parts, k)
+
+    def begin(self):
+        return segmented_iterator(self, 0)
+
+    def end(self):
+        return segmented_iterator(self, self.n)
+
+    def local_range(self, first: int, last: int):
+        """Intersection of global [first, last) with this rank's partition,
+        as local indices."""
+        a, b = max(first, self.lo), min(last, self.hi)
+        return (a - self.lo, b - self.lo) if a < b else (0, 0)
+
+
+class segmented_iterator:
+    """partitioned_vector_segmented_iterator.hpp:858-945 (global index view)."""
+    __slots__ = ("pv", "pos")
+
+    def __init__(self, pv, pos):
+        self.pv, self.pos = pv, int(pos)
+
+    def __add__(self, k):
+        return segmented_iterator(self.pv, self.pos + int(k))
+
+    def __sub__(self, other):
+        if isinstance(other, segmented_iterator):
+            return self.pos - other.pos
+        return segmented_iterator(self.pv, self.pos - int(other))
+
+    def __eq__(self, other):
+        return isinstance(other, segmented_iterator) and other.pv is self.pv and other.pos == self.pos
+
+    def __hash__(self):
+        return hash((id(self.pv), self.pos))
+
+
+def _range(first, last=None):
+    if isinstance(first, partitioned_vector):
+        return first, 0, first.n
+    if not isinstance(first, segmented_iterator) or not isinstance(last, segmented_iterator) or first.pv is not last.pv:
+        raise TypeError("expected segmented iterators of one partitioned_vector")
+    return first.pv, first.pos, last.pos
+
+
+# ---------------------------------------------------------------- algorithms
+class segmented:
+    """Segmented algorithms bound to an engine (HipEngine in the product)."""
+
+    def __init__(self, engine=None):
+        self._engine = engine
+
+    def engine(self, pv):
+        return self._engine or HipEngine(pv.tgt)
+
+    # --- for_each / transform / fill / generate: per-segment, no combine
+    def for_each(self, pol, first, last, f):
+        pv, a, b = _range(first, last)
+        lo, hi = pv.local_range(a, b)
+        from . import algorithms as A
+        if hi > lo:
+            A.for_each(pol.on(_exec(pv)), pv.local.begin() + lo, pv.local.begin() + hi, f)
+        return last
+
+    def fill(self, pol, first, last, value):
+        pv, a, b = _range(first, last)
+        lo, hi = pv.local_range(a, b)
+        from . import algorithms as A
+        if hi > lo:
+            A.fill(pol.on(_exec(pv)), pv.local.begin() + lo, pv.local.begin() + hi, value)
+
+    def generate(self, pol, first, last, kind="splitmix", seed=0x5EED, lo_=0, hi_=0):
+        """Counter-based generation by GLOBAL index, so the partitioned data
+        equals the unpartitioned data element for element."""
+        pv, a, b = _range(first, last)
+        lo, hi = pv.local_range(a, b)
+        if hi > lo:
+            kinds = {"iota": L.GEN_IOTA, "bits": L.GEN_BITS, "splitmix": L.GEN_BITS, "range": L.GEN_RANGE,
+                     "unit": L.GEN_UNIT}
+            L.call("hpxhip_generate_at", pv.dtype, kinds[kind], seed, pv.lo + lo, lo_, hi_,
+                   ctypes.c_void_p(pv.local.data() + lo * pv.local.value_size), hi - lo, pv.tgt.stream)
+        return last
+
+    def transform(self, pol, first, last, dest, f):
+        pv, a, b = _range(first, last)
+        pd, d0, _ = _range(dest, dest + (b - a)) if isinstance(dest, segmented_iterator) else (dest, 0, 0)
+        if pd.n != pv.n or d0 != a:
+            raise ValueError("segmented transform needs identically partitioned source and destination ranges")
+        lo, hi = pv.local_range(a, b)
+        from . import algorithms as A
+        if hi > lo:
+            A.transform(pol.on(_exec(pv)), pv.local.begin() + lo, pv.local.begin() + hi, pd.local.begin() + lo, f)
+        return dest + (b - a)
+
+    def transform_binary(self, pol, first1, last1, first2, dest, f):
+        pv, a, b = _range(first1, last1)
+        p2, a2, _ = _range(first2, first2 + (b - a))
+        pd, d0, _ = _range(dest, dest + (b - a))
+        if not (p2.n == pv.n == pd.n and a2 == a == d0):
+            raise ValueError("segmented transform needs identically partitioned ranges")
+        lo, hi = pv.local_range(a, b)
+        from . import algorithms as A
+        if hi > lo:
+            A.transform(pol.on(_exec(pv)), pv.local.begin() + lo, pv.local.begin() + hi, p2.local.begin() + lo,
+                        pd.local.begin() + lo, f)
+        return dest + (b - a)
+
+    # --- reduce (segmented_algorithms/reduce.hpp:112-209)
+    def transform_reduce(self, pol, first, last, init, red_op, conv_op):
+        red_op = F.require(red_op, F.BinaryOp, "segmented transform_reduce")
+        conv_op = F.require(conv_op, F.Unary, "segmented transform_reduce")
+        pv, a, b = _range(first, last)
+        eng, comm = self.engine(pv), pv.comm
+        from .algorithms import _acc_dtype, _slots_for
+        adt = _acc_dtype(pv.dtype, init)
+        send, recv = comm.slots(8)
+        lo, hi = pv.local_range(a, b)
+        eng.reduce_into(pv.local, lo, hi, red_op, conv_op, adt, send)  # S_k (identity if empty)
+        comm.allgather(8, eng.stream)                                    # one RCCL all-gather of 8 B
+        dev, _ = _slots_for(pv.tgt).next() if isinstance(eng, HipEngine) else (eng.scratch(), None)
+        eng.fold(adt, red_op, init, recv, comm.size, dev)                # init (op) S_0 (op) ... in order
+        return eng.read(dev, adt)
+
+    def reduce(self, pol, first, last, init=0, op=F.plus):
+        return self.transform_reduce(pol, first, last, init, op, F.identity())
+
+    # --- scans (segmented_algorithms/detail/scan.hpp:527-696)
+    def _scan(self, pol, first, last, dest, op, init, inclusive, conv):
+        op = F.require(op, F.BinaryOp, "segmented scan")
+        conv = F.require(conv, F.Unary, "segmented scan")
+        pv, a, b = _range(first, last)
+        pd, d0, _ = _range(dest, dest + (b - a))
+        if pd.n != pv.n or d0 != a:
+            raise ValueError("segmented scan needs identically partitioned input and output ranges")
+        eng, comm = self.engine(pv), pv.comm
+        lo, hi = pv.local_range(a, b)
+        send, recv = comm.slots(8)
+        from .algorithms import _slots_for
+        if comm.size > 1:
+            eng.reduce_into(pv.local, lo, hi, op, conv, pv.dtype, send)       # step 1: segment totals
+            comm.allgather(8, eng.stream)
+            carry = _slots_for(pv.tgt).next()[0] if isinstance(eng, HipEngine) else eng.scratch()
+            eng.fold(pv.dtype, op, init, recv, comm.rank, carry)              # carries in segment order
+        else:
+            carry = _slots_for(pv.tgt).next()[0] if isinstance(eng, HipEngine) else eng.scratch()
+            eng.fold(pv.dtype, op, init, recv, 0, carry)                      # = init
+        if hi > lo:
+            eng.scan(pv.local, lo, hi, pd.local, lo, op, conv, inclusive, carry)  # step 2 with init = carry
+        return dest + (b - a)
+
+    def inclusive_scan(self, pol, first, last, dest, op=F.plus, init=0):
+        return self._scan(pol, first, last, dest, op, init, True, F.identity())
+
+    def exclusive_scan(self, pol, first, last, dest, init, op=F.plus):
+        return self._scan(pol, first, last, dest, op, init, False, F.identity())
+
+    def transform_inclusive_scan(self, pol, first, last, dest, op, conv, init=0):
+        return self._scan(pol, first, last, dest, op, init, True, conv)
+
+    # --- copy_if: local compaction + all-gather of counts -> global offsets
+    def copy_if(self, pol, first, last, dest_pv, pred):
+        """Each rank compacts its segment into the front of its partition of
+        dest_pv; returns (global count, this rank's offset, local count)."""
+        pred = F.require(pred, F.Predicate, "segmented copy_if")
+        pv, a, b = _range(first, last)
+        eng, comm = self.engine(pv), pv.comm
+        lo, hi = pv.local_range(a, b)
+        send, recv = comm.slots(8)
+        eng.copy_if(pv.local, lo, hi, dest_pv.local, 0, pred, send)
+        comm.allgather(8, eng.stream)
+        counts = [int(c) for c in _read_words(eng, recv, comm.size, L.U64)]
+        return sum(counts), sum(counts[:comm.rank]), counts[comm.rank]
+
+
+def _read_words(eng, ptr, count, dt):
+    if hasattr(eng, "read_words"):
+        return eng.read_words(ptr, count, dt)
+    out = np.empty(count, np_dtype(dt))
+    L.call("hpxhip_memcpy_async", out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ptr), 8 * count, L.D2H,
+           eng.stream)
+    L.call("hpxhip_stream_synchronize", eng.stream)
+    return out
+
+
+def _exec(pv):
+    from .compute import default_executor
+    ex = getattr(pv, "_exec", None)
+    if ex is None:
+        ex = default_executor(pv.tgt)
+        pv._exec = ex
+    return ex
+
+
+# the default instance: hpx_amd.segmented.algorithms.reduce(...)
+algorithms = segmented()
+
+
+# ------------------------------------------------------------- comm factory
+def init_distributed(tgt_from_local_rank: bool = True):
+    """torchrun rendezvous (MASTER_ADDR 127.0.0.1), backend "nccl" (RCCL);
+    returns (comm, target).  World size 1 without torchrun -> LocalComm."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    tgt = target(local_rank if tgt_from_local_rank else 0)
+    if world <= 1:
+        return LocalComm(tgt), tgt
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(tgt.device)
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", device_id=torch.device("cuda", tgt.device))
+    return TorchComm(tgt), tgt

@@ -216,6 +216,10 @@ int hpxhip_fill(int dtype, const void* value, void* data, uint64_t n, hpxhip_str
 enum hpxhip_gen { HPXHIP_GEN_IOTA = 0, HPXHIP_GEN_BITS = 1, HPXHIP_GEN_RANGE = 2, HPXHIP_GEN_UNIT = 3 };
 int hpxhip_generate(int dtype, int kind, uint64_t seed, int64_t lo, int64_t hi, void* data, uint64_t n,
                     hpxhip_stream stream);
+/* Same with global indices i = index_base + j for data[j] (a partition of a
+   partitioned_vector generates exactly its slice of the global sequence). */
+int hpxhip_generate_at(int dtype, int kind, uint64_t seed, uint64_t index_base, int64_t lo, int64_t hi,
+                       void* data, uint64_t n, hpxhip_stream stream);
 /* copy.hpp:88-114: out[i] = in[i]. */
 int hpxhip_copy(int dtype, const void* in, void* out, uint64_t n, hpxhip_stream stream);
 /* for_each.hpp:369: data[i] = f(data[i]) in place (for_each_compute.cu `i += 5`). */

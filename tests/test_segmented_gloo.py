@@ -1,0 +1,189 @@
+"""Multi-rank orchestration of the segmented algorithms on CPU (gloo,
+world sizes 2 and 3): partition bounds, segment-order folds of the RCCL
+all-gathered totals, scan carries, copy_if offsets and the stencil halo ring.
+
+The per-partition kernels are replaced by a numpy test engine *in this test
+only* (the product engine is HipEngine, exercised by tests/test_gpu_*.py);
+the code under test is hpx_amd.segmented's orchestration."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from hpx_amd import functional as F  # noqa: E402
+from hpx_amd import segmented as S  # noqa: E402
+
+OPS = {0: np.add, 1: np.multiply, 2: np.minimum, 3: np.maximum, 4: np.bitwise_and, 5: np.bitwise_or, 6: np.bitwise_xor}
+
+
+class GlooComm:
+    def __init__(self):
+        self.rank, self.size = dist.get_rank(), dist.get_world_size()
+
+    def slots(self, nbytes):
+        self._send = np.zeros(1, np.int64)
+        self._recv = np.zeros(self.size, np.int64)
+        return self._send, self._recv
+
+    def allgather(self, nbytes, stream):
+        out = [torch.zeros(1, dtype=torch.int64) for _ in range(self.size)]
+        dist.all_gather(out, torch.from_numpy(self._send.copy()))
+        self._recv[:] = [int(t.item()) for t in out]
+
+    def barrier(self):
+        dist.barrier()
+
+
+class NumpyEngine:
+    """Test double of HipEngine: same calls, numpy arithmetic, values held
+    as 8-byte words like the device slots."""
+    stream = None
+
+    def _w2v(self, words, dt):
+        return np.asarray(words, np.int64).view(dt)
+
+    def reduce_into(self, vec, lo, hi, op, conv, acc_dt, out):
+        dt = np.dtype(vec.dtype)
+        x = vec[lo:hi].astype(dt)
+        ident = S._identity(op.kind, {np.dtype(np.int64): 2, np.dtype(np.float64): 5}[dt])
+        r = np.array([ident], dt)[0]
+        for v in x:
+            r = OPS[op.kind](r, v)
+        out[0] = np.array([r], dt).view(np.int64)[0]
+
+    def fold(self, dt_code, op, init, values, count, out):
+        dt = {2: np.int64, 5: np.float64}[dt_code]
+        acc = np.array([init], dt)[0]
+        for v in self._w2v(values[:count], dt):
+            acc = OPS[op.kind](acc, v)
+        out[0] = np.array([acc], dt).view(np.int64)[0]
+
+    def scratch(self):
+        return np.zeros(1, np.int64)
+
+    def read(self, h, dt_code):
+        return self._w2v(h[:1], {2: np.int64, 5: np.float64}[dt_code])[0]
+
+    def scan(self, src, lo, hi, dst, dlo, op, conv, inclusive, carry):
+        dt = src.dtype
+        acc = self._w2v(carry[:1], dt)[0]
+        for i in range(lo, hi):
+            nxt = OPS[op.kind](acc, src[i])
+            dst[dlo + i - lo] = nxt if inclusive else acc
+            acc = nxt
+
+    def copy_if(self, src, lo, hi, dst, dlo, pred, count):
+        sel = [v for v in src[lo:hi] if pred(v)]
+        dst[dlo:dlo + len(sel)] = sel
+        count[0] = len(sel)
+
+    def read_words(self, h, count, dt):
+        return list(h[:count])
+
+
+class HostPV(S.partitioned_vector):
+    def __init__(self, glob, comm):
+        self.comm = comm
+        self.tgt = None
+        self.n = glob.size
+        self.dtype = {np.dtype(np.int64): 2, np.dtype(np.float64): 5}[glob.dtype]
+        self.rank, self.parts = comm.rank, comm.size
+        self.lo, self.hi = S.partition_bounds(self.n, self.parts, self.rank)
+        self.local = glob[self.lo:self.hi].copy()
+
+
+def _worker(rank, size, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        comm = GlooComm()
+        alg = S.segmented(NumpyEngine())
+        res = {}
+        n = 10007
+        x = O.generate(np.int64, "range", n, 0x5EED, -1000, 1000)
+        pv = HostPV(x, comm)
+        # partitioned_vector_reduce.cpp: ones + init 1 == n + 1
+        ones = HostPV(np.ones(n, np.int64), comm)
+        res["reduce_ones"] = alg.reduce(None, ones.begin(), ones.end(), 1, F.plus)
+        res["reduce"] = alg.reduce(None, pv.begin(), pv.end(), 7, F.plus)
+        res["reduce_max"] = alg.reduce(None, pv, None, -(1 << 62), F.maximum)
+        out = HostPV(np.zeros(n, np.int64), comm)
+        alg.inclusive_scan(None, pv.begin(), pv.end(), out.begin(), F.plus, 5)
+        res["incl"] = (out.lo, out.local.copy())
+        alg.exclusive_scan(None, pv.begin(), pv.end(), out.begin(), 5)
+        res["excl"] = (out.lo, out.local.copy())
+        # sub-range scan
+        alg.inclusive_scan(None, pv.begin() + 1234, pv.end() - 77, out.begin() + 1234, F.plus, 0)
+        res["sub"] = (out.lo, out.local.copy())
+        dst = HostPV(np.zeros(n, np.int64), comm)
+        total, off, cnt = alg.copy_if(None, pv.begin(), pv.end(), dst, F.not_less_than(0))
+        res["copy_if"] = (total, off, dst.local[:cnt].copy())
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_segmented_algorithms_gloo(size):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, size, port, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(size))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 10007
+    x = O.generate(np.int64, "range", n, 0x5EED, -1000, 1000)
+    for r in range(size):
+        res = results[r]
+        assert res["reduce_ones"] == n + 1
+        assert res["reduce"] == O.segmented_reduce(x, 7, size) == 7 + int(x.sum())
+        assert res["reduce_max"] == x.max()
+    incl = O.segmented_scan(x, 5, size, True)
+    excl = O.segmented_scan(x, 5, size, False)
+    sub = np.zeros(n, np.int64)
+    sub[1234:n - 77] = np.cumsum(x[1234:n - 77])
+    for key, exp in (("incl", incl), ("excl", excl)):
+        got = np.zeros(n, np.int64)
+        for r in range(size):
+            lo, loc = results[r][key]
+            got[lo:lo + loc.size] = loc
+        np.testing.assert_array_equal(got, exp)
+    got = np.zeros(n, np.int64)
+    for r in range(size):
+        lo, loc = results[r]["sub"]
+        got[lo:lo + loc.size] = loc
+    np.testing.assert_array_equal(got[1234:n - 77], sub[1234:n - 77])
+    sel = O.copy_if(x, "not_less_than", 0)
+    parts = sorted((results[r]["copy_if"][1], results[r]["copy_if"][2]) for r in range(size))
+    assert all(results[r]["copy_if"][0] == sel.size for r in range(size))
+    np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), sel)
+
+
+def test_partition_bounds_match_reference_layout():
+    # partitioned_vector_impl.hpp:325: ceil(n/parts) per partition, last shorter
+    for n, p in [(10007, 2), (10007, 3), (10, 4), (3, 8), (0, 2), (2 ** 32, 8)]:
+        b = [S.partition_bounds(n, p, k) for k in range(p)]
+        assert b[0][0] == 0 and b[-1][1] == n
+        for (a0, a1), (b0, b1) in zip(b, b[1:]):
+            assert a1 == b0
+        part = -(-n // p)
+        assert all(e - s <= part for s, e in b)
