@@ -16,7 +16,10 @@ using namespace hpxhip;
 
 namespace {
 
-constexpr int kThreads = 256;
+// 1024 threads x 8 vectors = 128 KiB tiles: the tile-id counter (one agent
+// atomic per tile, ~88 per microsecond chip-wide) must not bound the pass,
+// see scan_kernel.hpp.
+constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / kWave;
 constexpr int kRounds = 8;
 

@@ -8,263 +8,46 @@
 // (and the IEEE total order for floats), so results are bit-exact against
 // std::sort for integer keys.
 //
-// Structure (8-bit digits, 4 passes for 32-bit keys, 8 for 64-bit keys):
+// Structure (8-bit digits, 4 passes for 32-bit keys, 8 for 64-bit keys;
+// kernels in sort_kernel.hpp):
 //   k_hist        one read of the keys -> all passes' 256-bin histograms
 //                 (per-block LDS histograms, one global atomic per bin);
 //   k_bin_offsets exclusive scan of each pass's histogram;
-//   k_onesweep    per pass, per 4096-key tile: wave-level match ranking
-//                 (8 ballots per key, no LDS atomics), per-wave LDS digit
-//                 counters, tile-local counting sort into LDS, per-bin
-//                 decoupled look-back across tiles (one thread per bin,
-//                 32-bit {flag,count} granules written by one sc1 store), and
-//                 a coalesced write of the LDS-sorted tile.
+//   k_onesweep    per pass, per tile: wave-level match ranking (8 ballots
+//                 per key, no LDS atomics), per-wave LDS digit counters,
+//                 tile-local counting sort into LDS, per-digit decoupled
+//                 look-back across tiles (one thread per digit, batched
+//                 granule loads, {flag,count} granules written by one sc1
+//                 store), and a coalesced write of the LDS-sorted tile.
 // A pass whose digit is constant over all keys is skipped (the histogram is
 // read back once per sort).  Traffic model: 8 B/key histogram + 16 B/key per
 // executed pass (+ values).
 #include "internal.hpp"
+#include "sort_kernel.hpp"
 
 #include <vector>
 
 using namespace hpxhip;
+using namespace hpxhip::sort_detail;
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / kWave;
-constexpr int kItems = 16;
-constexpr int kTile = kThreads * kItems;  // 4096 keys
-constexpr int kRadix = 256;
+constexpr int kHistThreads = 256;
 constexpr int kHistBlocksPerCU = 2;
 
-// Storage-bits -> ordered unsigned bits (ascending), optionally inverted.
-template <typename T, bool DESC>
-struct ordered_bits {
-    using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
-    __device__ __forceinline__ U operator()(U raw) const {
-        constexpr U sign = U(1) << (sizeof(U) * 8 - 1);
-        U u;
-        if constexpr (std::is_floating_point_v<T>) u = (raw & sign) ? ~raw : (raw | sign);
-        else if constexpr (std::is_signed_v<T>) u = raw ^ sign;
-        else u = raw;
-        return DESC ? ~u : u;
-    }
+// Tile shape per variant (scripts/ubench/sortpass.hip): keys only -> 512
+// threads x 16 keys = 8192-key tiles (64 KiB of u64 keys staged in LDS, 2
+// blocks/CU); with values -> 256 x 16 (keys and values staged).  Look-back:
+// each digit's thread loads 4 predecessors per step (4.88 ms/pass vs 5.00 at
+// 8 and 5.48 at 16; rocPRIM's radix_sort_keys takes 50.2 ms for the whole
+// 2^30 u64 sort on the same GPU, this one 43.5 ms).
+template <bool HAS_VAL>
+struct tile_shape {
+    static constexpr int threads = HAS_VAL ? 256 : 512;
+    static constexpr int items = 16;
+    static constexpr int lbb = 4;
+    static constexpr int tile = threads * items;
 };
-
-// Look-back granule: 0 = not yet published; ((c+1) << 1) = tile aggregate c;
-// (v << 1) | 1 = inclusive prefix v.
-template <typename G>
-__device__ __forceinline__ G enc_agg(uint64_t c) { return static_cast<G>((c + 1) << 1); }
-template <typename G>
-__device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 1) | 1u); }
-
-// ---------------------------------------------------------------- histogram
-template <typename U, typename X>
-__global__ __launch_bounds__(kThreads) void k_hist(const U* __restrict__ keys, uint64_t n, int passes, X xf,
-                                                    unsigned long long* __restrict__ hist) {
-    __shared__ uint32_t h[sizeof(U)][kRadix];
-    for (int i = threadIdx.x; i < static_cast<int>(sizeof(U)) * kRadix; i += kThreads) (&h[0][0])[i] = 0;
-    __syncthreads();
-    constexpr int V = 16 / sizeof(U);
-    using VT = vec<U, V>;
-    const uint64_t nvec = n / V;
-    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
-    const VT* vk = reinterpret_cast<const VT*>(keys);
-    for (uint64_t i = tid; i < nvec; i += stride * 4) {
-        VT x[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (i + u * stride < nvec) x[u] = vk[i + u * stride];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (i + u * stride < nvec) {
-#pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    const U b = xf(x[u].v[e]);
-#pragma unroll
-                    for (int p = 0; p < static_cast<int>(sizeof(U)); ++p)
-                        if (p < passes) atomicAdd(&h[p][(b >> (8 * p)) & 0xff], 1u);
-                }
-            }
-    }
-    if (tid < n - nvec * V) {
-        const U b = xf(keys[nvec * V + tid]);
-        for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(b >> (8 * p)) & 0xff], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < passes * kRadix; i += kThreads) {
-        const uint32_t c = (&h[0][0])[i];
-        if (c) atomicAdd(&hist[i], static_cast<unsigned long long>(c));
-    }
-}
-
-// Exclusive scan of each pass's 256 counts (one block per pass).
-__global__ __launch_bounds__(kThreads) void k_bin_offsets(const unsigned long long* __restrict__ hist,
-                                                           unsigned long long* __restrict__ start) {
-    __shared__ uint64_t s_w[kWaves];
-    const int p = blockIdx.x;
-    const int d = threadIdx.x;
-    const uint64_t c = hist[p * kRadix + d];
-    const uint64_t incl = wave_inclusive_scan(c, op_plus{});
-    const int wave = d / kWave;
-    if (lane_id() == kWave - 1) s_w[wave] = incl;
-    __syncthreads();
-    uint64_t pre = 0;
-    for (int w = 0; w < wave; ++w) pre += s_w[w];
-    start[p * kRadix + d] = pre + incl - c;
-}
-
-// ----------------------------------------------------------------- onesweep
-template <typename U, typename VAL, bool HAS_VAL, typename G, typename X>
-__global__ __launch_bounds__(kThreads) void k_onesweep(const U* __restrict__ kin, U* __restrict__ kout,
-                                                        const VAL* __restrict__ vin, VAL* __restrict__ vout,
-                                                        uint64_t n, int shift,
-                                                        const unsigned long long* __restrict__ bin_start,
-                                                        G* __restrict__ lb, uint32_t* __restrict__ counter,
-                                                        uint32_t* __restrict__ err, X xf) {
-    __shared__ uint32_t s_tile;
-    __shared__ uint32_t s_whist[kWaves][kRadix];
-    __shared__ uint32_t s_local[kRadix];
-    __shared__ uint32_t s_wsum[kWaves];
-    __shared__ uint64_t s_adj[kRadix];
-    __shared__ U s_keys[kTile];
-    __shared__ VAL s_vals[HAS_VAL ? kTile : 1];
-
-    const int t = threadIdx.x;
-    const int wave = t / kWave;
-    const int lane = lane_id();
-    if (t == 0) s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) s_whist[w][t] = 0;
-    __syncthreads();
-    const uint64_t tile = s_tile;
-    const uint64_t tile_base = tile * kTile;
-    const uint64_t wbase = tile_base + wave * (kTile / kWaves);
-
-    // ---- load: round r, lane l -> tile position wave*1024 + r*64 + l
-    U k[kItems];
-    VAL v[HAS_VAL ? kItems : 1];
-    const bool full = tile_base + kTile <= n;
-#pragma unroll
-    for (int r = 0; r < kItems; ++r) {
-        const uint64_t i = wbase + r * kWave + lane;
-        if (full || i < n) {
-            k[r] = kin[i];
-            if constexpr (HAS_VAL) v[r] = vin[i];
-        } else {
-            k[r] = 0;
-        }
-    }
-
-    // ---- wave-level match ranking
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t rank[kItems];
-#pragma unroll
-    for (int r = 0; r < kItems; ++r) {
-        const uint64_t i = wbase + r * kWave + lane;
-        const bool valid = full || i < n;
-        const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
-        const uint32_t below = static_cast<uint32_t>(__builtin_popcountll(peers & lt_mask));
-        const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(peers));
-        const uint32_t old = s_whist[wave][d];
-        rank[r] = old + below;
-        if (valid && below == 0) s_whist[wave][d] = old + cnt;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    }
-    __syncthreads();
-
-    // ---- per-bin tile count, wave offsets (thread t == bin t)
-    uint32_t tile_count = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-        const uint32_t c = s_whist[w][t];
-        s_whist[w][t] = tile_count;
-        tile_count += c;
-    }
-    // publish this tile's aggregate for bin t as early as possible
-    G* my = lb + tile * kRadix;
-    if (tile != 0) __hip_atomic_store(&my[t], enc_agg<G>(tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-
-    // ---- tile-local exclusive offsets over bins
-    {
-        const uint32_t incl = wave_inclusive_scan(tile_count, op_plus{});
-        if (lane == kWave - 1) s_wsum[wave] = incl;
-        __syncthreads();
-        uint32_t pre = 0;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w)
-            if (w < wave) pre += s_wsum[w];
-        s_local[t] = pre + incl - tile_count;
-    }
-    __syncthreads();
-
-    // ---- counting sort of the tile into LDS
-#pragma unroll
-    for (int r = 0; r < kItems; ++r) {
-        const uint64_t i = wbase + r * kWave + lane;
-        if (full || i < n) {
-            const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
-            const uint32_t pos = s_local[d] + s_whist[wave][d] + rank[r];
-            s_keys[pos] = k[r];
-            if constexpr (HAS_VAL) s_vals[pos] = v[r];
-        }
-    }
-
-    // ---- per-bin look-back across tiles
-    {
-        uint64_t excl = 0;
-        if (tile == 0) {
-            __hip_atomic_store(&my[t], enc_incl<G>(tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            int64_t pred = static_cast<int64_t>(tile) - 1;
-            uint32_t spins = 0;
-            while (pred >= 0) {
-                const G g = __hip_atomic_load(&lb[static_cast<uint64_t>(pred) * kRadix + t], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-                if (g == 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > kSpinLimit) {
-                        if (err)
-                            __hip_atomic_store(err, HPXHIP_DEVERR_LOOKBACK_TIMEOUT, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    continue;
-                }
-                if (g & 1u) {
-                    excl += static_cast<uint64_t>(g >> 1);
-                    break;
-                }
-                excl += static_cast<uint64_t>(g >> 1) - 1;
-                --pred;
-            }
-            __hip_atomic_store(&my[t], enc_incl<G>(excl + tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_adj[t] = static_cast<uint64_t>(bin_start[t]) + excl - s_local[t];
-    }
-    __syncthreads();
-
-    // ---- coalesced write of the LDS-sorted tile
-    const uint32_t nvalid = full ? kTile : static_cast<uint32_t>(n - tile_base);
-#pragma unroll
-    for (int r = 0; r < kItems; ++r) {
-        const uint32_t i = r * kThreads + t;
-        if (i < nvalid) {
-            const U key = s_keys[i];
-            const uint32_t d = static_cast<uint32_t>(xf(key) >> shift) & 0xffu;
-            const uint64_t dst = s_adj[d] + i;
-            kout[dst] = key;
-            if constexpr (HAS_VAL) vout[dst] = s_vals[i];
-        }
-    }
-}
 
 struct sort_layout {
     uint64_t ntiles;
@@ -272,9 +55,9 @@ struct sort_layout {
     bool wide;  // 64-bit granules
 };
 
-sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize) {
+sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     sort_layout L;
-    L.ntiles = (n + kTile - 1) / kTile;
+    L.ntiles = (n + tile - 1) / tile;
     L.wide = n >= (1ull << 31);
     size_t off = 0;
     L.alt_keys = off;
@@ -298,7 +81,8 @@ template <typename T, bool DESC, typename VAL, bool HAS_VAL>
 int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, size_t scratch_bytes) {
     using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
     using X = ordered_bits<T, DESC>;
-    const sort_layout L = make_layout(n, sizeof(U), HAS_VAL ? sizeof(VAL) : 0);
+    using TS = tile_shape<HAS_VAL>;
+    const sort_layout L = make_layout(n, sizeof(U), HAS_VAL ? sizeof(VAL) : 0, TS::tile);
     void* ws = nullptr;
     int rc = resolve_scratch(s, scratch, scratch_bytes, L.total, &ws);
     if (rc) return rc;
@@ -311,10 +95,10 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
 
     HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8, s));
     const unsigned hist_grid = static_cast<unsigned>(current_device_info().cus * kHistBlocksPerCU);
-    hipLaunchKernelGGL((k_hist<U, X>), dim3(hist_grid), dim3(kThreads), 0, s, static_cast<const U*>(keys), n, passes,
-                       X{}, hist);
+    hipLaunchKernelGGL((k_hist<U, X, kHistThreads>), dim3(hist_grid), dim3(kHistThreads), 0, s,
+                       static_cast<const U*>(keys), n, passes, X{}, hist);
     HPXHIP_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_bin_offsets, dim3(passes), dim3(kThreads), 0, s, hist, start);
+    hipLaunchKernelGGL(k_bin_offsets, dim3(passes), dim3(256), 0, s, hist, start);
     HPXHIP_CHECK_LAUNCH();
 
     // Pass skipping needs the histogram on the host.
@@ -333,15 +117,15 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             if (h[p * kRadix + d] == n) constant = true;
         if (constant) continue;
         HPXHIP_CHECK(hipMemsetAsync(counter, 0, 256 + L.lb_bytes, s));
-        const dim3 grid(static_cast<unsigned>(L.ntiles)), block(kThreads);
+        const dim3 grid(static_cast<unsigned>(L.ntiles)), block(TS::threads);
         if (L.wide)
-            hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, unsigned long long, X>), grid, block, 0, s, kc, ka, vc,
-                               va, n, 8 * p, start + p * kRadix,
+            hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, unsigned long long, X, TS::threads, TS::items, TS::lbb>), grid,
+                               block, 0, s, kc, ka, vc, va, n, 8 * p, start + p * kRadix,
                                reinterpret_cast<unsigned long long*>(base + L.lb), counter, err, X{});
         else
-            hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, uint32_t, X>), grid, block, 0, s, kc, ka, vc, va, n,
-                               8 * p, start + p * kRadix, reinterpret_cast<uint32_t*>(base + L.lb), counter, err,
-                               X{});
+            hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, uint32_t, X, TS::threads, TS::items, TS::lbb>), grid, block, 0, s,
+                               kc, ka, vc, va, n, 8 * p, start + p * kRadix, reinterpret_cast<uint32_t*>(base + L.lb),
+                               counter, err, X{});
         HPXHIP_CHECK_LAUNCH();
         std::swap(kc, ka);
         std::swap(vc, va);
@@ -364,7 +148,10 @@ int dispatch_desc(int descending, void* keys, void* vals, uint64_t n, hipStream_
 
 namespace hpxhip {
 size_t sort_scratch_bytes(int key_dtype, int value_dtype, uint64_t n) {
-    return make_layout(n, dtype_size(key_dtype), value_dtype < 0 ? 0 : dtype_size(value_dtype)).total;
+    const bool has_val = value_dtype >= 0;
+    return make_layout(n, dtype_size(key_dtype), has_val ? dtype_size(value_dtype) : 0,
+                       has_val ? tile_shape<true>::tile : tile_shape<false>::tile)
+        .total;
 }
 }  // namespace hpxhip
 
