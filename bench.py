@@ -77,7 +77,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--cpu-logn", type=int, default=27)
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
+    ap.add_argument("--triad-only", action="store_true", help=argparse.SUPPRESS)  # PMC child mode
     args = ap.parse_args()
+    if args.triad_only:
+        return triad_only(args.logn)
 
     import hpx_amd as hpx
     from hpx_amd import _lib as L
@@ -190,6 +194,10 @@ def main():
     y.local.free()
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_logn)
+    if rank == 0 and world == 1 and not args.no_pmc:
+        traffic, detail = pmc_traffic(args.logn)
+        out["roofline"]["traffic"] = traffic
+        out["roofline"]["traffic_detail"] = detail
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -243,6 +251,61 @@ def extras(hpx, L, ex, F, tgt, pol, x, y, n_local, world):
     for v in st.U:
         v.free()
     return res
+
+
+def triad_only(logn):
+    """PMC child: the dominant kernel alone (3 launches over 2^logn doubles)."""
+    import hpx_amd as hpx
+    from hpx_amd import execution as ex, functional as F, parallel as P
+    t = hpx.target(0)
+    pol = ex.par.on(hpx.default_executor(t))
+    n = 1 << logn
+    a, b, c = (hpx.vector(n, dtype=np.float64, tgt=t) for _ in range(3))
+    P.generate(pol, b.begin(), b.end(), "unit", 1)
+    P.generate(pol, c.begin(), c.end(), "unit", 2)
+    for _ in range(3):
+        P.transform(pol, b.begin(), b.end(), c.begin(), c.end(), a.begin(), F.triad_step(3.0))
+    t.synchronize()
+
+
+def pmc_traffic(logn):
+    """HBM bytes per triad launch from rocprofv3 PMC counters, collected as
+    MI355X_MICROARCH.md's HBM/rocprofv3 section prescribes: FETCH_SIZE and
+    WRITE_SIZE in separate passes (TCC slots), kilobytes -> bytes, and
+    FETCH_SIZE doubled (gfx950 tallies 128-B streaming reads at 64 B)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, {"error": "rocprofv3 not found"}
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="hpxhip_pmc_", dir="/tmp")
+        cmd = [exe, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--triad-only", "--logn", str(logn)]
+        try:
+            subprocess.run(cmd, check=True, capture_output=True, timeout=300, cwd="/tmp",
+                           env=dict(os.environ, TMPDIR="/tmp"))
+        except Exception as e:  # noqa: BLE001 -- report, never fake a number
+            return None, {"error": f"{counter}: {type(e).__name__}"}
+        per = []
+        for root, _, files in os.walk(d):
+            for f in files:
+                if f.endswith("counter_collection.csv"):
+                    for row in csv.DictReader(open(os.path.join(root, f))):
+                        if "k_binary" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                            per.append(float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not per:
+            return None, {"error": f"{counter}: no k_binary rows"}
+        vals[counter] = sum(per) / len(per)
+    fetch = 2.0 * vals["FETCH_SIZE"] * 1024.0
+    write = vals["WRITE_SIZE"] * 1024.0
+    return round(fetch + write), {"FETCH_SIZE_kb_raw": vals["FETCH_SIZE"], "WRITE_SIZE_kb": vals["WRITE_SIZE"],
+                                  "read_bytes_corrected": round(fetch), "write_bytes": round(write),
+                                  "algorithmic_bytes": 24 * (1 << logn)}
 
 
 def cpu_baseline(logn):
