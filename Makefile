@@ -20,6 +20,14 @@ OFLAGS   := -O2 -fPIC -std=c++17 -ffp-contract=off -Wall -pthread
 
 .PHONY: all lib oracle clean cxxtests
 
+# C++ tests of include/hpx (plain g++ host code linked to the C ABI library)
+CXXT     := compute_api algorithms_known_answer stream_hip
+CXXTBIN  := $(CXXT:%=tests/cxx/bin/%)
+CXXHDR   := $(shell find include -name '*.hpp') include/hpxhip.h
+TFLAGS   := -O2 -std=c++17 -Wall -Wextra -Wno-unused-parameter -pthread -Iinclude
+TLINK    := -Lhpx_amd -lhpxhip -Wl,-rpath,'$$ORIGIN/../../../hpx_amd' -Wl,-rpath,/opt/rocm/lib \
+            -Wl,-rpath-link,/opt/rocm/lib
+
 all: lib oracle
 
 lib: $(LIB)
@@ -36,5 +44,11 @@ $(ORACLE): oracle/oracle.cpp oracle/oracle.h
 	@mkdir -p $(dir $@)
 	$(CXX) $(OFLAGS) -shared -o $@ oracle/oracle.cpp
 
+cxxtests: $(CXXTBIN)
+
+tests/cxx/bin/%: tests/cxx/%.cpp $(CXXHDR) $(LIB)
+	@mkdir -p $(dir $@)
+	$(CXX) $(TFLAGS) $< -o $@ $(TLINK)
+
 clean:
-	rm -rf $(BUILD) $(LIB) oracle/_build
+	rm -rf $(BUILD) $(LIB) oracle/_build tests/cxx/bin

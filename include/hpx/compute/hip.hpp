@@ -1,0 +1,497 @@
+// hpx/compute/hip.hpp -- header-only C++ mirror of HPX 1.4.0's hpx::compute
+// CUDA layer for the MI355X backend, on top of the C ABI in <hpxhip.h>.
+//
+//   hpx::compute::hip::target            <- hpx/compute/cuda/target.hpp:36-200,
+//                                           src/compute/cuda/cuda_target.cpp:97-317
+//   hpx::compute::hip::get_local_targets <- src/compute/cuda/get_cuda_targets.cpp:30-65
+//   hpx::compute::hip::allocator<T>      <- hpx/compute/cuda/allocator.hpp:36-259
+//   hpx::compute::hip::default_executor  <- hpx/compute/cuda/default_executor.hpp:42-260
+//   hpx::compute::vector<T, Alloc>       <- hpx/compute/vector.hpp:28-372
+//   device iterator + value_proxy        <- hpx/compute/detail/iterator.hpp:23-85,
+//                                           cuda/value_proxy.hpp:25-124
+//   hpx::future / make_ready_future      <- hpx/lcos/future.hpp (completion from a
+//                                           stream callback, cuda_target.cpp:97-142)
+//
+// Compiles with any C++17 host compiler (g++ is enough) and links against
+// hpx_amd/libhpxhip.so; there is no host fallback -- a failing call throws.
+#pragma once
+
+#include <hpxhip.h>
+
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <exception>
+#include <functional>
+#include <iterator>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <ostream>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+namespace hpx {
+
+// ------------------------------------------------------------------ errors
+// hpx::exception analogues for the error paths of the reference:
+// kernel_error (detail/launch.hpp:106-113), out_of_memory (allocator.hpp:118-124).
+struct exception : std::runtime_error {
+    int status;
+    exception(int s, std::string const& what) : std::runtime_error(what), status(s) {}
+};
+struct kernel_error : exception {
+    using exception::exception;
+};
+struct out_of_memory : std::bad_alloc {
+    std::string msg;
+    explicit out_of_memory(std::string m) : msg(std::move(m)) {}
+    const char* what() const noexcept override { return msg.c_str(); }
+};
+
+namespace compute { namespace hip { namespace detail {
+inline void check(int status, char const* what) {
+    if (status == HPXHIP_SUCCESS) return;
+    std::string msg = std::string(what) + ": " + hpxhip_error_string(status);
+    if (status == HPXHIP_ERROR_OUT_OF_MEMORY) throw out_of_memory(msg);
+    throw kernel_error(status, msg);
+}
+inline kernel_error check_noexcept(int status) {
+    return kernel_error(status, std::string("hip stream callback: ") + hpxhip_error_string(status));
+}
+}}}  // namespace compute::hip::detail
+
+// ------------------------------------------------------------------ future
+namespace lcos { namespace detail {
+template <typename T>
+struct shared_state {
+    std::mutex mtx;
+    std::condition_variable cv;
+    bool ready = false;
+    std::exception_ptr exc;
+    std::function<T()> value_fn;  // run once the device work is done
+    typename std::conditional<std::is_void<T>::value, int, T>::type value{};
+    std::vector<std::function<void()>> continuations;
+    std::once_flag evaluated;  // value_fn runs once, on the first get()
+
+    void set_ready(int status) {
+        std::vector<std::function<void()>> conts;
+        {
+            std::lock_guard<std::mutex> lk(mtx);
+            if (status != 0)
+                exc = std::make_exception_ptr(compute::hip::detail::check_noexcept(status));
+            ready = true;
+            conts.swap(continuations);
+        }
+        cv.notify_all();
+        for (auto& c : conts) c();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> lk(mtx);
+        cv.wait(lk, [&] { return ready; });
+    }
+};
+}}  // namespace lcos::detail
+
+template <typename T>
+class future {
+    using state = lcos::detail::shared_state<T>;
+    std::shared_ptr<state> st_;
+
+    void resolve() {
+        st_->wait();
+        std::call_once(st_->evaluated, [this] {
+            if (st_->exc || !st_->value_fn) return;
+            try {
+                if constexpr (std::is_void<T>::value) st_->value_fn();
+                else st_->value = st_->value_fn();
+            } catch (...) {
+                st_->exc = std::current_exception();
+            }
+        });
+    }
+
+public:
+    future() = default;
+    explicit future(std::shared_ptr<state> s) : st_(std::move(s)) {}
+    bool valid() const { return static_cast<bool>(st_); }
+    bool is_ready() const {
+        std::lock_guard<std::mutex> lk(st_->mtx);
+        return st_->ready;
+    }
+    void wait() { st_->wait(); }
+    T get() {
+        resolve();
+        if (st_->exc) std::rethrow_exception(st_->exc);
+        if constexpr (!std::is_void<T>::value) return st_->value;
+    }
+    bool has_exception() {
+        resolve();
+        return static_cast<bool>(st_->exc);
+    }
+    // hpx::future::then -- runs the continuation on the thread that calls get()
+    // on the returned future (deferred), after this future is ready.
+    template <typename F>
+    auto then(F&& f) -> future<decltype(f(std::declval<future<T>&>()))> {
+        using R = decltype(f(std::declval<future<T>&>()));
+        auto nst = std::make_shared<lcos::detail::shared_state<R>>();
+        auto self = std::make_shared<future<T>>(std::move(*this));
+        nst->value_fn = [self, f = std::forward<F>(f)]() mutable -> R { return f(*self); };
+        auto raw = nst;
+        auto parent = self->st_;
+        {
+            std::unique_lock<std::mutex> lk(parent->mtx);
+            if (!parent->ready) {
+                parent->continuations.push_back([raw] { raw->set_ready(0); });
+                return future<R>(nst);
+            }
+        }
+        nst->set_ready(0);
+        return future<R>(nst);
+    }
+    std::shared_ptr<state> const& shared() const { return st_; }
+};
+
+template <typename T>
+future<typename std::decay<T>::type> make_ready_future(T&& v) {
+    using V = typename std::decay<T>::type;
+    auto st = std::make_shared<lcos::detail::shared_state<V>>();
+    V val = std::forward<T>(v);
+    st->value_fn = [val]() { return val; };
+    st->set_ready(0);
+    return future<V>(st);
+}
+inline future<void> make_ready_future() {
+    auto st = std::make_shared<lcos::detail::shared_state<void>>();
+    st->set_ready(0);
+    return future<void>(st);
+}
+
+// when_all over a vector of futures: ready when all are (values via get()).
+template <typename T>
+future<std::vector<future<T>>> when_all(std::vector<future<T>>&& fs) {
+    auto st = std::make_shared<lcos::detail::shared_state<std::vector<future<T>>>>();
+    auto v = std::make_shared<std::vector<future<T>>>(std::move(fs));
+    st->value_fn = [v]() {
+        for (auto& f : *v) f.wait();
+        return std::move(*v);
+    };
+    st->set_ready(0);
+    return future<std::vector<future<T>>>(st);
+}
+
+namespace compute { namespace hip {
+
+// ------------------------------------------------------------------ target
+class target {
+    struct handle {
+        int device = 0;
+        hpxhip_stream stream = nullptr;
+        std::mutex mtx;  // lazy stream creation, cuda_target.cpp:257 spinlock
+        // Ring of 64-byte result slots (device + pinned host) through which
+        // reduce/copy_if results travel back without a per-call allocation.
+        void* dev_slots = nullptr;
+        void* host_slots = nullptr;
+        unsigned next_slot = 0;
+        ~handle() {
+            if (stream) hpxhip_stream_destroy(stream);
+            if (dev_slots) hpxhip_free(dev_slots);
+            if (host_slots) hpxhip_free_host(host_slots);
+        }
+    };
+    static constexpr unsigned kSlots = 1024, kSlotBytes = 64;
+    std::shared_ptr<handle> h_;
+
+public:
+    target() : target(0) {}
+    explicit target(int device) : h_(std::make_shared<handle>()) { h_->device = device; }
+    // a copy gets its own stream (cuda_target.cpp:203-211)
+    target(target const& o) : h_(std::make_shared<handle>()) { h_->device = o.h_->device; }
+    target& operator=(target const& o) {
+        if (this != &o) {
+            h_ = std::make_shared<handle>();
+            h_->device = o.h_->device;
+        }
+        return *this;
+    }
+    target(target&&) = default;
+    target& operator=(target&&) = default;
+
+    struct native_handle_type {
+        handle* h;
+        int get_device() const { return h->device; }
+        hpxhip_stream get_stream() const {
+            std::lock_guard<std::mutex> lk(h->mtx);
+            if (!h->stream) detail::check(hpxhip_stream_create(h->device, &h->stream), "hpxhip_stream_create");
+            return h->stream;
+        }
+    };
+    native_handle_type native_handle() const { return native_handle_type{h_.get()}; }
+    int device() const { return h_->device; }
+    hpxhip_stream stream() const { return native_handle().get_stream(); }
+
+    void synchronize() const {
+        detail::check(hpxhip_stream_synchronize(stream()), "hpxhip_stream_synchronize");
+        uint32_t code = 0;
+        detail::check(hpxhip_device_error(h_->device, &code), "hpxhip_device_error");
+        if (code) throw kernel_error(HPXHIP_ERROR_DEVICE_TIMEOUT, "device kernel error word set");
+    }
+
+    // cuda_target.cpp:307-317: a future that becomes ready when all work queued
+    // so far on the stream is done; completed from the HIP callback thread.
+    future<void> get_future() const {
+        return async_result<void>([] {});
+    }
+
+    // A future completed from a stream callback once all work queued so far
+    // is done; fn() (e.g. reading a pinned result slot) runs on the first
+    // get(), after the device error word is checked.
+    template <typename R>
+    future<R> async_result(std::function<R()> fn) const {
+        using S = lcos::detail::shared_state<R>;
+        auto st = std::make_shared<S>();
+        int dev = h_->device;
+        st->value_fn = [dev, fn = std::move(fn)]() -> R {
+            uint32_t code = 0;
+            detail::check(hpxhip_device_error(dev, &code), "hpxhip_device_error");
+            if (code) throw kernel_error(HPXHIP_ERROR_DEVICE_TIMEOUT, "device kernel error word set");
+            return fn();
+        };
+        auto* keep = new std::shared_ptr<S>(st);  // owned by the callback
+        int rc = hpxhip_stream_add_callback(
+            stream(),
+            [](void* p, int status) {
+                auto* sp = static_cast<std::shared_ptr<S>*>(p);
+                (*sp)->set_ready(status);
+                delete sp;
+            },
+            keep);
+        if (rc != HPXHIP_SUCCESS) {
+            delete keep;
+            detail::check(rc, "hpxhip_stream_add_callback");
+        }
+        return future<R>(st);
+    }
+
+    // (device slot, host slot) pair; the host slot is filled by an async D2H
+    // copy queued after the kernel that writes the device slot.
+    std::pair<void*, void*> result_slot() const {
+        std::lock_guard<std::mutex> lk(h_->mtx);
+        if (!h_->dev_slots) {
+            detail::check(hpxhip_malloc(h_->device, &h_->dev_slots, kSlots * kSlotBytes), "result slots");
+            detail::check(hpxhip_malloc_host(&h_->host_slots, kSlots * kSlotBytes), "result slots");
+        }
+        unsigned i = h_->next_slot++ % kSlots;
+        return {static_cast<char*>(h_->dev_slots) + i * kSlotBytes,
+                static_cast<char*>(h_->host_slots) + i * kSlotBytes};
+    }
+
+    std::size_t processing_units() const {
+        hpxhip_device_props p;
+        detail::check(hpxhip_device_props_get(h_->device, &p), "hpxhip_device_props_get");
+        return static_cast<std::size_t>(p.compute_units);
+    }
+
+    friend bool operator==(target const& a, target const& b) { return a.h_->device == b.h_->device; }
+    friend bool operator!=(target const& a, target const& b) { return !(a == b); }
+};
+
+inline std::vector<target> get_local_targets() {
+    int n = 0;
+    detail::check(hpxhip_get_device_count(&n), "hpxhip_get_device_count");
+    std::vector<target> ts;
+    for (int i = 0; i < n; ++i) ts.emplace_back(i);
+    return ts;
+}
+
+template <typename T>
+struct dtype_of;
+template <> struct dtype_of<int32_t> { static constexpr int value = HPXHIP_I32; };
+template <> struct dtype_of<uint32_t> { static constexpr int value = HPXHIP_U32; };
+template <> struct dtype_of<int64_t> { static constexpr int value = HPXHIP_I64; };
+template <> struct dtype_of<uint64_t> { static constexpr int value = HPXHIP_U64; };
+template <> struct dtype_of<float> { static constexpr int value = HPXHIP_F32; };
+template <> struct dtype_of<double> { static constexpr int value = HPXHIP_F64; };
+#if defined(__LP64__) && !defined(_WIN32)
+template <> struct dtype_of<long long> { static constexpr int value = HPXHIP_I64; };
+template <> struct dtype_of<unsigned long long> { static constexpr int value = HPXHIP_U64; };
+#endif
+
+// --------------------------------------------------------------- allocator
+template <typename T>
+class allocator {
+    hip::target target_;
+
+public:
+    using value_type = T;
+    using pointer = T*;
+    using const_pointer = T const*;
+    using size_type = std::size_t;
+    using difference_type = std::ptrdiff_t;
+    using target_type = hip::target;
+    template <typename U>
+    struct rebind {
+        using other = allocator<U>;
+    };
+
+    allocator() = default;
+    explicit allocator(hip::target const& t) : target_(t) {}
+    template <typename U>
+    allocator(allocator<U> const& o) : target_(o.target()) {}
+
+    target_type const& target() const { return target_; }
+
+    pointer allocate(size_type n) {
+        void* p = nullptr;
+        detail::check(hpxhip_malloc(target_.device(), &p, n * sizeof(T)), "hip::allocator::allocate");
+        return static_cast<pointer>(p);
+    }
+    void deallocate(pointer p, size_type) {
+        if (p) hpxhip_free(p);
+    }
+    size_type max_size() const {
+        size_t free_b = 0, total = 0;
+        detail::check(hpxhip_mem_info(target_.device(), &free_b, &total), "hip::allocator::max_size");
+        return total / sizeof(T);
+    }
+    // Documented deviation: bulk_construct value-initialises on the device
+    // (the reference's host path leaves memory uninitialised, allocator.hpp:173-195).
+    void bulk_construct(pointer p, size_type n, T const& v = T()) {
+        if (!n) return;
+        detail::check(hpxhip_fill(dtype_of<T>::value, &v, p, n, target_.stream()), "hip::allocator::bulk_construct");
+        target_.synchronize();
+    }
+    void bulk_destroy(pointer, size_type) {}  // trivially destructible element types only
+};
+
+// --------------------------------------------------------- device iterator
+template <typename T>
+class value_proxy {
+    T* p_;
+    hip::target const* t_;
+
+public:
+    value_proxy(T* p, hip::target const* t) : p_(p), t_(t) {}
+    operator T() const {
+        T v;
+        detail::check(hpxhip_memcpy_async(&v, p_, sizeof(T), HPXHIP_D2H, t_->stream()), "value_proxy read");
+        t_->synchronize();
+        return v;
+    }
+    value_proxy& operator=(T const& v) {
+        detail::check(hpxhip_memcpy_async(p_, &v, sizeof(T), HPXHIP_H2D, t_->stream()), "value_proxy write");
+        t_->synchronize();
+        return *this;
+    }
+    friend std::ostream& operator<<(std::ostream& os, value_proxy const& v) { return os << T(v); }
+};
+
+template <typename T>
+class device_iterator {
+    T* p_ = nullptr;
+    hip::target const* t_ = nullptr;
+
+public:
+    using iterator_category = std::random_access_iterator_tag;
+    using value_type = T;
+    using difference_type = std::ptrdiff_t;
+    using pointer = T*;
+    using reference = value_proxy<T>;
+    using target_type = hip::target;
+
+    device_iterator() = default;
+    device_iterator(T* p, hip::target const* t) : p_(p), t_(t) {}
+    T* device_ptr() const { return p_; }
+    hip::target const& target() const { return *t_; }
+
+    reference operator*() const { return reference(p_, t_); }
+    reference operator[](difference_type i) const { return reference(p_ + i, t_); }
+    device_iterator& operator++() { ++p_; return *this; }
+    device_iterator operator++(int) { auto r = *this; ++p_; return r; }
+    device_iterator& operator--() { --p_; return *this; }
+    device_iterator& operator+=(difference_type n) { p_ += n; return *this; }
+    device_iterator& operator-=(difference_type n) { p_ -= n; return *this; }
+    friend device_iterator operator+(device_iterator a, difference_type n) { return a += n; }
+    friend device_iterator operator+(difference_type n, device_iterator a) { return a += n; }
+    friend device_iterator operator-(device_iterator a, difference_type n) { return a -= n; }
+    friend difference_type operator-(device_iterator const& a, device_iterator const& b) { return a.p_ - b.p_; }
+    friend bool operator==(device_iterator const& a, device_iterator const& b) { return a.p_ == b.p_; }
+    friend bool operator!=(device_iterator const& a, device_iterator const& b) { return a.p_ != b.p_; }
+    friend bool operator<(device_iterator const& a, device_iterator const& b) { return a.p_ < b.p_; }
+};
+
+template <typename It>
+struct is_device_iterator : std::false_type {};
+template <typename T>
+struct is_device_iterator<device_iterator<T>> : std::true_type {};
+
+// ----------------------------------------------------------------- executors
+class default_executor {
+    hip::target target_;
+
+public:
+    using execution_category = struct parallel_execution_tag {};
+    using executor_parameters_type = void;
+
+    default_executor() = default;
+    explicit default_executor(hip::target const& t) : target_(t) {}
+    hip::target const& target() const { return target_; }
+    hip::target const& context() const { return target_; }
+    std::size_t processing_units_count() const { return target_.processing_units(); }
+    friend bool operator==(default_executor const& a, default_executor const& b) { return a.target_ == b.target_; }
+};
+
+}}  // namespace compute::hip
+
+namespace compute {
+
+// ------------------------------------------------------------------ vector
+template <typename T, typename Allocator = hip::allocator<T>>
+class vector {
+    Allocator alloc_;
+    std::size_t size_ = 0;
+    T* data_ = nullptr;
+
+public:
+    using value_type = T;
+    using allocator_type = Allocator;
+    using size_type = std::size_t;
+    using iterator = hip::device_iterator<T>;
+    using const_iterator = hip::device_iterator<T>;
+
+    vector() = default;
+    explicit vector(size_type n, Allocator const& a = Allocator()) : alloc_(a), size_(n) {
+        data_ = alloc_.allocate(n);
+        alloc_.bulk_construct(data_, n);
+    }
+    vector(size_type n, T const& v, Allocator const& a = Allocator()) : alloc_(a), size_(n) {
+        data_ = alloc_.allocate(n);
+        alloc_.bulk_construct(data_, n, v);
+    }
+    vector(vector const&) = delete;
+    vector& operator=(vector const&) = delete;
+    vector(vector&& o) noexcept : alloc_(o.alloc_), size_(o.size_), data_(o.data_) {
+        o.data_ = nullptr;
+        o.size_ = 0;
+    }
+    ~vector() {
+        if (data_) alloc_.deallocate(data_, size_);
+    }
+
+    size_type size() const { return size_; }
+    size_type capacity() const { return size_; }
+    bool empty() const { return size_ == 0; }
+    T* device_data() const { return data_; }
+    T* data() const { return data_; }
+    allocator_type const& get_allocator() const { return alloc_; }
+    iterator begin() const { return iterator(data_, &alloc_.target()); }
+    iterator end() const { return iterator(data_ + size_, &alloc_.target()); }
+    hip::value_proxy<T> operator[](size_type i) const { return hip::value_proxy<T>(data_ + i, &alloc_.target()); }
+};
+
+}  // namespace compute
+}  // namespace hpx

@@ -1,0 +1,5 @@
+// hpx/hpx.hpp -- umbrella header of the HIP backend's HPX mirror.
+#pragma once
+#include <hpx/include/compute.hpp>
+#include <hpx/parallel/algorithms.hpp>
+#include <hpx/parallel/execution.hpp>

@@ -1,0 +1,5 @@
+// hpx/include/compute.hpp -- HIP counterpart of the reference's compute umbrella
+// (hpx/include/compute.hpp: target, allocator, executors, vector).
+#pragma once
+#include <hpx/compute/hip.hpp>
+#include <hpx/compute/hip/functional.hpp>

@@ -1,0 +1,3 @@
+// hpx/include/parallel_sort.hpp -- forwards to the HIP backend's algorithm layer.
+#pragma once
+#include <hpx/parallel/algorithms.hpp>

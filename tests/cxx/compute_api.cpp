@@ -1,0 +1,196 @@
+// C++ drop-in check of the HIP backend's HPX compute API: the shape of the
+// reference's tests/unit/computeapi/cuda/{for_each_compute,transform_compute}.cu
+// (target, allocator, compute::vector, default_executor, par.on(exec),
+// copy to and from the host, value_proxy element access), plus futures from
+// task policies (cuda_future.cpp) and the error paths.
+//
+// Built against include/ and hpx_amd/libhpxhip.so by `make cxxtests`; run by
+// tests/test_cxx_api.py under pytest -m gpu.
+#include <hpx/hpx.hpp>
+#include <hpx/hpx_init.hpp>
+#include <hpx/util/lightweight_test.hpp>
+
+#include <cstdint>
+#include <cstdlib>
+#include <iostream>
+#include <numeric>
+#include <random>
+#include <vector>
+
+using executor_type = hpx::compute::hip::default_executor;
+using target_allocator = hpx::compute::hip::allocator<int>;
+using target_vector = hpx::compute::vector<int, target_allocator>;
+namespace fn = hpx::compute::hip::functional;
+namespace ex = hpx::parallel::execution;
+
+// transform_compute.cu:29-40 defines `int operator()(a, b) { return a + 3.0 * b; }`;
+// a user functor reaches the device by declaring which built-in op it is.
+struct transform_test {
+    template <typename T>
+    int operator()(T const& a, T const& b) const {
+        return a + 3.0 * b;
+    }
+};
+template <>
+struct hpx::compute::hip::traits::binary<transform_test> {
+    static constexpr int kind = HPXHIP_B_TRIAD;
+    using compute_type = double;
+    template <typename C>
+    static void scalars(transform_test const&, C* s) {
+        s[0] = C(3.0);
+    }
+};
+
+// for_each_compute.cu:40 `i += 5`
+void test_for_each(executor_type& exec, target_vector& d_A) {
+    std::vector<int> h_C(d_A.size());
+    hpx::parallel::copy(ex::par, d_A.begin(), d_A.end(), h_C.begin());
+    hpx::parallel::for_each(ex::par.on(exec), d_A.begin(), d_A.end(), fn::add_value<int>{5});
+    std::vector<int> h_A(d_A.size());
+    hpx::parallel::copy(ex::par, d_A.begin(), d_A.end(), h_A.begin());
+    for (std::size_t i = 0; i != h_C.size(); ++i) {
+        if (!HPX_TEST_EQ(h_C[i] + 5, h_A[i])) break;
+        if (i < 16) HPX_TEST_EQ(h_C[i] + 5, d_A[i]);  // value_proxy reads (one D2H each)
+    }
+}
+
+void test_transform(executor_type& exec, target_vector& d_A, target_vector& d_B, target_vector& d_C,
+                    std::vector<int> const& ref) {
+    auto r = hpx::parallel::transform(ex::par.on(exec), d_A.begin(), d_A.end(), d_B.begin(), d_C.begin(),
+                                      transform_test());
+    HPX_TEST(r.out() == d_C.end());
+    HPX_TEST(r.in1() == d_A.end());
+    std::vector<int> h_C(d_C.size());
+    hpx::parallel::copy(ex::par, d_C.begin(), d_C.end(), h_C.begin());
+    HPX_TEST_EQ(h_C.size(), ref.size());
+    HPX_TEST_EQ(d_C.size(), ref.size());
+    for (std::size_t i = 0; i != ref.size(); ++i) {
+        if (!HPX_TEST_EQ(h_C[i], ref[i])) break;
+        if (i < 16) HPX_TEST_EQ(d_C[i], ref[i]);  // value_proxy reads (one D2H each)
+    }
+}
+
+void test_targets_and_vector() {
+    auto targets = hpx::compute::hip::get_local_targets();
+    HPX_TEST(!targets.empty());
+    hpx::compute::hip::target t;
+    HPX_TEST(t.processing_units() > 0);
+    HPX_TEST(t.native_handle().get_stream() != nullptr);
+
+    hpx::compute::hip::allocator<double> alloc(t);
+    HPX_TEST(alloc.max_size() > (std::size_t(1) << 30));
+    hpx::compute::vector<double, hpx::compute::hip::allocator<double>> v(1000, 2.5, alloc);
+    HPX_TEST_EQ(v.size(), std::size_t(1000));
+    HPX_TEST_EQ(double(v[999]), 2.5);
+    v[3] = 7.0;
+    HPX_TEST_EQ(double(v[3]), 7.0);
+    hpx::compute::vector<double, hpx::compute::hip::allocator<double>> z(17, alloc);  // value-initialised
+    HPX_TEST_EQ(double(z[16]), 0.0);
+    // move keeps the allocation
+    auto moved = std::move(v);
+    HPX_TEST_EQ(moved.size(), std::size_t(1000));
+    HPX_TEST_EQ(double(moved[3]), 7.0);
+}
+
+void test_futures(executor_type& exec) {
+    hpx::compute::hip::target t;
+    hpx::compute::hip::allocator<double> alloc(t);
+    std::size_t const n = 1 << 20;
+    hpx::compute::vector<double, hpx::compute::hip::allocator<double>> a(n, 1.0, alloc), b(n, 2.0, alloc),
+        c(n, alloc);
+    hpx::compute::hip::default_executor dexec(t);
+    auto pol = ex::par(ex::task).on(dexec);
+
+    hpx::future<void> f = hpx::parallel::fill(pol, c.begin(), c.end(), 0.5);
+    f.get();
+    auto tf = hpx::parallel::transform(pol, a.begin(), a.end(), b.begin(), c.begin(), fn::triad_step<double>{3.0});
+    auto r = tf.get();
+    HPX_TEST(r.out() == c.end());
+    HPX_TEST_EQ(double(c[n - 1]), 7.0);
+
+    // reduce as a future, chained with then()
+    hpx::future<double> s = hpx::parallel::reduce(pol, c.begin(), c.end(), 0.0);
+    auto twice = s.then([](hpx::future<double>& x) { return 2.0 * x.get(); });
+    HPX_TEST_EQ(twice.get(), 14.0 * double(n));
+
+    // target future: ready once all queued work is done
+    hpx::parallel::for_each(pol, c.begin(), c.end(), fn::multiply_step<double>{0.5});
+    auto tgt_done = dexec.target().get_future();
+    tgt_done.get();
+    HPX_TEST(tgt_done.is_ready());
+    HPX_TEST_EQ(double(c[0]), 3.5);
+
+    // when_all over futures of independent reductions
+    std::vector<hpx::future<double>> fs;
+    fs.push_back(hpx::parallel::reduce(pol, a.begin(), a.end(), 0.0));
+    fs.push_back(hpx::parallel::reduce(pol, b.begin(), b.end(), 0.0));
+    auto all = hpx::when_all(std::move(fs)).get();
+    HPX_TEST_EQ(all[0].get(), double(n));
+    HPX_TEST_EQ(all[1].get(), 2.0 * double(n));
+
+    auto ready = hpx::make_ready_future(42);
+    HPX_TEST_EQ(ready.get(), 42);
+    (void)exec;
+}
+
+void test_errors() {
+    hpx::compute::hip::target t;
+    hpx::compute::hip::allocator<float> alloc(t);
+    bool threw = false;
+    try {
+        (void)alloc.allocate(std::size_t(1) << 60);  // far beyond HBM
+    } catch (hpx::out_of_memory const&) {
+        threw = true;
+    } catch (std::bad_alloc const&) {
+        threw = true;
+    }
+    HPX_TEST(threw);
+
+    // reduce conversion not built for reductions (NEGATE) -> kernel_error, not a host fallback
+    hpx::compute::vector<float, hpx::compute::hip::allocator<float>> v(64, 1.0f, alloc);
+    threw = false;
+    try {
+        (void)hpx::parallel::transform_reduce(ex::par, v.begin(), v.end(), 0.0f, std::plus<float>(), fn::negate{});
+    } catch (hpx::kernel_error const& e) {
+        threw = (e.status == HPXHIP_ERROR_UNSUPPORTED);
+    }
+    HPX_TEST(threw);
+}
+
+int hpx_main(int argc, char* argv[]) {
+    unsigned seed = argc > 1 ? unsigned(std::strtoul(argv[1], nullptr, 10)) : std::random_device{}();
+    std::cout << "using seed: " << seed << std::endl;
+    std::mt19937 gen(seed);
+    std::uniform_int_distribution<> dis(2, 101);
+
+    for (int N : {100, 10007, 1 << 20}) {
+        std::vector<int> h_A(N), h_B(N);
+        std::iota(h_A.begin(), h_A.end(), dis(gen));
+        std::iota(h_B.begin(), h_B.end(), dis(gen));
+
+        hpx::compute::hip::target target;
+        target_allocator alloc(target);
+        target_vector d_A(N, alloc), d_B(N, alloc), d_C(N, alloc);
+        hpx::parallel::copy(ex::par, h_A.begin(), h_A.end(), d_A.begin());
+        hpx::parallel::copy(ex::par, h_B.begin(), h_B.end(), d_B.begin());
+
+        std::vector<int> ref(N);
+        std::transform(h_A.begin(), h_A.end(), h_B.begin(), ref.begin(), transform_test());
+
+        executor_type exec(target);
+        test_transform(exec, d_A, d_B, d_C, ref);
+        test_for_each(exec, d_A);
+    }
+    test_targets_and_vector();
+    executor_type exec;
+    test_futures(exec);
+    test_errors();
+    return hpx::finalize();
+}
+
+int main(int argc, char* argv[]) {
+    HPX_TEST_EQ(hpx::init(argc, argv), 0);
+    int errors = hpx::util::report_errors();
+    if (!errors) std::cout << "compute_api: all tests passed" << std::endl;
+    return errors;
+}
