@@ -93,6 +93,12 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     stream = tgt.stream
     pol = ex.par.on(hpx.default_executor(tgt))
+    # The step runs under par(task), as an HPX program composes asynchronous
+    # algorithms: each call returns a future and the work is ordered on the
+    # target's stream, so no host round trip sits between the three kernels.
+    # The reduce value is taken (get()) once the scan is enqueued; every step
+    # still completes and is checked (scan-last == reduce) below.
+    pol_task = ex.par(ex.task).on(hpx.default_executor(tgt))
     seg = S.algorithms
 
     n_local = 1 << args.logn
@@ -113,15 +119,15 @@ def main():
 
     def step(timed):
         e0 = ev.record(stream) if timed else None
-        seg.transform_binary(pol, b.begin(), b.end(), c.begin(), a.begin(), triad)
+        seg.transform_binary(pol_task, b.begin(), b.end(), c.begin(), a.begin(), triad)
         e1 = ev.record(stream) if timed else None
-        r = seg.reduce(pol, x.begin(), x.end(), 0, F.plus)
+        fr = seg.reduce(pol_task, x.begin(), x.end(), 0, F.plus)
         e2 = ev.record(stream) if timed else None
-        seg.inclusive_scan(pol, x.begin(), x.end(), y.begin(), F.plus, 0)
+        seg.inclusive_scan(pol_task, x.begin(), x.end(), y.begin(), F.plus, 0)
         e3 = ev.record(stream) if timed else None
         if timed:
             marks.append((e0, e1, e2, e3))
-        return r
+        return fr.get()
 
     for _ in range(args.warmup):
         step(False)

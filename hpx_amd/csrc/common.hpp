@@ -96,6 +96,41 @@ struct vec_width {
 };
 
 // ---------------------------------------------------------------------------
+// Streaming accesses: `global_load/store ... nt` (nontemporal cache policy).
+// Measured on MI355X at 2^30 doubles (scripts/ubench/{rd2,ew2}.hip,
+// profiles/r01_ubench_nt.log): read stream 6.36 -> 6.91 TB/s, triad 6.16 ->
+// 6.73 TB/s with both loads and stores nt, copy 6.34 -> 6.71 TB/s.  A
+// write-only stream (fill) is faster with plain stores (6.94 vs 6.79), so
+// the kernels choose per access.  Data touched this way is read once; the
+// policy bit changes caching only, never the value or its visibility at the
+// next kernel boundary.
+template <typename T>
+struct nt_word {
+    using type = std::conditional_t<
+        sizeof(T) == 16, uint32_t __attribute__((ext_vector_type(4))),
+        std::conditional_t<sizeof(T) == 8, uint64_t,
+                           std::conditional_t<sizeof(T) == 4, uint32_t,
+                                              std::conditional_t<sizeof(T) == 2, uint16_t, uint8_t>>>>;
+};
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+    using W = typename nt_word<T>::type;
+    static_assert(sizeof(W) == sizeof(T), "ld_stream: unsupported width");
+    const W w = __builtin_nontemporal_load(reinterpret_cast<const W*>(p));
+    T v;
+    __builtin_memcpy(&v, &w, sizeof(T));
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ void st_stream(T* p, const T& v) {
+    using W = typename nt_word<T>::type;
+    static_assert(sizeof(W) == sizeof(T), "st_stream: unsupported width");
+    W w;
+    __builtin_memcpy(&w, &v, sizeof(T));
+    __builtin_nontemporal_store(w, reinterpret_cast<W*>(p));
+}
+
+// ---------------------------------------------------------------------------
 // Bit casts between T and 32-bit lanes (DPP moves 32 bits per lane).
 template <typename T>
 __device__ __forceinline__ void to_words(T x, uint32_t (&w)[(sizeof(T) + 3) / 4]) {

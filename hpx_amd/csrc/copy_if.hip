@@ -6,8 +6,9 @@
 // Here: one pass.  Each wave evaluates the predicate on 64 lanes x 16 B,
 // ranks hits with `ballot` + `mbcnt` (no flag array in HBM), the tile's hit
 // count goes through the same decoupled look-back as the scan
-// (lookback.hpp), and hits are written to out[prefix + rank] -- consecutive
-// addresses within a wave round.  Traffic: 8 B read + 8 B x selectivity
+// (lookback.hpp), and hits are written to out[prefix + rank]: each wave
+// round's hits are compacted through LDS and stored by consecutive lanes.
+// Input loads are nontemporal.  Traffic: 8 B read + 8 B x selectivity
 // written per int64 element.
 #include "internal.hpp"
 #include "lookback.hpp"
@@ -46,6 +47,7 @@ __global__ __launch_bounds__(kThreads) void k_copy_if(const T* in, T* out, uint6
     __shared__ uint32_t s_tile;
     __shared__ uint32_t s_wave_total[kWaves];
     __shared__ uint64_t s_prefix;
+    __shared__ T s_stage[kWaves][kWave * V];  // one wave round of hits, compacted
 
     if (threadIdx.x == 0)
         s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(kThreads) void k_copy_if(const T* in, T* out, uint6
     if (ALIGNED && full) {
         const VT* src = reinterpret_cast<const VT*>(in + wbase);
 #pragma unroll
-        for (int r = 0; r < kRounds; ++r) x[r] = src[r * kWave + lane];
+        for (int r = 0; r < kRounds; ++r) x[r] = ld_stream(&src[r * kWave + lane]);
 #pragma unroll
         for (int r = 0; r < kRounds; ++r)
 #pragma unroll
@@ -125,12 +127,32 @@ __global__ __launch_bounds__(kThreads) void k_copy_if(const T* in, T* out, uint6
         }
     }
     __syncthreads();
+    // Write-out: per wave round, the hits are compacted into LDS at their
+    // round-local rank and stored back by consecutive lanes, so each store
+    // instruction covers one contiguous run of the output (a direct
+    // out[base + rank] scatter leaves holes in every wave store).
     const uint64_t base = s_prefix + wave_prefix;
+    T* stage = s_stage[wave];
+    uint32_t round_base = 0;
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r)
+    for (int r = 0; r < kRounds; ++r) {
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int e = 0; e < V; ++e) cnt += __builtin_popcountll(__ballot((hit >> (r * V + e)) & 1u));
 #pragma unroll
         for (int e = 0; e < V; ++e)
-            if ((hit >> (r * V + e)) & 1u) out[base + rank[r][e]] = x[r].v[e];
+            if ((hit >> (r * V + e)) & 1u) stage[rank[r][e] - round_base] = x[r].v[e];
+        // LDS is in order within a wave; the wait + clobber keep the compiler
+        // from hoisting the reads above the writes of other lanes.
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const uint32_t j = k * kWave + lane;
+            if (j < cnt) out[base + round_base + j] = stage[j];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next round's writes
+        round_base += cnt;
+    }
 }
 
 __global__ void k_zero_count(uint64_t* c) {

@@ -9,6 +9,9 @@
 //     launch vs 5.1 TB/s for a 2048-block grid-stride loop with 4 vectors
 //     in flight per thread -- scripts/ubench/ew.hip); the loop only strides
 //     when the range exceeds 2^31-1 blocks.  64-bit indexing throughout;
+//   * read+write kernels use 64-thread blocks and nontemporal (`nt`) loads
+//     and stores: triad 6.16 -> 6.73 TB/s (scripts/ubench/ew2.hip); the
+//     write-only fill keeps plain stores on 256-thread blocks (6.94 TB/s);
 //   * a head (to reach 16-B alignment) and a tail handled inside the same
 //     launch, so any iterator offset works; ranges whose arrays cannot all
 //     be aligned together fall back to the scalar (V = 1) instantiation.
@@ -20,8 +23,8 @@ using namespace hpxhip;
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kUnroll = 1;
+constexpr int kThreads = 256;     // fill / generate (write-only streams)
+constexpr int kRwThreads = 64;    // transform / copy / for_each (read + write streams)
 
 // Geometry: vector part of [0, nvec) processed grid-stride, each thread
 // handling vectors i, i+S, ..., i+(U-1)S per iteration (coalesced per
@@ -32,8 +35,8 @@ struct span3 {
     uint64_t tail;  // scalar elements after the vector part
 };
 
-inline unsigned grid_for(uint64_t work_items) {
-    const uint64_t per_block = static_cast<uint64_t>(kThreads) * kUnroll;
+inline unsigned grid_for(uint64_t work_items, int threads = kThreads) {
+    const uint64_t per_block = static_cast<uint64_t>(threads);
     uint64_t blocks = (work_items + per_block - 1) / per_block;
     const uint64_t cap = 0x7fffffffull;
     if (blocks > cap) blocks = cap;
@@ -43,11 +46,11 @@ inline unsigned grid_for(uint64_t work_items) {
 
 // out[i] = (TO) f((C) in[i])
 template <typename TI, typename C, typename TO, typename F, int V>
-__global__ __launch_bounds__(kThreads) void k_unary(const TI* in, TO* out, span3 sp, F f) {
+__global__ __launch_bounds__(kRwThreads) void k_unary(const TI* in, TO* out, span3 sp, F f) {
     using VI = vec<TI, V>;
     using VO = vec<TO, V>;
-    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kRwThreads + threadIdx.x;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kRwThreads;
 
     // Head and tail: scalar, first threads of the grid.
     if (tid < sp.head) out[tid] = static_cast<TO>(f(static_cast<C>(in[tid])));
@@ -56,33 +59,22 @@ __global__ __launch_bounds__(kThreads) void k_unary(const TI* in, TO* out, span3
 
     const VI* vin = reinterpret_cast<const VI*>(in + sp.head);
     VO* vout = reinterpret_cast<VO*>(out + sp.head);
-    for (uint64_t i = tid; i < sp.nvec; i += stride * kUnroll) {
-        VI x[kUnroll];
+    for (uint64_t i = tid; i < sp.nvec; i += stride) {
+        const VI x = ld_stream(&vin[i]);
+        VO y;
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const uint64_t j = i + u * stride;
-            if (j < sp.nvec) x[u] = vin[j];
-        }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const uint64_t j = i + u * stride;
-            if (j < sp.nvec) {
-                VO y;
-#pragma unroll
-                for (int e = 0; e < V; ++e) y.v[e] = static_cast<TO>(f(static_cast<C>(x[u].v[e])));
-                vout[j] = y;
-            }
-        }
+        for (int e = 0; e < V; ++e) y.v[e] = static_cast<TO>(f(static_cast<C>(x.v[e])));
+        st_stream(&vout[i], y);
     }
 }
 
 // out[i] = (TO) f((C) a[i], (C) b[i])
 template <typename TI, typename C, typename TO, typename F, int V>
-__global__ __launch_bounds__(kThreads) void k_binary(const TI* a, const TI* b, TO* out, span3 sp, F f) {
+__global__ __launch_bounds__(kRwThreads) void k_binary(const TI* a, const TI* b, TO* out, span3 sp, F f) {
     using VI = vec<TI, V>;
     using VO = vec<TO, V>;
-    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kRwThreads + threadIdx.x;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kRwThreads;
 
     if (tid < sp.head) out[tid] = static_cast<TO>(f(static_cast<C>(a[tid]), static_cast<C>(b[tid])));
     const uint64_t tail0 = sp.head + sp.nvec * V;
@@ -92,27 +84,13 @@ __global__ __launch_bounds__(kThreads) void k_binary(const TI* a, const TI* b, T
     const VI* va = reinterpret_cast<const VI*>(a + sp.head);
     const VI* vb = reinterpret_cast<const VI*>(b + sp.head);
     VO* vout = reinterpret_cast<VO*>(out + sp.head);
-    for (uint64_t i = tid; i < sp.nvec; i += stride * kUnroll) {
-        VI x[kUnroll], y[kUnroll];
+    for (uint64_t i = tid; i < sp.nvec; i += stride) {
+        const VI x = ld_stream(&va[i]);
+        const VI y = ld_stream(&vb[i]);
+        VO z;
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const uint64_t j = i + u * stride;
-            if (j < sp.nvec) {
-                x[u] = va[j];
-                y[u] = vb[j];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const uint64_t j = i + u * stride;
-            if (j < sp.nvec) {
-                VO z;
-#pragma unroll
-                for (int e = 0; e < V; ++e)
-                    z.v[e] = static_cast<TO>(f(static_cast<C>(x[u].v[e]), static_cast<C>(y[u].v[e])));
-                vout[j] = z;
-            }
-        }
+        for (int e = 0; e < V; ++e) z.v[e] = static_cast<TO>(f(static_cast<C>(x.v[e]), static_cast<C>(y.v[e])));
+        st_stream(&vout[i], z);
     }
 }
 
@@ -161,11 +139,12 @@ int launch_unary(const TI* in, TO* out, uint64_t n, F f, hipStream_t s) {
     constexpr int V = VW < 1 ? 1 : VW;
     span3 sp;
     if ((sizeof(TI) == sizeof(TO)) && make_span<V>(n, sizeof(TI), &sp, {in, out})) {
-        hipLaunchKernelGGL((k_unary<TI, C, TO, F, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail)),
-                           dim3(kThreads), 0, s, in, out, sp, f);
+        hipLaunchKernelGGL((k_unary<TI, C, TO, F, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail, kRwThreads)),
+                           dim3(kRwThreads), 0, s, in, out, sp, f);
     } else {
         sp = span3{0, n, 0};
-        hipLaunchKernelGGL((k_unary<TI, C, TO, F, 1>), dim3(grid_for(n)), dim3(kThreads), 0, s, in, out, sp, f);
+        hipLaunchKernelGGL((k_unary<TI, C, TO, F, 1>), dim3(grid_for(n, kRwThreads)), dim3(kRwThreads), 0, s, in, out,
+                           sp, f);
     }
     HPXHIP_CHECK_LAUNCH();
     return 0;
@@ -177,12 +156,12 @@ int launch_binary(const TI* a, const TI* b, TO* out, uint64_t n, F f, hipStream_
     constexpr int V = VW < 1 ? 1 : VW;
     span3 sp;
     if ((sizeof(TI) == sizeof(TO)) && make_span<V>(n, sizeof(TI), &sp, {a, b, out})) {
-        hipLaunchKernelGGL((k_binary<TI, C, TO, F, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail)),
-                           dim3(kThreads), 0, s, a, b, out, sp, f);
+        hipLaunchKernelGGL((k_binary<TI, C, TO, F, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail, kRwThreads)),
+                           dim3(kRwThreads), 0, s, a, b, out, sp, f);
     } else {
         sp = span3{0, n, 0};
-        hipLaunchKernelGGL((k_binary<TI, C, TO, F, 1>), dim3(grid_for(n)), dim3(kThreads), 0, s, a, b, out,
-                           sp, f);
+        hipLaunchKernelGGL((k_binary<TI, C, TO, F, 1>), dim3(grid_for(n, kRwThreads)), dim3(kRwThreads), 0, s, a,
+                           b, out, sp, f);
     }
     HPXHIP_CHECK_LAUNCH();
     return 0;

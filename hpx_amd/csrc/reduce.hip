@@ -8,7 +8,9 @@
 //   * each 1024-thread block owns a contiguous chunk of 8 x 1024 16-B
 //     vectors (128 KiB) and walks it 16 KiB at a time -- the geometry that
 //     measured fastest for a read stream on MI355X (6.6 TB/s at 2^30 int64,
-//     vs 5.7 TB/s for a 2048-block grid-stride loop; scripts/ubench/rd.hip);
+//     vs 5.7 TB/s for a 2048-block grid-stride loop; scripts/ubench/rd.hip),
+//     all 8 loads in flight before the fold, nontemporal (6.91 TB/s for
+//     the bare stream, scripts/ubench/rd2.hip);
 //   * per thread a serial fold, DPP wave64 reduction, LDS across waves, one
 //     partial per block;
 //   * two-level deterministic fold inside the same launch: the last block to
@@ -83,13 +85,31 @@ __global__ __launch_bounds__(kThreads) void k_reduce(source<TI, TA, Conv, BINARY
     }
     const VI* va = reinterpret_cast<const VI*>(src.a + g.head);
     const VI* vb = reinterpret_cast<const VI*>((BINARY ? src.b : src.a) + g.head);
+    if (base + static_cast<uint64_t>(kSteps - 1) * kThreads < g.nvec) {
+        // full chunk: every load in flight before the first fold
+        VI x[kSteps], y[kSteps];
+#pragma unroll
+        for (int k = 0; k < kSteps; ++k) {
+            x[k] = ld_stream(&va[base + static_cast<uint64_t>(k) * kThreads]);
+            if constexpr (BINARY) y[k] = ld_stream(&vb[base + static_cast<uint64_t>(k) * kThreads]);
+        }
+#pragma unroll
+        for (int k = 0; k < kSteps; ++k)
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                TA c;
+                if constexpr (BINARY) c = src.conv(static_cast<TA>(x[k].v[e]), static_cast<TA>(y[k].v[e]));
+                else c = src.conv(static_cast<TA>(x[k].v[e]));
+                acc = op(acc, c);
+            }
+    } else {
 #pragma unroll 2
     for (int k = 0; k < kSteps; ++k) {
         const uint64_t i = base + static_cast<uint64_t>(k) * kThreads;
         if (i < g.nvec) {
-            const VI x = va[i];
+            const VI x = ld_stream(&va[i]);
             VI y;
-            if constexpr (BINARY) y = vb[i];
+            if constexpr (BINARY) y = ld_stream(&vb[i]);
 #pragma unroll
             for (int e = 0; e < V; ++e) {
                 TA c;
@@ -98,6 +118,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce(source<TI, TA, Conv, BINARY
                 acc = op(acc, c);
             }
         }
+    }
     }
 
     const TA blk = block_reduce(acc, op, lds);

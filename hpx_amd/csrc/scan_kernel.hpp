@@ -52,7 +52,7 @@ __global__ __launch_bounds__(THREADS) void k_scan(const T* in, T* out, uint64_t 
     if (ALIGNED && full) {
         const VT* src = reinterpret_cast<const VT*>(in + wbase);
 #pragma unroll
-        for (int r = 0; r < ROUNDS; ++r) x[r] = src[r * kWave + lane];
+        for (int r = 0; r < ROUNDS; ++r) x[r] = ld_stream(&src[r * kWave + lane]);
 #pragma unroll
         for (int r = 0; r < ROUNDS; ++r)
 #pragma unroll

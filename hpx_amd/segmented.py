@@ -334,6 +334,17 @@ class segmented:
         comm.allgather(8, eng.stream)                                    # one RCCL all-gather of 8 B
         dev, _ = _slots_for(pv.tgt).next() if isinstance(eng, HipEngine) else (eng.scratch(), None)
         eng.fold(adt, red_op, init, recv, comm.size, dev)                # init (op) S_0 (op) ... in order
+        if getattr(pol, "is_task", False):
+            # par(task): future<T> resolved by the stream, no host round trip
+            # inside the pipeline (segmented_algorithms/reduce.hpp:112-209
+            # returns the same future through algorithm_result).
+            from .future import future, make_ready_future
+            if isinstance(eng, HipEngine):
+                from .algorithms import _read_host
+                hdev, host = _slots_for(pv.tgt).next()
+                L.call("hpxhip_memcpy_async", ctypes.c_void_p(host), ctypes.c_void_p(dev), 8, L.D2H, eng.stream)
+                return future.on_stream(eng.stream, thunk=lambda: _read_host(host, adt))
+            return make_ready_future(eng.read(dev, adt))
         return eng.read(dev, adt)
 
     def reduce(self, pol, first, last, init=0, op=F.plus):
