@@ -11,7 +11,7 @@ BUILD    := build
 HIPFLAGS := -O3 --offload-arch=$(ARCH) -fPIC -std=c++17 -ffp-contract=off \
             -Wall -Wno-unused-result -Wno-unused-function -Iinclude
 LIB      := hpx_amd/libhpxhip.so
-KSRC     := runtime elementwise reduce scan copy_if sort stencil
+KSRC     := runtime elementwise reduce scan copy_if sort merge stencil
 KOBJ     := $(KSRC:%=$(BUILD)/csrc/%.o)
 KHDR     := $(wildcard hpx_amd/csrc/*.hpp) include/hpxhip.h
 

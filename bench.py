@@ -194,10 +194,12 @@ def main():
     }
     for v in (a, b, c):
         v.local.free()
-    if rank == 0 and not args.no_extras:
+    if not args.no_extras and world == 1:
         out["extras"] = extras(hpx, L, ex, F, tgt, pol, x, y, n_local, world)
     x.local.free()
     y.local.free()
+    if not args.no_extras and world > 1:
+        out["extras"] = dist_extras(S, F, comm, tgt, pol, n_local, world)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_logn)
     if rank == 0 and world == 1 and not args.no_pmc:
@@ -255,6 +257,79 @@ def extras(hpx, L, ex, F, tgt, pol, x, y, n_local, world):
                            "gpoint_steps_per_s": round(nx * nt / ms / 1e6, 2),
                            "gbs_model_16B": round(16 * nx * nt / ms / 1e6, 1), "pct_peak": pct(16 * nx * nt / ms / 1e6)}
     for v in st.U:
+        v.free()
+    return res
+
+
+def dist_extras(S, F, comm, tgt, pol, n_local, world):
+    """Multi-GPU rows of SURVEY.md section 8(e) (all ranks, max-over-ranks
+    wall time between barriers):
+      * segmented sort of 2^logn uint64 keys per GPU (weak scaling): local
+        radix sort, exact global cut, one RCCL all-to-all, pairwise merges;
+        checked: every partition sorted on sampled windows, partitions
+        ordered across ranks (first/last keys all-gathered);
+      * 1d_stencil heat, 2^32 points over the ranks (strong scaling), halo
+        ring over RCCL send/recv overlapped with the interior update;
+        checked: ramp interior unchanged (steady state away from the wrap)."""
+    import time
+    import torch
+    import torch.distributed as dist
+    res = {}
+    dev = torch.device("cuda", tgt.device)
+
+    def tmax(v):
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    n = n_local * world
+    keys = S.partitioned_vector(n, np.uint64, comm=comm, tgt=tgt)
+    best = None
+    for rep in range(3):
+        S.algorithms.generate(pol, keys.begin(), keys.end(), "bits", 7 + rep)
+        tgt.synchronize()
+        comm.barrier()
+        t0 = time.perf_counter()
+        S.algorithms.sort(pol, keys.begin(), keys.end())
+        tgt.synchronize()
+        comm.barrier()
+        el = tmax(time.perf_counter() - t0)
+        best = el if best is None else min(best, el)
+    loc = keys.local
+    m = len(loc)
+    ok = True
+    from hpx_amd import _lib as L
+    for w0 in (0, m // 2, max(0, m - (1 << 20))):
+        win = np.empty(min(1 << 20, m - w0), np.uint64)
+        if win.size:
+            L.call("hpxhip_memcpy_async", win.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(loc.data() + 8 * w0),
+                   8 * win.size, L.D2H, tgt.stream)
+            tgt.synchronize()
+            ok = ok and bool(np.all(win[1:] >= win[:-1]))
+    ends = np.array([loc[0], loc[m - 1]] if m else [0, 0], np.uint64).view(np.int64)
+    g = comm.allgather_host(ends).view(np.uint64)
+    ok = ok and all(g[r, 1] <= g[r + 1, 0] for r in range(world - 1)) and all(g[r, 0] <= g[r, 1] for r in range(world))
+    res["segmented_sort_uint64"] = {"keys_per_gpu": n_local, "keys_total": n, "ms": round(1e3 * best, 3),
+                                    "gkeys_per_s": round(n / best / 1e9, 3), "ordered_across_partitions": bool(ok)}
+    loc.free()
+    nx = 1 << 32
+    hs = S.heat_solver(nx, comm, tgt)
+    hs.do_work(1)
+    hs.synchronize()
+    comm.barrier()
+    nt = 10
+    t0 = time.perf_counter()
+    hs.do_work(nt)
+    hs.synchronize()
+    comm.barrier()
+    el = tmax(time.perf_counter() - t0)
+    cur = hs.current
+    mid = len(cur) // 2
+    ok = float(cur[mid]) == float(hs.lo + mid)  # ramp steady state in the interior
+    res["stencil_heat_dist"] = {"points": nx, "ranks": world, "steps": nt, "ms": round(1e3 * el, 3),
+                                "gpoint_steps_per_s": round(nx * nt / el / 1e9, 2),
+                                "gbs_model_16B": round(16 * nx * nt / el / 1e9, 1), "interior_check": bool(ok)}
+    for v in hs.U:
         v.free()
     return res
 

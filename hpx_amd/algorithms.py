@@ -370,3 +370,20 @@ def sort_by_key(pol, key_first, key_last, value_first, comp=F.less):
     L.call("hpxhip_sort_by_key", key_first.dtype, value_first.dtype, _vp(key_first.address),
            _vp(value_first.address), n, 1 if comp.descending else 0, stream, None, 0)
     return _finish(is_task, stream, tgt, lambda: (key_last, value_first + n))
+
+
+def merge(pol, first1, last1, first2, last2, dest, comp=F.less):
+    """merge.hpp:476: stable merge of two sorted ranges into dest (equal keys:
+    the first range's first, merge.hpp:52-80); returns the tagged tuple
+    (last1, last2, dest_end), or its future under par(task)."""
+    comp = F.require(comp, F.Compare, "merge")
+    n1 = _check_range(first1, last1)
+    n2 = _check_range(first2, last2)
+    if not isinstance(dest, iterator):
+        raise TypeError("merge: dest must be a device iterator")
+    if not (first1.dtype == first2.dtype == dest.dtype):
+        raise TypeError("merge: the ranges and dest must have one dtype")
+    stream, tgt, is_task = _context(pol, first1, first2, dest)
+    L.call("hpxhip_merge", first1.dtype, _vp(first1.address), n1, _vp(first2.address), n2, _vp(dest.address),
+           1 if comp.descending else 0, stream, None, 0)
+    return _finish(is_task, stream, tgt, lambda: (last1, last2, dest + (n1 + n2)))

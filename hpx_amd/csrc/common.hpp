@@ -131,6 +131,24 @@ __device__ __forceinline__ void st_stream(T* p, const T& v) {
 }
 
 // ---------------------------------------------------------------------------
+// Sort key order (radix sort, merge, sorted-range searches).
+// Storage bits -> ordered unsigned bits (ascending), optionally inverted:
+// signed integers flip the sign bit, IEEE floats flip all bits of negatives
+// and the sign bit of non-negatives (total order), descending inverts.
+template <typename T, bool DESC>
+struct ordered_bits {
+    using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
+    __device__ __forceinline__ U operator()(U raw) const {
+        constexpr U sign = U(1) << (sizeof(U) * 8 - 1);
+        U u;
+        if constexpr (std::is_floating_point_v<T>) u = (raw & sign) ? ~raw : (raw | sign);
+        else if constexpr (std::is_signed_v<T>) u = raw ^ sign;
+        else u = raw;
+        return DESC ? ~u : u;
+    }
+};
+
+// ---------------------------------------------------------------------------
 // Bit casts between T and 32-bit lanes (DPP moves 32 bits per lane).
 template <typename T>
 __device__ __forceinline__ void to_words(T x, uint32_t (&w)[(sizeof(T) + 3) / 4]) {

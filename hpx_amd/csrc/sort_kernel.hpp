@@ -10,21 +10,7 @@ namespace sort_detail {
 
 constexpr int kRadix = 256;
 
-// Storage bits -> ordered unsigned bits (ascending), optionally inverted:
-// signed integers flip the sign bit, IEEE floats flip all bits of negatives
-// and the sign bit of non-negatives (total order), descending inverts.
-template <typename T, bool DESC>
-struct ordered_bits {
-    using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
-    __device__ __forceinline__ U operator()(U raw) const {
-        constexpr U sign = U(1) << (sizeof(U) * 8 - 1);
-        U u;
-        if constexpr (std::is_floating_point_v<T>) u = (raw & sign) ? ~raw : (raw | sign);
-        else if constexpr (std::is_signed_v<T>) u = raw ^ sign;
-        else u = raw;
-        return DESC ? ~u : u;
-    }
-};
+// ordered_bits (storage bits -> ordered unsigned bits): common.hpp
 
 // Look-back granule (one aligned store, the data is the flag):
 //   0 = not yet published; ((c+1) << 1) = tile aggregate c; (v << 1) | 1 = inclusive v.

@@ -104,20 +104,43 @@ class TorchComm:
         return self._send.data_ptr(), self._recv.data_ptr()
 
     def allgather(self, nbytes: int, stream):
-        """recv[r*8 : r*8+nbytes] <- rank r's send[0:nbytes] (8-byte words)."""
+        """Packed all-gather: recv bytes [r*nbytes, (r+1)*nbytes) <- rank r's
+        send[0:nbytes] (nbytes a multiple of 8, at most 64), so the segment
+        values sit contiguously for hpxhip_fold."""
         words = max(1, nbytes // 8)
         with self.torch.cuda.stream(self._stream(stream)):
-            out = self._recv.view(self.size, 8)[:, :words]
-            if words == 8:
-                self.dist.all_gather_into_tensor(self._recv, self._send)
-            else:
-                tmp = self.torch.empty(self.size * words, dtype=self.torch.int64, device=self.device)
-                self.dist.all_gather_into_tensor(tmp, self._send[:words].contiguous())
-                out.copy_(tmp.view(self.size, words))
+            self.dist.all_gather_into_tensor(self._recv[:self.size * words], self._send[:words])
         return None
 
     def barrier(self):
         self.dist.barrier()
+
+    def allgather_host(self, words):
+        """Small host-level all-gather of int64 words -> array (size, k)."""
+        torch = self.torch
+        w = torch.as_tensor(np.ascontiguousarray(words, np.int64), device=self.device)
+        out = torch.empty(self.size * w.numel(), dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(out, w)
+        return out.cpu().numpy().reshape(self.size, -1)
+
+    def _bytes_view(self, addr, nbytes):
+        """A uint8 torch view of device memory the library allocated
+        (__cuda_array_interface__, no copy)."""
+        class _cai:
+            __cuda_array_interface__ = {"shape": (int(nbytes),), "typestr": "|u1", "data": (int(addr), False),
+                                        "version": 2, "strides": None}
+        return self.torch.as_tensor(_cai(), device=self.device)
+
+    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream):
+        """RCCL all-to-all with uneven splits: send_counts[j] elements from
+        send_buf[send_off:] go to rank j (in rank order); recv_counts[i]
+        elements from rank i land in recv_buf in rank order."""
+        sb = [int(c) * itemsize for c in send_counts]
+        rb = [int(c) * itemsize for c in recv_counts]
+        src = self._bytes_view(send_buf.data() + send_off * itemsize, max(1, sum(sb)))[:sum(sb)]
+        dst = self._bytes_view(recv_buf.data(), max(1, sum(rb)))[:sum(rb)]
+        with self.torch.cuda.stream(self._stream(stream)):
+            self.dist.all_to_all_single(dst, src, rb, sb)
 
     def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream):
         """Ring halo: my first point goes to the left neighbour (its right
@@ -174,10 +197,113 @@ class HipEngine:
         L.call("hpxhip_stream_synchronize", self.stream)
         return out[0].item()
 
+    # --- segmented sort primitives
+    def sort(self, vec, lo, hi, descending):
+        if hi - lo > 1:
+            L.call("hpxhip_sort", vec.dtype, ctypes.c_void_p(vec.data() + lo * vec.value_size), hi - lo,
+                   1 if descending else 0, self.stream, None, 0)
+
+    def bounds(self, vec, lo, hi, values, upper, descending):
+        """Local counts of sorted vec[lo:hi] elements ordered before (upper:
+        before or equal to) each of `values` (host array of vec's dtype)."""
+        values = np.ascontiguousarray(values, np_dtype(vec.dtype))
+        m = values.size
+        dv = vector.from_host(values, self.tgt)
+        dout = vector(m, dtype=np.uint64, tgt=self.tgt)
+        L.call("hpxhip_sorted_bounds", vec.dtype, ctypes.c_void_p(vec.data() + lo * vec.value_size), hi - lo,
+               ctypes.c_void_p(dv.data()), m, 1 if upper else 0, 1 if descending else 0,
+               ctypes.c_void_p(dout.data()), self.stream)
+        out = dout.to_host()
+        dv.free()
+        dout.free()
+        return out.astype(np.int64)
+
+    def buffer(self, like, n):
+        return vector(max(1, n), dtype=like.dtype, tgt=self.tgt)
+
+    def merge(self, dt, a, a_off, na, b, b_off, nb, out, out_off, descending):
+        it = np_dtype(dt).itemsize
+        L.call("hpxhip_merge", dt, ctypes.c_void_p(a.data() + a_off * it), na, ctypes.c_void_p(b.data() + b_off * it),
+               nb, ctypes.c_void_p(out.data() + out_off * it), 1 if descending else 0, self.stream, None, 0)
+
+    def copy(self, dt, src, s_off, n, dst, d_off):
+        if n:
+            it = np_dtype(dt).itemsize
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(dst.data() + d_off * it),
+                   ctypes.c_void_p(src.data() + s_off * it), n * it, L.D2D, self.stream)
+
+    def release(self, buf):
+        buf.free()
+
+    # --- 1d_stencil primitives
+    def heat_buffers(self, n, offset, init=None):
+        """U[0] = global index (1d_stencil_4.cpp:64-66) or `init`; U[1] scratch."""
+        if init is not None:
+            u0 = vector.from_host(np.ascontiguousarray(init, np.float64), self.tgt)
+        else:
+            u0 = vector(max(1, n), dtype=np.float64, tgt=self.tgt)
+            if n:
+                L.call("hpxhip_generate", L.F64, L.GEN_IOTA, 0, int(offset), 0, ctypes.c_void_p(u0.data()), n,
+                       self.stream)
+        return [u0, vector(max(1, n), dtype=np.float64, tgt=self.tgt)]
+
+    def halo_buffer(self):
+        return vector(4, dtype=np.float64, value=0.0, tgt=self.tgt)
+
+    def loc(self, buf, idx):
+        return buf.data() + 8 * int(idx)
+
+    def heat_step(self, cur, c_off, nxt, n_off, n, left, right, k, dt, dx, stream):
+        if n:
+            L.call("hpxhip_stencil_heat_step", ctypes.c_void_p(cur.data() + 8 * c_off),
+                   ctypes.c_void_p(nxt.data() + 8 * n_off), n, ctypes.c_void_p(left), ctypes.c_void_p(right),
+                   ctypes.c_double(k), ctypes.c_double(dt), ctypes.c_double(dx), stream)
+
+    def side_stream(self):
+        s = getattr(self, "_side", None)
+        if s is None:
+            s = ctypes.c_void_p()
+            L.call("hpxhip_stream_create", self.tgt.device, ctypes.byref(s))
+            self._side = s
+        return s
+
+    def record(self, stream):
+        from .future import _Event
+        e = _Event()
+        e.record(stream)
+        return e
+
+    def wait(self, stream, event):
+        L.call("hpxhip_stream_wait_event", stream, event.handle)
+
+    def synchronize(self):
+        L.call("hpxhip_stream_synchronize", self.stream)
+        if getattr(self, "_side", None) is not None:
+            L.call("hpxhip_stream_synchronize", self._side)
+
     def copy_if(self, src, lo, hi, dst, dlo, pred, count_ptr):
         L.call("hpxhip_copy_if", src.dtype, pred.kind, L.scalar_buf(src.dtype, pred.arg),
                ctypes.c_void_p(src.data() + lo * src.value_size), ctypes.c_void_p(dst.data() + dlo * dst.value_size),
                hi - lo, ctypes.c_void_p(count_ptr), self.stream, None, 0)
+
+
+def _from_ordered(u, dt, descending):
+    """Inverse of the sort's key order (common.hpp ordered_bits): ordered
+    unsigned bits -> the dtype's values."""
+    u = np.asarray(u)
+    npdt = np_dtype(dt)
+    ut = np.uint64 if npdt.itemsize == 8 else np.uint32
+    u = u.astype(ut)
+    if descending:
+        u = ~u
+    sign = ut(1) << ut(8 * npdt.itemsize - 1)
+    if npdt.kind == "f":
+        raw = np.where(u & sign, u ^ sign, ~u).astype(ut)
+    elif npdt.kind == "i":
+        raw = u ^ sign
+    else:
+        raw = u
+    return raw.view(npdt)
 
 
 def _identity(kind, dt):
@@ -383,6 +509,87 @@ class segmented:
     def transform_inclusive_scan(self, pol, first, last, dest, op, conv, init=0):
         return self._scan(pol, first, last, dest, op, init, True, conv)
 
+    # --- sort: local radix sort + exact global cut + one all-to-all + merge
+    def sort(self, pol, first, last=None, comp=F.less):
+        """Globally sorted partitioned_vector (BASELINE configs[2]; HPX 1.4
+        has no segmented sort, so the local algorithm is sort.hpp:364 and the
+        result obeys std::sort's contract over the global index order).
+
+        1. each rank radix-sorts its partition (hpxhip_sort);
+        2. the p-1 partition boundaries (global ranks partition_bounds(n, p,
+           j)[0]) are located exactly by a radix select over the ordered key
+           bits, 8 bits per round: every round each rank counts its keys
+           ordered before 256 candidates per boundary (hpxhip_sorted_bounds,
+           binary searches), one all-gather sums the counts;
+        3. equal keys straddling a boundary are split in rank order, giving
+           each rank contiguous, key-ordered slices for every destination;
+        4. one RCCL all-to-all with uneven splits moves the slices;
+        5. the p received sorted runs are merged pairwise (hpxhip_merge,
+           ceil(log2 p) rounds of 16 B/key) into the partition.
+        Returns last (the partitioned_vector's end)."""
+        comp = F.require(comp, F.Compare, "segmented sort")
+        pv, a, b = _range(first, last)
+        if a != 0 or b != pv.n:
+            raise ValueError("segmented sort sorts a whole partitioned_vector")
+        eng, comm = self.engine(pv), pv.comm
+        desc = comp.descending
+        dt = pv.dtype
+        lo, hi = pv.local_range(0, pv.n)
+        n_loc = hi - lo
+        eng.sort(pv.local, lo, hi, desc)
+        p = comm.size
+        if p == 1:
+            return segmented_iterator(pv, pv.n)
+        bits = 8 * np_dtype(dt).itemsize
+        ut = np.uint64 if bits == 64 else np.uint32
+        targets = np.array([partition_bounds(pv.n, p, j)[0] for j in range(1, p)], np.int64)
+        prefix = np.zeros(p - 1, ut)
+        digits = np.arange(256, dtype=ut)
+        for rnd in range(bits // 8):
+            shift = ut(bits - 8 * (rnd + 1))
+            cand = (prefix[:, None] | (digits[None, :] << shift)).ravel()
+            cnt = eng.bounds(pv.local, lo, hi, _from_ordered(cand, dt, desc), False, desc)
+            tot = comm.allgather_host(cnt).sum(axis=0).reshape(p - 1, 256)
+            d = (tot <= targets[:, None]).sum(axis=1) - 1          # count(< prefix|0) <= target holds
+            prefix = prefix | (d.astype(ut) << shift)
+        keys = _from_ordered(prefix, dt, desc)                        # key at each boundary's global rank
+        lt = eng.bounds(pv.local, lo, hi, keys, False, desc)
+        le = eng.bounds(pv.local, lo, hi, keys, True, desc)
+        g = comm.allgather_host(np.concatenate([lt, le - lt]))        # (p, 2(p-1))
+        LT, EQ = g[:, :p - 1], g[:, p - 1:]
+        remaining = targets - LT.sum(axis=0)                          # equal keys still owed to the left
+        before = np.cumsum(EQ, axis=0) - EQ                           # equal keys of lower ranks
+        take = np.clip(remaining[None, :] - before, 0, EQ)
+        cuts = np.concatenate([[0], (LT + take)[comm.rank], [n_loc]])
+        send = np.diff(cuts)
+        recv = comm.allgather_host(send)[:, comm.rank]
+        if int(recv.sum()) != n_loc:
+            raise RuntimeError(f"segmented sort: rank {comm.rank} receives {int(recv.sum())} keys for a "
+                               f"partition of {n_loc}")
+        rbuf = eng.buffer(pv.local, n_loc)
+        comm.alltoallv(pv.local, lo, send, rbuf, recv, np_dtype(dt).itemsize, eng.stream)
+        # pairwise merge rounds, ping-pong between rbuf and the partition
+        runs = [(int(o), int(c)) for o, c in zip(np.cumsum(recv) - recv, recv)]
+        src, dst = rbuf, pv.local
+        src_base, dst_base = 0, lo
+        while len(runs) > 1:
+            nxt = []
+            for k in range(0, len(runs) - 1, 2):
+                (oa, na), (ob, nb) = runs[k], runs[k + 1]
+                eng.merge(dt, src, src_base + oa, na, src, src_base + ob, nb, dst, dst_base + oa, desc)
+                nxt.append((oa, na + nb))
+            if len(runs) % 2:
+                oa, na = runs[-1]
+                eng.copy(dt, src, src_base + oa, na, dst, dst_base + oa)
+                nxt.append((oa, na))
+            runs = nxt
+            src, dst = dst, src
+            src_base, dst_base = dst_base, src_base
+        if src is not pv.local:
+            eng.copy(dt, src, src_base, n_loc, pv.local, lo)
+        eng.release(rbuf)
+        return segmented_iterator(pv, pv.n)
+
     # --- copy_if: local compaction + all-gather of counts -> global offsets
     def copy_if(self, pol, first, last, dest_pv, pred):
         """Each rank compacts its segment into the front of its partition of
@@ -419,6 +626,75 @@ def _exec(pv):
 
 # the default instance: hpx_amd.segmented.algorithms.reduce(...)
 algorithms = segmented()
+
+
+# ------------------------------------------------------------- 1d_stencil
+class heat_solver:
+    """examples/1d_stencil over a partitioned ring, one partition per rank
+    (1d_stencil_8.cpp:240-258 partition_server + 482-531 do_work: every step
+    each partition needs its neighbours' boundary points, periodic ring
+    1d_stencil_4_parallel.cpp:147-150; U0[i] = global i, 1d_stencil_4.cpp:64-66).
+
+    Step t on partition [lo, hi) of n >= 4 points, with cur = U[t%2]:
+      main stream: edge points 0,1 and n-2,n-1 of next (they read the halos
+                   received for cur), event E_edges;
+      side stream: waits E_edges, sends next[0] left and next[n-1] right,
+                   receives the neighbours' points into the other halo slot
+                   (RCCL send/recv of 8 B each way), event E_halo;
+      main stream: the interior [2, n-2) of next, concurrent with the
+                   exchange; step t+1 waits E_halo before its edges.
+    The halo latency (~10-30 us for RCCL) hides behind the interior kernel
+    (1.4 ms at 2^29 points per GPU).  n < 4: one full step per partition."""
+
+    def __init__(self, nx, comm, tgt=None, k=0.5, dt=1.0, dx=1.0, engine=None, init=None):
+        self.comm = comm
+        self.tgt = tgt
+        self.eng = engine or HipEngine(tgt)
+        self.nx = int(nx)
+        self.lo, self.hi = partition_bounds(self.nx, comm.size, comm.rank)
+        self.n = self.hi - self.lo
+        if partition_bounds(self.nx, comm.size, comm.size - 1)[1] - partition_bounds(self.nx, comm.size,
+                                                                                      comm.size - 1)[0] <= 0:
+            raise ValueError(f"1d_stencil: {self.nx} points leave an empty partition on {comm.size} ranks")
+        self.k, self.dt, self.dx = k, dt, dx
+        self.U = self.eng.heat_buffers(self.n, self.lo, None if init is None else init[self.lo:self.hi])
+        self.H = self.eng.halo_buffer()   # [left, right] x 2 slots
+        self.t = 0
+        self._halo_ev = None
+        self._exchange(self.U[0], 0, self.eng.stream)   # halos of U0 into slot 0
+
+    def _exchange(self, buf, slot, after_stream):
+        eng, side = self.eng, self.eng.side_stream()
+        eng.wait(side, eng.record(after_stream))
+        self.comm.halo_exchange(eng.loc(buf, 0), eng.loc(buf, self.n - 1), eng.loc(self.H, 2 * slot),
+                                eng.loc(self.H, 2 * slot + 1), side)
+        self._halo_ev = eng.record(side)
+
+    @property
+    def current(self):
+        return self.U[self.t % 2]
+
+    def do_work(self, nt):
+        eng, n, S = self.eng, self.n, self.eng.stream
+        k, dt, dx = self.k, self.dt, self.dx
+        for _ in range(nt):
+            cur, nxt = self.U[self.t % 2], self.U[(self.t + 1) % 2]
+            slot = self.t % 2
+            left, right = eng.loc(self.H, 2 * slot), eng.loc(self.H, 2 * slot + 1)
+            eng.wait(S, self._halo_ev)
+            if n >= 4:
+                eng.heat_step(cur, 0, nxt, 0, 2, left, eng.loc(cur, 2), k, dt, dx, S)
+                eng.heat_step(cur, n - 2, nxt, n - 2, 2, eng.loc(cur, n - 3), right, k, dt, dx, S)
+                self._exchange(nxt, 1 - slot, S)
+                eng.heat_step(cur, 2, nxt, 2, n - 4, eng.loc(cur, 1), eng.loc(cur, n - 2), k, dt, dx, S)
+            else:
+                eng.heat_step(cur, 0, nxt, 0, n, left, right, k, dt, dx, S)
+                self._exchange(nxt, 1 - slot, S)
+            self.t += 1
+        return self.current
+
+    def synchronize(self):
+        self.eng.synchronize()
 
 
 # ------------------------------------------------------------- comm factory

@@ -128,7 +128,8 @@ enum hpxhip_algo {
     HPXHIP_ALGO_SCAN = 1,
     HPXHIP_ALGO_COPY_IF = 2,
     HPXHIP_ALGO_SORT = 3,
-    HPXHIP_ALGO_SORT_BY_KEY = 4
+    HPXHIP_ALGO_SORT_BY_KEY = 4,
+    HPXHIP_ALGO_MERGE = 5  /* n = n1 + n2 */
 };
 
 typedef struct hpxhip_stream_opaque* hpxhip_stream; /* == hipStream_t */
@@ -286,6 +287,21 @@ int hpxhip_sort(int dtype, void* keys, uint64_t n, int descending, hpxhip_stream
    (value dtype = any 4/8-byte dtype). */
 int hpxhip_sort_by_key(int key_dtype, int value_dtype, void* keys, void* values, uint64_t n,
                        int descending, hpxhip_stream stream, void* scratch, size_t scratch_bytes);
+
+/* -------------------------------------------------------------- merge */
+/* merge.hpp:476: stable merge of the sorted ranges in1[0,n1) and in2[0,n2)
+   into out[0,n1+n2) (equal keys: in1's first, merge.hpp:52-80), ascending
+   (std::less) or descending (std::greater), in the same key order as
+   hpxhip_sort.  out must not overlap the inputs. */
+int hpxhip_merge(int dtype, const void* in1, uint64_t n1, const void* in2, uint64_t n2, void* out,
+                 int descending, hpxhip_stream stream, void* scratch, size_t scratch_bytes);
+/* Batched binary search in a sorted range (the partition cut of the
+   segmented sort; std::lower_bound / std::upper_bound semantics under the
+   sort's key order): out_dev[i] = number of sorted[] elements ordered before
+   values_dev[i] (upper != 0: before or equal).  All pointers are device
+   memory; out_dev holds m uint64 counts. */
+int hpxhip_sorted_bounds(int dtype, const void* sorted, uint64_t n, const void* values_dev, uint64_t m,
+                         int upper, int descending, uint64_t* out_dev, hpxhip_stream stream);
 
 /* ---------------------------------------------------------- 1d_stencil */
 /* One heat step of examples/1d_stencil: next[i] = heat(cur[i-1], cur[i], cur[i+1])

@@ -453,6 +453,34 @@ int oracle_sort_by_key(int key_dt, int val_dt, void* keys, void* values, uint64_
     });
 }
 
+// merge.hpp:52-80 (sequential_merge): take from the second range only when
+// comp(*first2, *first1); then copy the rest of both.  comp is std::less /
+// std::greater over the sort's key order (ordered()).
+int oracle_merge(int dtype, const void* in1, uint64_t n1, const void* in2, uint64_t n2, void* out, int descending) {
+    return with_dtype(dtype, [&](auto t) {
+        using T = typename decltype(t)::type;
+        const T* a = static_cast<const T*>(in1);
+        const T* b = static_cast<const T*>(in2);
+        T* d = static_cast<T*>(out);
+        auto comp = [&](T x, T y) { return descending ? ordered(y) < ordered(x) : ordered(x) < ordered(y); };
+        uint64_t i = 0, j = 0;
+        if (n1 && n2) {
+            while (true) {
+                if (comp(b[j], a[i])) {
+                    *d++ = b[j++];
+                    if (j == n2) break;
+                } else {
+                    *d++ = a[i++];
+                    if (i == n1) break;
+                }
+            }
+        }
+        while (i < n1) *d++ = a[i++];
+        while (j < n2) *d++ = b[j++];
+        return 0;
+    });
+}
+
 static inline double heat(double left, double middle, double right, double k, double dt, double dx) {
     return middle + (k * dt / (dx * dx)) * (left - 2 * middle + right);  // 1d_stencil_1.cpp:45
 }

@@ -67,6 +67,8 @@ int oracle_copy_if(int dtype, int pred_kind, const void* pred_arg, const void* i
    the order the radix sort produces; on data without signed zeros or NaNs
    it equals std::less. */
 int oracle_sort(int dtype, void* keys, uint64_t n, int descending);
+/* merge.hpp:52-80 sequential_merge (stable, first range first on ties). */
+int oracle_merge(int dtype, const void* in1, uint64_t n1, const void* in2, uint64_t n2, void* out, int descending);
 /* sort_by_key.hpp:42-78, stable variant (ties keep input order). */
 int oracle_sort_by_key(int key_dtype, int value_dtype, void* keys, void* values, uint64_t n,
                        int descending);

@@ -143,6 +143,16 @@ def sort(a, descending=False):
     return out
 
 
+def merge(a, b, descending=False):
+    """merge.hpp:52-80: stable merge of two sorted arrays (oracle_merge)."""
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b, dtype=a.dtype)
+    out = np.empty(a.size + b.size, a.dtype)
+    _check(load().oracle_merge(DT[dtname(a.dtype)], _p(a), ctypes.c_uint64(a.size), _p(b), ctypes.c_uint64(b.size),
+                               _p(out), 1 if descending else 0), "merge")
+    return out
+
+
 def sort_by_key(keys, values, descending=False):
     k = np.array(keys, copy=True)
     v = np.array(values, copy=True)

@@ -1,0 +1,164 @@
+"""Two ranks on the GPU: the product engine (HipEngine: radix sort, sorted-
+range searches, merge, heat steps, reduce/scan/fold kernels) driven by the
+multi-rank orchestration of hpx_amd.segmented, with both processes on
+cuda:0.  RCCL refuses two ranks on one device, so the collectives here go
+through a host-staged gloo test double (device -> host -> gloo -> device);
+TorchComm's RCCL calls themselves are covered on a one-rank group in
+tests/test_gpu_merge_sort.py.  Results are checked against the oracle."""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class HostStagedComm:
+    def __init__(self, tgt):
+        import torch.distributed as dist
+        import hpx_amd as hpx
+        self.dist = dist
+        self.tgt = tgt
+        self.rank, self.size = dist.get_rank(), dist.get_world_size()
+        self._send = hpx.vector(8, dtype=np.int64, tgt=tgt)
+        self._recv = hpx.vector(8 * self.size, dtype=np.int64, tgt=tgt)
+
+    def _d2h(self, addr, nbytes):
+        from hpx_amd import _lib as L
+        buf = np.empty(nbytes, np.uint8)
+        L.call("hpxhip_memcpy_async", buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(addr), nbytes, L.D2H,
+               self.tgt.stream)
+        self.tgt.synchronize()
+        return buf
+
+    def _h2d(self, addr, buf):
+        from hpx_amd import _lib as L
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(addr), buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes, L.H2D,
+               self.tgt.stream)
+        self.tgt.synchronize()
+
+    def _allgather_bytes(self, b):
+        import torch
+        t = torch.from_numpy(b.copy())
+        out = [torch.zeros_like(t) for _ in range(self.size)]
+        self.dist.all_gather(out, t)
+        return [o.numpy() for o in out]
+
+    # reduce / scan / copy_if exchange
+    def slots(self, nbytes):
+        return self._send.data(), self._recv.data()
+
+    def allgather(self, nbytes, stream):
+        self.tgt.synchronize()
+        parts = self._allgather_bytes(self._d2h(self._send.data(), nbytes))   # packed, as TorchComm
+        self._h2d(self._recv.data(), np.concatenate(parts))
+
+    def allgather_host(self, words):
+        return np.stack(self._allgather_bytes(np.ascontiguousarray(words, np.int64).view(np.uint8))).view(np.int64)
+
+    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream):
+        import torch
+        self.tgt.synchronize()
+        n = int(sum(send_counts))
+        src = torch.from_numpy(self._d2h(send_buf.data() + send_off * itemsize, n * itemsize) if n else
+                               np.zeros(0, np.uint8))
+        dst = torch.zeros(int(sum(recv_counts)) * itemsize, dtype=torch.uint8)
+        self.dist.all_to_all_single(dst, src, [int(c) * itemsize for c in recv_counts],
+                                    [int(c) * itemsize for c in send_counts])
+        if dst.numel():
+            self._h2d(recv_buf.data(), dst.numpy())
+
+    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream):
+        from hpx_amd import _lib as L
+        L.call("hpxhip_stream_synchronize", stream)
+        mine = np.concatenate([self._d2h(send_left, 8), self._d2h(send_right, 8)])
+        got = self._allgather_bytes(mine)
+        left, right = (self.rank - 1) % self.size, (self.rank + 1) % self.size
+        self._h2d(recv_left, got[left][8:16].copy())
+        self._h2d(recv_right, got[right][0:8].copy())
+
+    def barrier(self):
+        self.dist.barrier()
+
+
+def _worker(rank, size, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        import hpx_amd as hpx
+        from hpx_amd import execution as ex, functional as F
+        from hpx_amd import segmented as S
+        tgt = hpx.target(0)
+        pol = ex.par.on(hpx.default_executor(tgt))
+        comm = HostStagedComm(tgt)
+        alg = S.segmented()
+        res = {}
+        n = (1 << 20) + 12345
+        for dt, kind in ((np.uint64, "bits"), (np.int64, "range")):
+            pv = S.partitioned_vector(n, dt, comm=comm, tgt=tgt)
+            alg.generate(pol, pv.begin(), pv.end(), kind, 99, -50, 50)
+            for desc in (False, True):
+                alg.sort(pol, pv.begin(), pv.end(), F.greater if desc else F.less)
+                tgt.synchronize()
+                res[("sort", np.dtype(dt).name, desc)] = (pv.lo, pv.local.to_host())
+        x = S.partitioned_vector(n, np.int64, comm=comm, tgt=tgt)
+        alg.generate(pol, x.begin(), x.end(), "range", 0x5EED, -1000, 1000)
+        res["reduce"] = alg.reduce(pol, x.begin(), x.end(), 3, F.plus)
+        y = S.partitioned_vector(n, np.int64, comm=comm, tgt=tgt)
+        alg.inclusive_scan(pol, x.begin(), x.end(), y.begin(), F.plus, 3)
+        tgt.synchronize()
+        res["scan"] = (y.lo, y.local.to_host())
+        for nx, nt in ((1 << 20, 6), (1001, 9)):
+            init = np.random.default_rng(nx).standard_normal(nx)
+            hs = S.heat_solver(nx, comm, tgt, init=init)
+            out = hs.do_work(nt)
+            hs.synchronize()
+            res[("heat", nx)] = (hs.lo, out.to_host())
+        q.put((rank, res))
+    except Exception as e:  # report to the parent
+        q.put((rank, e))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_ranks_on_gpu_segmented_sort_reduce_scan_stencil(gpu_target):
+    import torch.multiprocessing as mp
+    from oracle import oracle as O
+    size = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, size, port, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=110) for _ in range(size))
+    for p in procs:
+        p.join(timeout=30)
+    for r in range(size):
+        assert not isinstance(results[r], Exception), results[r]
+    n = (1 << 20) + 12345
+    for dt, kind in ((np.uint64, "bits"), (np.int64, "range")):
+        base = O.generate(dt, kind, n, 99, -50, 50)
+        for desc in (False, True):
+            got = np.concatenate([results[r][("sort", np.dtype(dt).name, desc)][1] for r in range(size)])
+            np.testing.assert_array_equal(got, O.sort(base, desc))
+    x = O.generate(np.int64, "range", n, 0x5EED, -1000, 1000)
+    assert all(results[r]["reduce"] == 3 + int(x.sum()) for r in range(size))
+    got = np.concatenate([results[r]["scan"][1] for r in range(size)])
+    np.testing.assert_array_equal(got, O.segmented_scan(x, 3, size, True))
+    for nx, nt in ((1 << 20, 6), (1001, 9)):
+        init = np.random.default_rng(nx).standard_normal(nx)
+        got = np.concatenate([results[r][("heat", nx)][1] for r in range(size)])
+        np.testing.assert_array_equal(got, O.stencil_heat(init, nt))

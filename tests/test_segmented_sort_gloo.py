@@ -1,0 +1,170 @@
+"""Segmented sort across ranks on CPU (gloo, world sizes 2-4): the exact
+global cut (radix select over ordered key bits + rank-order split of equal
+keys), the uneven all-to-all and the pairwise merge rounds of
+hpx_amd.segmented.segmented.sort.  The per-partition kernels are replaced by
+the oracle (sort.hpp:364 std::sort, merge.hpp:52-80 sequential_merge) and
+numpy searchsorted *in this test only*; the product engine is HipEngine
+(tests/test_gpu_parity.py covers hpxhip_merge / hpxhip_sorted_bounds and the
+single-rank path on the GPU)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from hpx_amd import _lib as L  # noqa: E402
+from hpx_amd import functional as F  # noqa: E402
+from hpx_amd import segmented as S  # noqa: E402
+
+CODES = {np.dtype(np.int64): L.I64, np.dtype(np.uint64): L.U64, np.dtype(np.float64): L.F64,
+         np.dtype(np.int32): L.I32, np.dtype(np.uint32): L.U32, np.dtype(np.float32): L.F32}
+
+
+def _ordered(x, desc):
+    """Host restatement of the key order (common.hpp ordered_bits)."""
+    it = x.dtype.itemsize
+    ut = np.uint64 if it == 8 else np.uint32
+    raw = x.view(ut)
+    sign = ut(1) << ut(8 * it - 1)
+    if x.dtype.kind == "f":
+        o = np.where(raw & sign, ~raw, raw | sign).astype(ut)
+    elif x.dtype.kind == "i":
+        o = raw ^ sign
+    else:
+        o = raw.copy()
+    return ~o if desc else o
+
+
+class GlooComm:
+    def __init__(self):
+        self.rank, self.size = dist.get_rank(), dist.get_world_size()
+
+    def allgather_host(self, words):
+        w = torch.from_numpy(np.ascontiguousarray(words, np.int64))
+        out = [torch.zeros_like(w) for _ in range(self.size)]
+        dist.all_gather(out, w)
+        return np.stack([o.numpy() for o in out])
+
+    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream):
+        n = int(sum(send_counts))
+        src = torch.from_numpy(send_buf[send_off:send_off + n].view(np.uint8).copy())
+        dst = torch.zeros(int(sum(recv_counts)) * itemsize, dtype=torch.uint8)
+        dist.all_to_all_single(dst, src, [int(c) * itemsize for c in recv_counts],
+                               [int(c) * itemsize for c in send_counts])
+        recv_buf[:int(sum(recv_counts))] = dst.numpy().view(recv_buf.dtype)
+
+    def barrier(self):
+        dist.barrier()
+
+
+class SortEngine:
+    stream = None
+
+    def sort(self, vec, lo, hi, desc):
+        vec[lo:hi] = O.sort(vec[lo:hi], desc)
+
+    def bounds(self, vec, lo, hi, values, upper, desc):
+        keys = _ordered(vec[lo:hi], desc)
+        v = _ordered(np.asarray(values, vec.dtype), desc)
+        return np.searchsorted(keys, v, side="right" if upper else "left").astype(np.int64)
+
+    def buffer(self, like, n):
+        return np.zeros(max(1, n), like.dtype)
+
+    def merge(self, dt, a, a_off, na, b, b_off, nb, out, out_off, desc):
+        out[out_off:out_off + na + nb] = O.merge(a[a_off:a_off + na], b[b_off:b_off + nb], desc)
+
+    def copy(self, dt, src, s_off, n, dst, d_off):
+        dst[d_off:d_off + n] = src[s_off:s_off + n]
+
+    def release(self, buf):
+        pass
+
+
+class HostPV(S.partitioned_vector):
+    def __init__(self, glob, comm):
+        self.comm = comm
+        self.tgt = None
+        self.n = glob.size
+        self.dtype = CODES[glob.dtype]
+        self.rank, self.parts = comm.rank, comm.size
+        self.lo, self.hi = S.partition_bounds(self.n, self.parts, self.rank)
+        self.local = glob[self.lo:self.hi].copy()
+
+
+def cases():
+    rng = np.random.default_rng(0x5EED)
+    f = rng.standard_normal(3001)
+    f[::17] = 0.0
+    f[::19] = -0.0
+    f[5] = np.inf
+    f[6] = -np.inf
+    return {
+        "i64_random": O.generate(np.int64, "range", 10007, 0x5EED, -1000, 1000),
+        "u64_bits": O.generate(np.uint64, "bits", 4099, 7),
+        "i64_dups": rng.integers(0, 3, 5000).astype(np.int64),
+        "i64_const": np.full(777, 42, np.int64),
+        "f64_signed_zeros": f,
+        "u32": rng.integers(0, 2 ** 32, 3333, dtype=np.uint64).astype(np.uint32),
+        "i32_small": np.array([5, -1, 3], np.int32),
+        "f32": rng.standard_normal(2048).astype(np.float32),
+        "empty": np.zeros(0, np.int64),
+    }
+
+
+def _worker(rank, size, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        comm = GlooComm()
+        alg = S.segmented(SortEngine())
+        res = {}
+        for name, x in cases().items():
+            for desc in (False, True):
+                pv = HostPV(x, comm)
+                alg.sort(None, pv.begin(), pv.end(), F.greater if desc else F.less)
+                res[(name, desc)] = (pv.lo, pv.local.copy())
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("size", [2, 3, 4])
+def test_segmented_sort_gloo(size):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, size, port, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=180) for _ in range(size))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for name, x in cases().items():
+        for desc in (False, True):
+            got = np.zeros_like(x)
+            sizes = []
+            for r in range(size):
+                lo, loc = results[r][(name, desc)]
+                got[lo:lo + loc.size] = loc
+                sizes.append(loc.size)
+            # partition sizes unchanged (partitioned_vector_impl.hpp:325) and
+            # the concatenation is the oracle sort bit for bit
+            assert sizes == [b - a for a, b in (S.partition_bounds(x.size, size, k) for k in range(size))]
+            exp = O.sort(x, desc)
+            np.testing.assert_array_equal(got.view(np.uint8), exp.view(np.uint8), err_msg=f"{name} desc={desc}")

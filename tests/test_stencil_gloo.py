@@ -1,0 +1,122 @@
+"""examples/1d_stencil over a partitioned periodic ring on CPU (gloo, 1-3
+ranks): the halo ring, the double-buffered halo slots and the edge /
+exchange / interior ordering of hpx_amd.segmented.heat_solver, against the
+serial oracle (1d_stencil_1.cpp:41-72).  Per-partition kernels are replaced
+by the oracle's one-step restatement *in this test only*; the product engine
+(HipEngine + hpxhip_stencil_heat_step) is exercised on the GPU by
+tests/test_gpu_parity.py and tests/test_gpu_merge_sort.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from hpx_amd import segmented as S  # noqa: E402
+
+
+class RingComm:
+    def __init__(self):
+        self.rank, self.size = dist.get_rank(), dist.get_world_size()
+
+    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream):
+        (a0, i0), (a1, i1) = send_left, send_right
+        mine = torch.tensor([a0[i0], a1[i1]], dtype=torch.float64)
+        got = [torch.zeros(2, dtype=torch.float64) for _ in range(self.size)]
+        dist.all_gather(got, mine)
+        left, right = (self.rank - 1) % self.size, (self.rank + 1) % self.size
+        (b0, j0), (b1, j1) = recv_left, recv_right
+        b0[j0] = float(got[left][1])    # left neighbour's last point
+        b1[j1] = float(got[right][0])   # right neighbour's first point
+
+
+class HeatEngine:
+    stream = None
+
+    def heat_buffers(self, n, offset, init=None):
+        u0 = np.arange(offset, offset + n, dtype=np.float64) if init is None else np.array(init, np.float64)
+        return [u0, np.zeros(n)]
+
+    def halo_buffer(self):
+        return np.zeros(4)
+
+    def loc(self, buf, idx):
+        return (buf, int(idx))
+
+    def heat_step(self, cur, c_off, nxt, n_off, n, left, right, k, dt, dx, stream):
+        lv = left[0][left[1]]
+        rv = right[0][right[1]]
+        nxt[n_off:n_off + n] = O.stencil_heat_step(cur[c_off:c_off + n], lv, rv, k, dt, dx)
+
+    def side_stream(self):
+        return None
+
+    def record(self, stream):
+        return None
+
+    def wait(self, stream, ev):
+        pass
+
+    def synchronize(self):
+        pass
+
+
+CASES = [(1001, 25, "ramp"), (1001, 25, "random"), (9, 7, "random"), (64, 40, "random")]
+
+
+def _worker(rank, size, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        comm = RingComm()
+        res = {}
+        for nx, nt, kind in CASES:
+            init = None if kind == "ramp" else np.random.default_rng(nx).standard_normal(nx)
+            hs = S.heat_solver(nx, comm, engine=HeatEngine(), init=init)
+            out = hs.do_work(nt)
+            res[(nx, nt, kind)] = (hs.lo, out.copy())
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("size", [1, 2, 3])
+def test_heat_solver_ring_gloo(size):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, size, port, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(size))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for nx, nt, kind in CASES:
+        u0 = np.arange(nx, dtype=np.float64) if kind == "ramp" else np.random.default_rng(nx).standard_normal(nx)
+        exp = O.stencil_heat(u0, nt)
+        got = np.zeros(nx)
+        for r in range(size):
+            lo, loc = results[r][(nx, nt, kind)]
+            got[lo:lo + loc.size] = loc
+        np.testing.assert_array_equal(got, exp, err_msg=f"nx={nx} nt={nt} {kind} ranks={size}")
+
+
+def test_heat_solver_rejects_empty_partitions():
+    class C:
+        rank, size = 0, 8
+    with pytest.raises(ValueError):
+        S.heat_solver(9, C(), engine=HeatEngine())
