@@ -76,6 +76,20 @@ class LocalComm:
         L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_right), ctypes.c_void_p(send_left), 8, L.D2D, stream)
 
 
+def ring_halo_ops(dist, rank, size, first, last, left_halo, right_halo):
+    """P2P ops of one periodic halo step (1d_stencil_4_parallel.cpp:147-150):
+    my last point becomes the right neighbour's left halo, my first point the
+    left neighbour's right halo.  Point-to-point messages between one pair of
+    ranks match in posting order, and with two ranks the left and right
+    neighbour are the same rank, so the order is fixed: send last (to the
+    right) before first (to the left), receive from the left before the
+    right -- then the k-th send of one rank meets the k-th receive of the
+    other for every ring size."""
+    left, right = (rank - 1) % size, (rank + 1) % size
+    return [dist.P2POp(dist.isend, last, right), dist.P2POp(dist.isend, first, left),
+            dist.P2POp(dist.irecv, left_halo, left), dist.P2POp(dist.irecv, right_halo, right)]
+
+
 class TorchComm:
     """One rank per GPU over torch.distributed (backend "nccl" = RCCL on ROCm).
 
@@ -152,9 +166,8 @@ class TorchComm:
             L.call("hpxhip_memcpy_async", ctypes.c_void_p(h.data_ptr()), ctypes.c_void_p(send_left), 8, L.D2D, stream)
             L.call("hpxhip_memcpy_async", ctypes.c_void_p(h.data_ptr() + 8), ctypes.c_void_p(send_right), 8, L.D2D,
                    stream)
-            ops = [dist.P2POp(dist.isend, h[0:1], left), dist.P2POp(dist.isend, h[1:2], right),
-                   dist.P2POp(dist.irecv, h[2:3], left), dist.P2POp(dist.irecv, h[3:4], right)]
-            for w in dist.batch_isend_irecv(ops):
+            for w in dist.batch_isend_irecv(ring_halo_ops(dist, self.rank, self.size, h[0:1], h[1:2], h[2:3],
+                                                           h[3:4])):
                 w.wait()
             L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_left), ctypes.c_void_p(h.data_ptr() + 16), 8, L.D2D,
                    stream)
