@@ -387,3 +387,64 @@ def merge(pol, first1, last1, first2, last2, dest, comp=F.less):
     L.call("hpxhip_merge", first1.dtype, _vp(first1.address), n1, _vp(first2.address), n2, _vp(dest.address),
            1 if comp.descending else 0, stream, None, 0)
     return _finish(is_task, stream, tgt, lambda: (last1, last2, dest + (n1 + n2)))
+
+
+# ------------------------------------------------------------------ for_loop
+class induction:
+    """for_loop_induction.hpp:210-219: an induction variable whose value at
+    iteration i is value + stride * i (pointer / iterator inductions here)."""
+    __slots__ = ("value", "stride")
+
+    def __init__(self, value, stride: int = 1):
+        self.value, self.stride = value, int(stride)
+
+
+def for_loop_n(pol, first, count, *args):
+    """for_loop.hpp:808 for_loop_n(policy, first, size, inductions..., f) as
+    for_loop_compute.cu uses it: the loop iterator and pointer inductions
+    (stride 1) walk device ranges in lock step and the body writes one of
+    them from one or two others (functional.assign).  The iteration space
+    maps onto the elementwise transform kernels; returns None (future<void>
+    under par(task))."""
+    if not args:
+        raise TypeError("for_loop_n: missing loop body")
+    *inds, body = args
+    body = F.require(body, F.LoopBody, "for_loop_n")
+    for ind in inds:
+        if not isinstance(ind, induction):
+            raise TypeError("for_loop_n: extra arguments must be hpx::parallel::induction objects "
+                            "(reductions are not carried by the C ABI)")
+        if not isinstance(ind.value, iterator):
+            raise TypeError("for_loop_n: inductions over device iterators only")
+        if ind.stride != 1:
+            raise ValueError("for_loop_n: pointer inductions with stride != 1 are not supported by the "
+                             "contiguous elementwise kernels")
+    if not isinstance(first, iterator):
+        raise TypeError("for_loop_n: the loop variable must be a device iterator")
+    n = int(count)
+    if n < 0:
+        raise ValueError("for_loop_n: negative count")
+    vars_ = [first] + [ind.value for ind in inds]
+    try:
+        out = vars_[body.out]
+        ins = [vars_[i] for i in body.ins]
+    except IndexError:
+        raise IndexError("for_loop_n: loop body refers to a variable that is not passed") from None
+    stream, tgt, is_task = _context(pol, out, *ins)
+    fn = body.fn
+    if isinstance(fn, F.Unary):
+        cdt = _compute_dtype(ins[0].dtype, fn)
+        L.call("hpxhip_transform", ins[0].dtype, cdt, out.dtype, fn.kind, L.scalars_buf(cdt, fn.scalars),
+               _vp(ins[0].address), _vp(out.address), n, stream)
+    else:
+        if ins[0].dtype != ins[1].dtype:
+            raise TypeError("for_loop_n: both inputs of a binary body must have one dtype")
+        cdt = _compute_dtype(ins[0].dtype, fn)
+        L.call("hpxhip_transform_binary", ins[0].dtype, cdt, out.dtype, fn.kind, L.scalars_buf(cdt, fn.scalars),
+               _vp(ins[0].address), _vp(ins[1].address), _vp(out.address), n, stream)
+    return _finish(is_task, stream, tgt, lambda: None)
+
+
+def for_loop(pol, first, last, *args):
+    """for_loop.hpp for_loop(policy, first, last, inductions..., f)."""
+    return for_loop_n(pol, first, _check_range(first, last), *args)

@@ -209,6 +209,25 @@ def any_bits(mask) -> Predicate:
     return Predicate(L.P_BITS, mask)
 
 
+# ------------------------------------------------------------- loop bodies
+@dataclass(frozen=True)
+class LoopBody:
+    """Body of for_loop / for_loop_n over pointer inductions: writes
+    ``*vars[out] = fn(*vars[ins[0]] [, *vars[ins[1]]])`` where vars are the
+    loop iterator (position 0) followed by the inductions in call order.
+    for_loop_compute.cu:40-48's ``[](int* A, int* B, int* C) { *C = *A +
+    3.0 * *B; }`` is ``assign(2, triad_step(3.0, "float64"), 0, 1)``."""
+    out: int
+    fn: object
+    ins: tuple
+
+
+def assign(out: int, fn, *ins) -> LoopBody:
+    if isinstance(fn, Unary) and len(ins) == 1 or isinstance(fn, Binary) and len(ins) == 2:
+        return LoopBody(int(out), fn, tuple(int(i) for i in ins))
+    raise TypeError("assign: a Unary functor takes one loop variable, a Binary functor two")
+
+
 # ------------------------------------------------------------------ compare
 @dataclass(frozen=True)
 class Compare:
