@@ -42,3 +42,11 @@ def srt():
 timeit("generate u64", lambda: lib.hpxhip_generate(L.U64, L.GEN_BITS, 7, 0, 0, keys, N, st), 8*N, reps=3)
 timeit("gen+sort u64", srt, 136*N, reps=3)
 code = ctypes.c_uint32(); L.check(lib.hpxhip_device_error(0, ctypes.byref(code))); print("deverr", code.value)
+# merge of two sorted 2^(LOGN-1) u64 runs (evens and odds: alternating path)
+h = N // 2
+ma, mb, mo = a, vp(c.value), vp(b.value)
+L.check(lib.hpxhip_generate(L.U64, L.GEN_IOTA, 0, 0, 0, ma, h, st))
+L.check(lib.hpxhip_transform(L.U64, L.U64, L.U64, L.U_AFFINE, L.scalars_buf(L.U64, [2, 0]), ma, ma, h, st))
+L.check(lib.hpxhip_transform(L.U64, L.U64, L.U64, L.U_AFFINE, L.scalars_buf(L.U64, [1, 1]), ma, mb, h, st))
+timeit("merge u64 (2x2^29 -> 2^30)", lambda: lib.hpxhip_merge(L.U64, ma, h, mb, h, mo, 0, st, None, 0), 16 * N)
+code = ctypes.c_uint32(); L.check(lib.hpxhip_device_error(0, ctypes.byref(code))); print("deverr", code.value)
