@@ -258,6 +258,23 @@ def extras(hpx, L, ex, F, tgt, pol, x, y, n_local, world):
                            "gbs_model_16B": round(16 * nx * nt / ms / 1e6, 1), "pct_peak": pct(16 * nx * nt / ms / 1e6)}
     for v in st.U:
         v.free()
+    # host <-> device transfer (hpx/compute/cuda/transfer.hpp:188-348): 1 GiB,
+    # pinned (hpxhip_malloc_host) and pageable host buffers
+    nb = 1 << 30
+    dbuf = hpx.vector(nb // 8, dtype=np.uint64, tgt=tgt)
+    hp = ctypes.c_void_p()
+    L.call("hpxhip_malloc_host", ctypes.byref(hp), nb)
+    pageable = np.ones(nb // 8, np.uint64)
+    xfer = {}
+    for name, host in (("pinned", hp), ("pageable", pageable.ctypes.data_as(ctypes.c_void_p))):
+        for kind, (dst, src) in (("h2d", (ctypes.c_void_p(dbuf.data()), host)),
+                                 ("d2h", (host, ctypes.c_void_p(dbuf.data())))):
+            k = L.H2D if kind == "h2d" else L.D2H
+            ms = timed(L, tgt, lambda: L.call("hpxhip_memcpy_async", dst, src, nb, k, tgt.stream), reps=3)
+            xfer[f"{kind}_{name}_gbs"] = round(nb / ms / 1e6, 1)
+    L.call("hpxhip_free_host", hp)
+    dbuf.free()
+    res["host_device_copy_1GiB"] = xfer
     return res
 
 

@@ -263,6 +263,21 @@ class HipEngine:
     def halo_buffer(self):
         return vector(4, dtype=np.float64, value=0.0, tgt=self.tgt)
 
+    def read_values(self, buf, n):
+        out = np.empty(n, np.float64)
+        if n:
+            L.call("hpxhip_memcpy_async", out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(buf.data()), 8 * n,
+                   L.D2H, self.stream)
+            L.call("hpxhip_stream_synchronize", self.stream)
+        return out
+
+    def write_values(self, buf, vals):
+        vals = np.ascontiguousarray(vals, np.float64)
+        if vals.size:
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(buf.data()), vals.ctypes.data_as(ctypes.c_void_p),
+                   vals.nbytes, L.H2D, self.stream)
+            L.call("hpxhip_stream_synchronize", self.stream)
+
     def loc(self, buf, idx):
         return buf.data() + 8 * int(idx)
 
@@ -708,6 +723,47 @@ class heat_solver:
 
     def synchronize(self):
         self.eng.synchronize()
+
+    # --- checkpoint / restart (1d_stencil_4_checkpoint.cpp:145-191, 266-330)
+    _MAGIC = b"HPXHEAT1"
+
+    def save_checkpoint(self, path: str) -> str:
+        """Write this rank's partition at the current step to
+        ``{path}.part{rank}`` (the reference's backup::save + write: one
+        archive per checkpoint step holding every partition).  Format: 8-byte
+        magic, u64 nx, np, rank, t, lo, hi (6 x u64), f64 k, dt, dx, then hi-lo f64
+        values -- a flat dump, not HPX's serialization archive."""
+        import struct
+        self.synchronize()
+        vals = self.eng.read_values(self.current, self.n)
+        fn = f"{path}.part{self.comm.rank}"
+        with open(fn, "wb") as f:
+            f.write(self._MAGIC)
+            f.write(struct.pack("<6Q3d", self.nx, self.comm.size, self.comm.rank, self.t, self.lo, self.hi,
+                                self.k, self.dt, self.dx))
+            f.write(np.ascontiguousarray(vals, np.float64).tobytes())
+        return fn
+
+    def restore_checkpoint(self, path: str) -> int:
+        """backup::revive: load this rank's partition from
+        ``{path}.part{rank}``, continue from the saved step; returns it."""
+        import struct
+        fn = f"{path}.part{self.comm.rank}"
+        with open(fn, "rb") as f:
+            if f.read(8) != self._MAGIC:
+                raise ValueError(f"{fn}: not a 1d_stencil checkpoint")
+            nx, npart, rank, t, lo, hi = struct.unpack("<6Q", f.read(48))
+            k, dt, dx = struct.unpack("<3d", f.read(24))
+            if (nx, npart, rank, lo, hi) != (self.nx, self.comm.size, self.comm.rank, self.lo, self.hi):
+                raise ValueError(f"{fn}: checkpoint of a different partitioning ({nx=}, {npart=}, {rank=})")
+            vals = np.frombuffer(f.read(8 * (hi - lo)), np.float64)
+            if vals.size != hi - lo:
+                raise ValueError(f"{fn}: truncated")
+        self.k, self.dt, self.dx = k, dt, dx
+        self.t = int(t)
+        self.eng.write_values(self.current, vals)
+        self._exchange(self.current, self.t % 2, self.eng.stream)
+        return self.t
 
 
 # ------------------------------------------------------------- comm factory

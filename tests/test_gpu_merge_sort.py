@@ -141,3 +141,18 @@ def test_heat_solver_one_partition(gpu_target, nx, nt, kind):
     hs.synchronize()
     u0 = np.arange(nx, dtype=np.float64) if init is None else init
     np.testing.assert_array_equal(out.to_host(), O.stencil_heat(u0, nt))
+
+
+def test_heat_solver_checkpoint_restart(gpu_target, tmp_path):
+    """1d_stencil_4_checkpoint: save at step 5, revive into a fresh solver,
+    continue -- equals the uninterrupted run bit for bit."""
+    nx = (1 << 18) + 5
+    init = np.random.default_rng(3).standard_normal(nx)
+    hs = S.heat_solver(nx, S.LocalComm(gpu_target), gpu_target, init=init)
+    hs.do_work(5)
+    hs.save_checkpoint(str(tmp_path / "heat"))
+    hs2 = S.heat_solver(nx, S.LocalComm(gpu_target), gpu_target)
+    assert hs2.restore_checkpoint(str(tmp_path / "heat")) == 5
+    out = hs2.do_work(6)
+    hs2.synchronize()
+    np.testing.assert_array_equal(out.to_host(), O.stencil_heat(init, 11))

@@ -58,6 +58,12 @@ class HeatEngine:
         rv = right[0][right[1]]
         nxt[n_off:n_off + n] = O.stencil_heat_step(cur[c_off:c_off + n], lv, rv, k, dt, dx)
 
+    def read_values(self, buf, n):
+        return buf[:n].copy()
+
+    def write_values(self, buf, vals):
+        buf[:len(vals)] = vals
+
     def side_stream(self):
         return None
 
@@ -74,7 +80,7 @@ class HeatEngine:
 CASES = [(1001, 25, "ramp"), (1001, 25, "random"), (9, 7, "random"), (64, 40, "random")]
 
 
-def _worker(rank, size, port, q):
+def _worker(rank, size, port, q, ckdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=size)
     try:
@@ -89,7 +95,20 @@ def _worker(rank, size, port, q):
                 continue
             out = hs.do_work(nt)
             res[(nx, nt, kind)] = (hs.lo, out.copy())
+        # checkpoint after 7 steps, restart in a fresh solver, 9 more steps
+        nx = 1001
+        init = np.random.default_rng(5).standard_normal(nx)
+        hs = S.heat_solver(nx, comm, engine=HeatEngine(), init=init)
+        hs.do_work(7)
+        hs.save_checkpoint(os.path.join(ckdir, "heat_7"))
+        dist.barrier()
+        hs2 = S.heat_solver(nx, comm, engine=HeatEngine())
+        assert hs2.restore_checkpoint(os.path.join(ckdir, "heat_7")) == 7
+        res["restart"] = (hs2.lo, hs2.do_work(9).copy())
         q.put((rank, res))
+    except Exception as e:  # surface worker failures in the parent
+        q.put((rank, e))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -103,17 +122,18 @@ def _free_port():
 
 
 @pytest.mark.parametrize("size", [1, 2, 3, 4])
-def test_heat_solver_ring_gloo(size):
+def test_heat_solver_ring_gloo(size, tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, size, port, q)) for r in range(size)]
+    procs = [ctx.Process(target=_worker, args=(r, size, port, q, str(tmp_path))) for r in range(size)]
     for p in procs:
         p.start()
     results = dict(q.get(timeout=120) for _ in range(size))
     for p in procs:
         p.join(timeout=60)
-        assert p.exitcode == 0
+    for r in range(size):
+        assert not isinstance(results[r], Exception), results[r]
     for nx, nt, kind in CASES:
         u0 = np.arange(nx, dtype=np.float64) if kind == "ramp" else np.random.default_rng(nx).standard_normal(nx)
         exp = O.stencil_heat(u0, nt)
@@ -125,6 +145,13 @@ def test_heat_solver_ring_gloo(size):
             lo, loc = results[r][(nx, nt, kind)]
             got[lo:lo + loc.size] = loc
         np.testing.assert_array_equal(got, exp, err_msg=f"nx={nx} nt={nt} {kind} ranks={size}")
+    # restart from the step-7 checkpoint == an uninterrupted 16-step run
+    exp = O.stencil_heat(np.random.default_rng(5).standard_normal(1001), 16)
+    got = np.zeros(1001)
+    for r in range(size):
+        lo, loc = results[r]["restart"]
+        got[lo:lo + loc.size] = loc
+    np.testing.assert_array_equal(got, exp)
 
 
 def test_heat_solver_rejects_empty_partitions():
