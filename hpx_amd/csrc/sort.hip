@@ -33,7 +33,7 @@ using namespace hpxhip::sort_detail;
 namespace {
 
 constexpr int kHistThreads = 256;
-constexpr int kHistBlocksPerCU = 2;
+constexpr int kHistBlocksPerCU = 4;  // 4 lane copies x 8 KiB per pass histogram: 2.48 -> 1.87 ms (profiles/r01_ubench_sortpass2.log)
 
 // Tile shape per variant (scripts/ubench/sortpass.hip): keys only -> 512
 // threads x 16 keys = 8192-key tiles (64 KiB of u64 keys staged in LDS, 2

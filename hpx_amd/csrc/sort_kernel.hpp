@@ -20,43 +20,50 @@ template <typename G>
 __device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 1) | 1u); }
 
 // ---------------------------------------------------------------- histogram
-// One read of the keys -> all passes' 256-bin histograms.
-template <typename U, typename X, int THREADS = 256>
+// One read of the keys -> all passes' 256-bin histograms.  Each bin has
+// COPIES lane-private LDS counters (lane % COPIES), interleaved so that bin
+// b, copy c sits at word b*COPIES + c: lanes of one wave-instruction that hit
+// different bins then collide on a bank only when their bins agree mod
+// 32/COPIES, instead of mod 32 (the single-copy histogram spent 72 % of its
+// LDS cycles in bank conflicts, profiles/r01_pmc_sort.txt).  Keys are read
+// with nontemporal 16-B loads.
+template <typename U, typename X, int THREADS = 256, int COPIES = 4>
 __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, uint64_t n, int passes, X xf,
                                                    unsigned long long* __restrict__ hist) {
-    __shared__ uint32_t h[sizeof(U)][kRadix];
-    for (int i = threadIdx.x; i < static_cast<int>(sizeof(U)) * kRadix; i += THREADS) (&h[0][0])[i] = 0;
+    constexpr int P = static_cast<int>(sizeof(U));
+    __shared__ uint32_t h[P * kRadix * COPIES];
+    for (int i = threadIdx.x; i < P * kRadix * COPIES; i += THREADS) h[i] = 0;
     __syncthreads();
     constexpr int V = 16 / sizeof(U);
     using VT = vec<U, V>;
+    const uint32_t copy = threadIdx.x % COPIES;
     const uint64_t nvec = n / V;
     const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * THREADS + threadIdx.x;
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * THREADS;
     const VT* vk = reinterpret_cast<const VT*>(keys);
+    auto count = [&](U b) {
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+            if (p < passes) atomicAdd(&h[(p * kRadix + ((b >> (8 * p)) & 0xff)) * COPIES + copy], 1u);
+    };
     for (uint64_t i = tid; i < nvec; i += stride * 4) {
         VT x[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (i + u * stride < nvec) x[u] = vk[i + u * stride];
+            if (i + u * stride < nvec) x[u] = ld_stream(&vk[i + u * stride]);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if (i + u * stride < nvec) {
 #pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    const U b = xf(x[u].v[e]);
-#pragma unroll
-                    for (int p = 0; p < static_cast<int>(sizeof(U)); ++p)
-                        if (p < passes) atomicAdd(&h[p][(b >> (8 * p)) & 0xff], 1u);
-                }
+                for (int e = 0; e < V; ++e) count(xf(x[u].v[e]));
             }
     }
-    if (tid < n - nvec * V) {
-        const U b = xf(keys[nvec * V + tid]);
-        for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(b >> (8 * p)) & 0xff], 1u);
-    }
+    if (tid < n - nvec * V) count(xf(keys[nvec * V + tid]));
     __syncthreads();
     for (int i = threadIdx.x; i < passes * kRadix; i += THREADS) {
-        const uint32_t c = (&h[0][0])[i];
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < COPIES; ++k) c += h[i * COPIES + k];
         if (c) atomicAdd(&hist[i], static_cast<unsigned long long>(c));
     }
 }

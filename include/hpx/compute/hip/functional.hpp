@@ -31,6 +31,7 @@
 #include <hpxhip.h>
 
 #include <functional>
+#include <tuple>
 #include <type_traits>
 
 namespace hpx { namespace compute { namespace hip {
@@ -89,6 +90,23 @@ struct axpy {
     using compute_type = T;
     T a;
     T operator()(T x, T y) const { return x * a + y; }
+};
+
+// ---- for_loop bodies ----------------------------------------------------------
+// for_loop_n(policy, first, n, induction(b), induction(c), body) passes the
+// body one iterator per loop variable (position 0 = the loop iterator, then
+// the inductions in call order).  loop_assign<Out, F, In...> is the body
+// `*v[Out] = f(*v[In]...)`; for_loop_compute.cu:40-48's lambda
+// `*C = *A + 3.0 * *B` is loop_assign<2, triad_step<double>, 0, 1>{{3.0}}.
+template <std::size_t Out, typename F, std::size_t... In>
+struct loop_assign {
+    static_assert(sizeof...(In) == 1 || sizeof...(In) == 2, "loop_assign: one or two inputs");
+    F f;
+    template <typename... P>
+    void operator()(P... p) const {  // host meaning (pointers / iterators)
+        auto t = std::make_tuple(p...);
+        *std::get<Out>(t) = f(*std::get<In>(t)...);
+    }
 };
 
 // ---- reduction operators not in <functional> ------------------------------

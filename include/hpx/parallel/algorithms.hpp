@@ -452,6 +452,106 @@ detail::result_t<P, util::tagged_pair<KeyIt, ValIt>> sort_by_key(P&& p, KeyIt ke
     return detail::finish<R>(p, t, [key_last, vend] { return R{key_last, vend}; });
 }
 
+// ------------------------------------------------------------------ merge
+// merge.hpp:476: stable (first range first on ties), ascending / descending.
+template <typename P, typename In1, typename In2, typename Out, typename Comp = std::less<>>
+detail::result_t<P, util::tagged_tuple<In1, In2, Out>> merge(P&& p, In1 first1, In1 last1, In2 first2, In2 last2,
+                                                            Out dest, Comp&& = Comp()) {
+    static_assert(detail::is_dev<In1> && detail::is_dev<In2> && detail::is_dev<Out>, "merge: device iterators required");
+    using T = detail::value_t<In1>;
+    static_assert(std::is_same<T, detail::value_t<In2>>::value && std::is_same<T, detail::value_t<Out>>::value,
+                  "merge: one element type");
+    using R = util::tagged_tuple<In1, In2, Out>;
+    auto const& t = detail::target_of(p, first1);
+    uint64_t n1 = detail::distance(first1, last1), n2 = detail::distance(first2, last2);
+    detail::check(hpxhip_merge(detail::dt<T>, first1.device_ptr(), n1, first2.device_ptr(), n2, dest.device_ptr(),
+                               detail::tr::compare_t<Comp>::descending ? 1 : 0, t.stream(), nullptr, 0),
+                  "merge");
+    Out end = dest + static_cast<std::ptrdiff_t>(n1 + n2);
+    return detail::finish<R>(p, t, [last1, last2, end] { return R{last1, last2, end}; });
+}
+
+// --------------------------------------------------------------- for_loop
+// for_loop_induction.hpp:210-219: an induction over an iterator, value at
+// iteration i = it + stride * i (stride 1 on the device: contiguous kernels).
+template <typename It>
+struct induction_stride_helper {
+    It var_;
+    std::size_t stride_;
+};
+template <typename It>
+induction_stride_helper<It> induction(It it, std::size_t stride = 1) {
+    return induction_stride_helper<It>{it, stride};
+}
+
+namespace detail {
+template <typename It>
+It loop_var(It it) { return it; }
+template <typename It>
+It loop_var(induction_stride_helper<It> const& h) {
+    if (h.stride_ != 1)
+        throw hpx::exception(HPXHIP_ERROR_UNSUPPORTED,
+                             "for_loop_n: pointer inductions with stride != 1 are not supported by the contiguous "
+                             "elementwise kernels");
+    return h.var_;
+}
+template <typename P, typename Vars, std::size_t Out, typename F, std::size_t In0>
+result_t<P, void> for_loop_body(P&& p, Vars const& v, uint64_t n, compute::hip::functional::loop_assign<Out, F, In0> const& b) {
+    auto in = std::get<In0>(v);
+    auto out = std::get<Out>(v);
+    using TI = value_t<decltype(in)>;
+    using TO = value_t<decltype(out)>;
+    using Tr = tr::unary_t<F>;
+    using C = tr::compute_t<Tr, F, TI>;
+    auto const& t = target_of(p, in);
+    C s[2] = {};
+    Tr::scalars(b.f, s);
+    check(hpxhip_transform(dt<TI>, dt<C>, dt<TO>, Tr::kind, s, in.device_ptr(), out.device_ptr(), n, t.stream()),
+          "for_loop_n");
+    return finish<void>(p, t, [] {});
+}
+template <typename P, typename Vars, std::size_t Out, typename F, std::size_t In0, std::size_t In1>
+result_t<P, void> for_loop_body(P&& p, Vars const& v, uint64_t n,
+                                compute::hip::functional::loop_assign<Out, F, In0, In1> const& b) {
+    auto in0 = std::get<In0>(v);
+    auto in1 = std::get<In1>(v);
+    auto out = std::get<Out>(v);
+    using TI = value_t<decltype(in0)>;
+    static_assert(std::is_same<TI, value_t<decltype(in1)>>::value, "for_loop_n: both inputs need one element type");
+    using TO = value_t<decltype(out)>;
+    using Tr = tr::binary_t<F>;
+    using C = tr::compute_t<Tr, F, TI>;
+    auto const& t = target_of(p, in0);
+    C s[2] = {};
+    Tr::scalars(b.f, s);
+    check(hpxhip_transform_binary(dt<TI>, dt<C>, dt<TO>, Tr::kind, s, in0.device_ptr(), in1.device_ptr(),
+                                  out.device_ptr(), n, t.stream()),
+          "for_loop_n");
+    return finish<void>(p, t, [] {});
+}
+template <typename P, typename It, typename Tuple, std::size_t... I>
+auto for_loop_dispatch(P&& p, It first, uint64_t n, Tuple&& args, std::index_sequence<I...>) {
+    constexpr std::size_t last = std::tuple_size<std::decay_t<Tuple>>::value - 1;
+    auto vars = std::make_tuple(first, loop_var(std::get<I>(args))...);
+    return for_loop_body(std::forward<P>(p), vars, n, std::get<last>(args));
+}
+}  // namespace detail
+
+// for_loop.hpp:808 for_loop_n(policy, first, size, inductions..., body) with
+// a loop_assign body (the C ABI cannot carry arbitrary closures).
+template <typename P, typename It, typename Size, typename... Args>
+detail::result_t<P, void> for_loop_n(P&& p, It first, Size count, Args&&... args) {
+    static_assert(sizeof...(Args) >= 1, "for_loop_n: missing loop body");
+    static_assert(detail::is_dev<It>, "for_loop_n: the loop variable must be a device iterator");
+    uint64_t n = count > 0 ? static_cast<uint64_t>(count) : 0;
+    return detail::for_loop_dispatch(std::forward<P>(p), first, n, std::forward_as_tuple(args...),
+                                     std::make_index_sequence<sizeof...(Args) - 1>{});
+}
+template <typename P, typename It, typename... Args>
+detail::result_t<P, void> for_loop(P&& p, It first, It last, Args&&... args) {
+    return for_loop_n(std::forward<P>(p), first, detail::distance(first, last), std::forward<Args>(args)...);
+}
+
 }  // namespace v1
 }}  // namespace hpx::parallel
 
@@ -465,6 +565,10 @@ using parallel::v1::fill;
 using parallel::v1::fill_n;
 using parallel::v1::for_each;
 using parallel::v1::for_each_n;
+using parallel::v1::for_loop;
+using parallel::v1::for_loop_n;
+using parallel::v1::induction;
+using parallel::v1::merge;
 using parallel::v1::inclusive_scan;
 using parallel::v1::reduce;
 using parallel::v1::sort;
