@@ -64,11 +64,22 @@ class Events:
         return f.value
 
 
+def max_over_ranks(comm, v: float) -> float:
+    """Max of a host float over the ranks (one small all-gather)."""
+    if comm.size == 1:
+        return v
+    g = comm.allgather_host(np.array([v], np.float64).view(np.int64))
+    return float(np.asarray(g).view(np.float64).max())
+
+
 def pct(gbs):
     return round(100.0 * gbs / HBM_PEAK_GBS, 2)
 
 
-def main():
+def main(argv=None, comm_tgt=None):
+    """argv: command line (default sys.argv); comm_tgt: an already built
+    (communicator, target) pair -- the multi-rank test drives the N > 1 path
+    through it on one GPU (tests/test_gpu_bench_ranks.py)."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -79,7 +90,7 @@ def main():
     ap.add_argument("--cpu-logn", type=int, default=27)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--triad-only", action="store_true", help=argparse.SUPPRESS)  # PMC child mode
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.triad_only:
         return triad_only(args.logn)
 
@@ -87,7 +98,7 @@ def main():
     from hpx_amd import _lib as L
     from hpx_amd import execution as ex, functional as F, segmented as S
 
-    comm, tgt = S.init_distributed()
+    comm, tgt = comm_tgt if comm_tgt is not None else S.init_distributed()
     rank, world = comm.rank, comm.size
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
@@ -141,12 +152,7 @@ def main():
     tgt.synchronize()
     comm.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{tgt.device}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(comm, elapsed)
 
     # per-kernel HIP-event timings (segment-local kernels + their collectives)
     k_triad = np.mean([ev.ms(m[0], m[1]) for m in marks])
@@ -209,9 +215,10 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        comm.barrier()
         import torch.distributed as dist
-        dist.barrier()
-        dist.destroy_process_group()
+        if dist.is_initialized():
+            dist.destroy_process_group()
 
 
 def timed(L, tgt, fn, reps=3):
@@ -289,15 +296,10 @@ def dist_extras(S, F, comm, tgt, pol, n_local, world):
         ring over RCCL send/recv overlapped with the interior update;
         checked: ramp interior unchanged (steady state away from the wrap)."""
     import time
-    import torch
-    import torch.distributed as dist
     res = {}
-    dev = torch.device("cuda", tgt.device)
 
     def tmax(v):
-        t = torch.tensor([v], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return max_over_ranks(comm, v)
 
     n = n_local * world
     keys = S.partitioned_vector(n, np.uint64, comm=comm, tgt=tgt)
@@ -329,7 +331,7 @@ def dist_extras(S, F, comm, tgt, pol, n_local, world):
     res["segmented_sort_uint64"] = {"keys_per_gpu": n_local, "keys_total": n, "ms": round(1e3 * best, 3),
                                     "gkeys_per_s": round(n / best / 1e9, 3), "ordered_across_partitions": bool(ok)}
     loc.free()
-    nx = 1 << 32
+    nx = min(1 << 32, 4 * n)   # 2^32 points at the benchmark sizes
     hs = S.heat_solver(nx, comm, tgt)
     hs.do_work(1)
     hs.synchronize()

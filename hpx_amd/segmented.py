@@ -58,6 +58,9 @@ class LocalComm:
         self.tgt = tgt or target(0)
         self._buf = None
 
+    def allgather_host(self, words):
+        return np.ascontiguousarray(words, np.int64).reshape(1, -1)
+
     def slots(self, nbytes: int):
         """(send_ptr, recv_ptr) device buffers for one all-gather."""
         if self._buf is None:
