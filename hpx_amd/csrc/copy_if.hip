@@ -161,17 +161,14 @@ __global__ void k_zero_count(uint64_t* c) {
 
 struct cif_layout {
     uint64_t ntiles;
-    size_t flags_off, agg_off, incl_off, total, memset_bytes;
+    size_t slots_off, total;  // [counter | tile slots], all zeroed per call
 };
 
 cif_layout make_layout(uint64_t n, uint64_t tile) {
     cif_layout L;
     L.ntiles = (n + tile - 1) / tile;
-    L.flags_off = 256;
-    L.agg_off = align_up(L.flags_off + L.ntiles * 4, 256);
-    L.memset_bytes = L.agg_off;
-    L.incl_off = align_up(L.agg_off + L.ntiles * 8, 256);
-    L.total = align_up(L.incl_off + L.ntiles * 8, 256);
+    L.slots_off = 256;
+    L.total = align_up(L.slots_off + L.ntiles * tile_state<uint64_t>::bytes_per_tile(), 256);
     return L;
 }
 
@@ -203,10 +200,8 @@ extern "C" int hpxhip_copy_if(int dtype, int pred_kind, const void* pred_arg, co
             int rc = resolve_scratch(s, scratch, scratch_bytes, L.total, &ws);
             if (rc) return rc;
             char* base = static_cast<char*>(ws);
-            HPXHIP_CHECK(hipMemsetAsync(base, 0, L.memset_bytes, s));
-            tile_state<uint64_t> st{reinterpret_cast<uint32_t*>(base + L.flags_off),
-                                    reinterpret_cast<uint64_t*>(base + L.agg_off),
-                                    reinterpret_cast<uint64_t*>(base + L.incl_off), device_error_word(s)};
+            HPXHIP_CHECK(hipMemsetAsync(base, 0, L.total, s));
+            tile_state<uint64_t> st{reinterpret_cast<uint64_t*>(base + L.slots_off), device_error_word(s)};
             uint32_t* counter = reinterpret_cast<uint32_t*>(base);
             const bool aligned = reinterpret_cast<uintptr_t>(in) % 16 == 0;
             const dim3 grid(static_cast<unsigned>(L.ntiles)), block(kThreads);

@@ -9,11 +9,19 @@
 //
 // Tile ids come from an atomic counter, so a tile only ever waits on tiles
 // whose workgroups are already running (forward progress does not depend on
-// dispatch order).  Hand-off form (MI355X guide, Guideline 16 table row 1):
-// the value is stored with an agent-scope sc1 store, the lane drains
-// (`s_waitcnt vmcnt(0)`), then stores the flag; the consumer polls the flag
-// with sc1 loads and only after the poll matched loads the value with sc1.
-// Every wait is bounded (kSpinLimit) and raises the device error word.
+// dispatch order).
+//
+// Hand-off form: the data IS the flag (MI355X guide, Guideline 16 recipe R2).
+// A value is published as 8-byte granules {status tag : 32, value word : 32},
+// each written by one agent-scope relaxed (sc1) 8-byte store; a 64-bit value
+// is two granules.  The reader polls the granules themselves with sc1 loads
+// and accepts a slot only when every granule carries the slot's tag, so no
+// store drain sits between value and flag (the earlier value-then-drain-
+// then-flag form put two write-through round trips on every tile's critical
+// path).  Aggregate and inclusive values live in separate slots, each written
+// once per call, so a reader never mixes the halves of two different values.
+// Slots are zeroed (TILE_INVALID) by the per-call memset.  Every wait is
+// bounded (kSpinLimit) and raises the device error word.
 #pragma once
 
 #include "common.hpp"
@@ -24,16 +32,52 @@ enum : uint32_t { TILE_INVALID = 0, TILE_AGGREGATE = 1, TILE_INCLUSIVE = 2 };
 
 template <typename T>
 struct tile_state {
-    uint32_t* flags;  // [ntiles]
-    T* agg;           // [ntiles]
-    T* incl;          // [ntiles]
+    static constexpr int G = sizeof(T) / 4;  // granules per value (1 or 2)
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4/8-byte tile values only");
+
+    uint64_t* slots;  // [ntiles][2 (aggregate, inclusive)][G]
     uint32_t* err;    // device error word (may be null)
+
+    static constexpr size_t bytes_per_tile() { return 2 * G * sizeof(uint64_t); }
 
     // Lane-uniform call by ONE lane.
     __device__ __forceinline__ void publish(uint64_t tile, T v, uint32_t status) const {
-        st_agent(status == TILE_INCLUSIVE ? &incl[tile] : &agg[tile], v);
-        drain_stores();
-        __hip_atomic_store(&flags[tile], status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t w[G];
+        to_words(v, w);
+        uint64_t* p = slots + (tile * 2 + (status == TILE_INCLUSIVE ? 1 : 0)) * G;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            __hip_atomic_store(&p[g], (static_cast<uint64_t>(status) << 32) | w[g], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    // Status and value of tile j's best published slot (TILE_INVALID if none).
+    __device__ __forceinline__ uint32_t read(uint64_t j, T* v) const {
+        const uint64_t* p = slots + j * 2 * G;
+        uint64_t a[G], c[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            c[g] = __hip_atomic_load(&p[G + g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a[g] = __hip_atomic_load(&p[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bool inc = true, agg = true;
+        uint32_t wc[G], wa[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            inc = inc && static_cast<uint32_t>(c[g] >> 32) == TILE_INCLUSIVE;
+            agg = agg && static_cast<uint32_t>(a[g] >> 32) == TILE_AGGREGATE;
+            wc[g] = static_cast<uint32_t>(c[g]);
+            wa[g] = static_cast<uint32_t>(a[g]);
+        }
+        if (inc) {
+            *v = from_words<T>(wc);
+            return TILE_INCLUSIVE;
+        }
+        if (agg) {
+            *v = from_words<T>(wa);
+            return TILE_AGGREGATE;
+        }
+        return TILE_INVALID;
     }
 
     // Called by ALL 64 lanes of one wave; returns the exclusive prefix of
@@ -48,12 +92,12 @@ struct tile_state {
         uint32_t spins = 0;
         while (true) {
             const int64_t j = pred - lane;
+            T v = id;
             uint32_t f = TILE_INCLUSIVE;  // j < 0: behind tile 0, never reached
-            if (j >= 0) f = __hip_atomic_load(&flags[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (j >= 0) f = read(static_cast<uint64_t>(j), &v);
             while (!__all(f != TILE_INVALID)) {
                 __builtin_amdgcn_s_sleep(1);
-                if (f == TILE_INVALID)
-                    f = __hip_atomic_load(&flags[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (f == TILE_INVALID) f = read(static_cast<uint64_t>(j), &v);
                 if (++spins > kSpinLimit) {
                     if (lane == 0 && err)
                         __hip_atomic_store(err, HPXHIP_DEVERR_LOOKBACK_TIMEOUT, __ATOMIC_RELAXED,
@@ -61,12 +105,9 @@ struct tile_state {
                     return excl;
                 }
             }
-            order_after_poll();
             const uint64_t inclusive_lanes = __ballot(f == TILE_INCLUSIVE);
             const int first = inclusive_lanes ? __builtin_ctzll(inclusive_lanes) : kWave;
-            T v = id;
-            if (lane < first) v = ld_agent(&agg[j]);
-            else if (lane == first && j >= 0) v = ld_agent(&incl[j]);
+            if (lane > first) v = id;
             const T s = wave_reduce(v, op);
             excl = op(s, excl);
             if (first < kWave) break;

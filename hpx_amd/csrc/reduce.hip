@@ -12,12 +12,13 @@
 //     all 8 loads in flight before the fold, nontemporal (6.91 TB/s for
 //     the bare stream, scripts/ubench/rd2.hip);
 //   * per thread a serial fold, DPP wave64 reduction, LDS across waves, one
-//     partial per block;
-//   * two-level deterministic fold inside the same launch: the last block to
-//     arrive in each group of 256 blocks folds that group's partials in
-//     block order, and the last group folder folds the group partials.
-//     Partials are stored sc1 and drained before the agent-scope ticket add,
-//     and read with sc1 loads after it (MI355X guide, Guideline 16 row 1).
+//     partial per block, written with a plain store as the block retires;
+//   * a second one-block launch folds the partials in a fixed order.
+//     (The first version folded inside the same launch: the last block to
+//     arrive behind agent-scope tickets folded the partials.  The drain +
+//     ticket round trip held every 1024-thread block ~2 us past its last
+//     load, which at two blocks per CU cost 1.45 ms against 1.24 ms for the
+//     bare read stream; the extra launch costs a few microseconds.)
 // The reduction tree depends only on n, so FP results are bitwise
 // reproducible run to run; integer results are exact.
 #include "internal.hpp"
@@ -28,8 +29,7 @@ namespace {
 
 constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / kWave;
-constexpr int kSteps = 8;        // vectors per thread per block
-constexpr uint32_t kGroup = 256;  // blocks per first-level fold group
+constexpr int kSteps = 8;  // vectors per thread per block
 
 struct reduce_geom {
     uint64_t head, nvec, tail;
@@ -60,18 +60,11 @@ __device__ __forceinline__ T block_reduce(T x, Op op, T* lds) {
     return r;  // valid in wave 0
 }
 
-struct tickets {
-    uint32_t* group;  // [ngroups]
-    uint32_t* top;    // [1]
-};
-
 template <typename TI, typename TA, typename Conv, typename Op, bool BINARY, int V>
 __global__ __launch_bounds__(kThreads) void k_reduce(source<TI, TA, Conv, BINARY> src, reduce_geom g, Op op, TA init,
-                                                      TA* __restrict__ partials, TA* __restrict__ group_partials,
-                                                      tickets tk, TA* __restrict__ out) {
+                                                      TA* __restrict__ partials, TA* __restrict__ out) {
     using VI = vec<TI, V>;
     __shared__ TA lds[kWaves];
-    __shared__ int s_flag;
 
     const TA id = Op::template identity<TA>();
     const uint64_t tid = threadIdx.x;
@@ -122,43 +115,35 @@ __global__ __launch_bounds__(kThreads) void k_reduce(source<TI, TA, Conv, BINARY
     }
 
     const TA blk = block_reduce(acc, op, lds);
-    if (gridDim.x == 1) {
-        if (tid == 0) *out = op(init, blk);
-        return;
-    }
-
-    // ---- level 1: last arriver of each group folds the group's partials
-    const uint32_t group = blockIdx.x / kGroup;
-    const uint32_t ngroups = (gridDim.x + kGroup - 1) / kGroup;
-    const uint32_t gfirst = group * kGroup;
-    const uint32_t gsize = min(kGroup, gridDim.x - gfirst);
     if (tid == 0) {
-        st_agent(&partials[blockIdx.x], blk);
-        drain_stores();
-        const uint32_t t = __hip_atomic_fetch_add(&tk.group[group], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_flag = (t == gsize - 1) ? 1 : 0;
+        if (gridDim.x == 1) *out = op(init, blk);
+        else partials[blockIdx.x] = blk;
     }
-    __syncthreads();
-    if (!s_flag) return;
-    order_after_poll();
-    __syncthreads();  // lds reuse
-    const TA gv = block_reduce(tid < gsize ? ld_agent(&partials[gfirst + tid]) : id, op, lds);
+}
 
-    // ---- level 2: last group folder folds the group partials
-    if (tid == 0) {
-        st_agent(&group_partials[group], gv);
-        drain_stores();
-        const uint32_t t = __hip_atomic_fetch_add(tk.top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_flag = (t == ngroups - 1) ? 1 : 0;
-    }
-    __syncthreads();
-    if (!s_flag) return;
-    order_after_poll();
+// Fold of the block partials (one block; the previous launch's stores are
+// visible at the kernel boundary).  Thread t folds partials t, t + 1024, ...
+// with kBatch loads in flight, then the block tree: a fixed order for a given
+// partial count.
+template <typename TA, typename Op>
+__global__ __launch_bounds__(kThreads) void k_reduce_partials(const TA* __restrict__ partials, uint32_t count, Op op,
+                                                              TA init, TA* __restrict__ out) {
+    constexpr int kBatch = 16;
+    __shared__ TA lds[kWaves];
+    const TA id = Op::template identity<TA>();
     TA r = id;
-    for (uint32_t i = tid; i < ngroups; i += kThreads) r = op(r, ld_agent(&group_partials[i]));
-    __syncthreads();
+    for (uint32_t i0 = 0; i0 < count; i0 += kThreads * kBatch) {
+        TA v[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const uint32_t i = i0 + k * kThreads + threadIdx.x;
+            v[k] = i < count ? partials[i] : id;
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) r = op(r, v[k]);
+    }
     const TA total = block_reduce(r, op, lds);
-    if (tid == 0) *out = op(init, total);
+    if (threadIdx.x == 0) *out = op(init, total);
 }
 
 template <typename TA, typename Op>
@@ -167,8 +152,8 @@ __global__ void k_write_init(TA init, TA* out) {
 }
 
 struct reduce_layout {
-    uint64_t blocks, ngroups;
-    size_t tickets_bytes, partials_off, group_off, total;
+    uint64_t blocks;
+    size_t total;
 };
 
 reduce_layout make_layout(uint64_t n) {
@@ -178,11 +163,7 @@ reduce_layout make_layout(uint64_t n) {
     const uint64_t nvec = n;  // upper bound on vectors for V >= 1
     L.blocks = (nvec + per_block - 1) / per_block;
     if (L.blocks == 0) L.blocks = 1;
-    L.ngroups = (L.blocks + kGroup - 1) / kGroup;
-    L.tickets_bytes = align_up(16 + L.ngroups * 4, 256);  // [top ticket | group tickets]
-    L.partials_off = L.tickets_bytes;
-    L.group_off = align_up(L.partials_off + L.blocks * 8, 256);
-    L.total = align_up(L.group_off + L.ngroups * 8, 256);
+    L.total = align_up(L.blocks * 8, 256);
     return L;
 }
 
@@ -198,11 +179,7 @@ int launch_reduce(const TI* a, const TI* b, uint64_t n, Conv conv, Op op, TA ini
     void* ws = nullptr;
     int rc = resolve_scratch(s, scratch, scratch_bytes, L.total, &ws);
     if (rc) return rc;
-    char* base = static_cast<char*>(ws);
-    tickets tk{reinterpret_cast<uint32_t*>(base + 16), reinterpret_cast<uint32_t*>(base)};
-    TA* partials = reinterpret_cast<TA*>(base + L.partials_off);
-    TA* gpart = reinterpret_cast<TA*>(base + L.group_off);
-    HPXHIP_CHECK(hipMemsetAsync(base, 0, L.tickets_bytes, s));
+    TA* partials = static_cast<TA*>(ws);
 
     constexpr int V = 16 / sizeof(TI);
     source<TI, TA, Conv, BINARY> src{a, b, conv};
@@ -210,25 +187,31 @@ int launch_reduce(const TI* a, const TI* b, uint64_t n, Conv conv, Op op, TA ini
     uint64_t ha = head_to_align16(a, sizeof(TI));
     uint64_t hb = BINARY ? head_to_align16(b, sizeof(TI)) : ha;
     const uint64_t per_block = static_cast<uint64_t>(kThreads) * kSteps;
+    uint64_t blocks = 0;
     if (ha != UINT64_MAX && ha == hb) {
         if (ha > n) ha = n;
         g.head = ha;
         g.nvec = (n - ha) / V;
         g.tail = n - ha - g.nvec * V;
-        uint64_t blocks = (g.nvec + per_block - 1) / per_block;
+        blocks = (g.nvec + per_block - 1) / per_block;
         if (blocks == 0) blocks = 1;
         hipLaunchKernelGGL((k_reduce<TI, TA, Conv, Op, BINARY, V>), dim3(static_cast<unsigned>(blocks)),
-                           dim3(kThreads), 0, s, src, g, op, init, partials, gpart, tk, out);
+                           dim3(kThreads), 0, s, src, g, op, init, partials, out);
     } else if constexpr (BINARY) {
         // Inputs that cannot be aligned together: scalar loads.
         g = reduce_geom{0, n, 0};
-        const uint64_t blocks = (n + per_block - 1) / per_block;
+        blocks = (n + per_block - 1) / per_block;
         hipLaunchKernelGGL((k_reduce<TI, TA, Conv, Op, BINARY, 1>), dim3(static_cast<unsigned>(blocks)),
-                           dim3(kThreads), 0, s, src, g, op, init, partials, gpart, tk, out);
+                           dim3(kThreads), 0, s, src, g, op, init, partials, out);
     } else {
         return HPXHIP_ERROR_INVALID_ARGUMENT;  // pointer not element-aligned
     }
     HPXHIP_CHECK_LAUNCH();
+    if (blocks > 1) {
+        hipLaunchKernelGGL((k_reduce_partials<TA, Op>), dim3(1), dim3(kThreads), 0, s, partials,
+                           static_cast<uint32_t>(blocks), op, init, out);
+        HPXHIP_CHECK_LAUNCH();
+    }
     return 0;
 }
 

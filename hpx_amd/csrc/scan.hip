@@ -5,9 +5,10 @@
 // once and written twice plus a re-read (section 3.3 of SURVEY.md).  Here:
 // one pass, 16 B/element of HBM traffic (read once, write once).
 //
-// Tile = 256 threads x 8 vectors of 16 B (4096 int64 / 8192 int32 = 32 KiB).
-// Each wave owns a contiguous quarter of the tile and walks it in 8 rounds of
-// 64 lanes x 16 B (coalesced 1 KiB per instruction):
+// Tile = 1024 threads x 16 vectors of 16 B (32768 int64 / 65536 int32 =
+// 256 KiB, scan_kernel.hpp).  Each wave owns a contiguous sixteenth of the
+// tile and walks it in 16 rounds of 64 lanes x 16 B (coalesced 1 KiB per
+// instruction):
 //   round r:  lane-serial scan of its V elements -> DPP wave scan of lane
 //             totals -> running wave carry (readlane 63);
 //   then      wave totals through LDS -> tile aggregate -> decoupled look-back
@@ -25,23 +26,31 @@ namespace {
 
 using namespace hpxhip::scan_detail;
 
-template <typename T>
-struct scan_layout {
-    uint64_t ntiles;
-    size_t flags_off, agg_off, incl_off, total;
-    size_t memset_bytes;  // counter + flags, from the allocation start
-};
+// Scratch: [counter | tile slots], zeroed per call.  Sized for the variant
+// with the smallest tiles (8 rounds), so one size serves every launch.
+constexpr size_t kSlotsOff = 256;
+
+template <typename T, int ROUNDS>
+uint64_t ntiles_for(uint64_t n) {
+    return (n + tile_elems<T, ROUNDS>() - 1) / tile_elems<T, ROUNDS>();
+}
 
 template <typename T>
-scan_layout<T> make_layout(uint64_t n) {
-    scan_layout<T> L;
-    L.ntiles = (n + tile_elems<T>() - 1) / tile_elems<T>();
-    L.flags_off = 256;
-    L.agg_off = align_up(L.flags_off + L.ntiles * 4, 256);
-    L.memset_bytes = L.agg_off;
-    L.incl_off = align_up(L.agg_off + L.ntiles * sizeof(T), 256);
-    L.total = align_up(L.incl_off + L.ntiles * sizeof(T), 256);
-    return L;
+size_t scratch_total(uint64_t n) {
+    return align_up(kSlotsOff + ntiles_for<T, 8>(n) * tile_state<T>::bytes_per_tile(), 256);
+}
+
+template <typename T, bool INCL, bool ALIGNED, typename Conv, typename Op>
+int launch_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init, const T* prefix_dev, char* ws,
+                hipStream_t s) {
+    constexpr int R = rounds_for<T, ALIGNED>();
+    const uint64_t ntiles = ntiles_for<T, R>(n);
+    HPXHIP_CHECK(hipMemsetAsync(ws, 0, align_up(kSlotsOff + ntiles * tile_state<T>::bytes_per_tile(), 256), s));
+    tile_state<T> st{reinterpret_cast<uint64_t*>(ws + kSlotsOff), device_error_word(s)};
+    hipLaunchKernelGGL((k_scan<T, Conv, Op, INCL, ALIGNED, R>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads),
+                       0, s, in, out, n, conv, op, init, prefix_dev, reinterpret_cast<uint32_t*>(ws), st);
+    HPXHIP_CHECK_LAUNCH();
+    return 0;
 }
 
 template <typename T, typename F>
@@ -67,7 +76,7 @@ int with_scan_conv(int kind, const void* scalars, F&& f) {
 
 namespace hpxhip {
 size_t scan_scratch_bytes(int dtype, uint64_t n) {
-    return dtype_size(dtype) == 8 ? make_layout<uint64_t>(n).total : make_layout<uint32_t>(n).total;
+    return dtype_size(dtype) == 8 ? scratch_total<uint64_t>(n) : scratch_total<uint32_t>(n);
 }
 }  // namespace hpxhip
 
@@ -84,42 +93,21 @@ extern "C" int hpxhip_scan(int dtype, int op, int inclusive, int conv_kind, cons
         T iv = T(0);
         if (init) __builtin_memcpy(&iv, init, sizeof(T));
         return with_binop<T>(op, [&](auto o) -> int {
-            using Op = decltype(o);
             return with_scan_conv<T>(conv_kind, conv_scalars, [&](auto conv) -> int {
-                using Conv = decltype(conv);
-                const scan_layout<T> L = make_layout<T>(n);
                 void* ws = nullptr;
-                int rc = resolve_scratch(s, scratch, scratch_bytes, L.total, &ws);
+                int rc = resolve_scratch(s, scratch, scratch_bytes, scratch_total<T>(n), &ws);
                 if (rc) return rc;
                 char* base = static_cast<char*>(ws);
-                HPXHIP_CHECK(hipMemsetAsync(base, 0, L.memset_bytes, s));
-                tile_state<T> st{reinterpret_cast<uint32_t*>(base + L.flags_off),
-                                 reinterpret_cast<T*>(base + L.agg_off), reinterpret_cast<T*>(base + L.incl_off),
-                                 device_error_word(s)};
-                uint32_t* counter = reinterpret_cast<uint32_t*>(base);
                 const bool aligned = (reinterpret_cast<uintptr_t>(in) % 16 == 0) &&
                                      (reinterpret_cast<uintptr_t>(out) % 16 == 0);
                 const T* pd = static_cast<const T*>(prefix_dev);
-                const dim3 grid(static_cast<unsigned>(L.ntiles)), block(kThreads);
                 const T* ip = static_cast<const T*>(in);
                 T* op_ = static_cast<T*>(out);
-                if (inclusive) {
-                    if (aligned)
-                        hipLaunchKernelGGL((k_scan<T, Conv, Op, true, true>), grid, block, 0, s, ip, op_, n, conv, o,
-                                           iv, pd, counter, st);
-                    else
-                        hipLaunchKernelGGL((k_scan<T, Conv, Op, true, false>), grid, block, 0, s, ip, op_, n, conv, o,
-                                           iv, pd, counter, st);
-                } else {
-                    if (aligned)
-                        hipLaunchKernelGGL((k_scan<T, Conv, Op, false, true>), grid, block, 0, s, ip, op_, n, conv, o,
-                                           iv, pd, counter, st);
-                    else
-                        hipLaunchKernelGGL((k_scan<T, Conv, Op, false, false>), grid, block, 0, s, ip, op_, n, conv,
-                                           o, iv, pd, counter, st);
-                }
-                HPXHIP_CHECK_LAUNCH();
-                return 0;
+                if (inclusive)
+                    return aligned ? launch_scan<T, true, true>(ip, op_, n, conv, o, iv, pd, base, s)
+                                   : launch_scan<T, true, false>(ip, op_, n, conv, o, iv, pd, base, s);
+                return aligned ? launch_scan<T, false, true>(ip, op_, n, conv, o, iv, pd, base, s)
+                               : launch_scan<T, false, false>(ip, op_, n, conv, o, iv, pd, base, s);
             });
         });
     });

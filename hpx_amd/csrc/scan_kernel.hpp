@@ -9,13 +9,30 @@
 namespace hpxhip {
 namespace scan_detail {
 
-// Shipped tile shape: 1024 threads x 8 vectors of 16 B = 128 KiB per tile.
-// Tile ids come from one atomic counter, which saturates at ~88 increments
-// per microsecond (MI355X guide, row `dequeue`): at 32 KiB tiles the counter,
-// not HBM, bounded the scan (measured 3.3 ms for 2^30 int64 even with the
-// look-back removed); 128 KiB tiles cut the counter time 4x.
+// Shipped tile shape: 1024 threads x 16 vectors of 16 B = 256 KiB per tile,
+// one workgroup per CU (122 VGPRs).  Tile ids come from one atomic counter,
+// which saturates at ~88 increments per microsecond (MI355X guide, row
+// `dequeue`): at 32 KiB tiles the counter, not HBM, bounded the scan
+// (measured 3.3 ms for 2^30 int64 even with the look-back removed).  Fewer,
+// larger tiles also mean fewer look-back hand-offs: at 2^30 int64 the same
+// kernel takes 2.99 ms with 128 KiB tiles (two workgroups per CU), 2.85 ms
+// with 192 KiB and 2.82 ms with 256 KiB (scripts/ubench/scan.hip,
+// profiles/r01_ubench_scan_structure.log).  A variant with a dedicated
+// look-back wave (15 loading waves + 1) was slower at every tile size.
 constexpr int kThreads = 1024;
-constexpr int kRounds = 8;
+constexpr int kRounds = 16;
+
+// Rounds per launch variant: 16 where the kernel fits 128 VGPRs without
+// spilling (aligned integer scans); the FP scans (no reassociation, DPP moves
+// not fused into the 64-bit FP adds) and the element-wise unaligned path
+// spill at 16 and use kRoundsFP / 8.
+constexpr int kRoundsFP = 12;
+template <typename T, bool ALIGNED>
+constexpr int rounds_for() {
+    if constexpr (!ALIGNED) return 8;
+    else if constexpr (std::is_integral_v<T>) return kRounds;
+    else return kRoundsFP;
+}
 
 template <typename T, int ROUNDS = kRounds, int THREADS = kThreads>
 constexpr uint64_t tile_elems() {

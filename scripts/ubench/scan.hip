@@ -1,5 +1,7 @@
 // Microbenchmark: the shipped scan kernel (scan_kernel.hpp) at several tile
-// shapes, with and without the look-back (ablation), 2^30 int64.
+// shapes, with and without the look-back (ablation), 2^30 int64, all in one
+// process so the comparison shares one box.
+// build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../include scan.hip -o scan
 #include "../../hpx_amd/csrc/scan_kernel.hpp"
 #include "../../hpx_amd/csrc/internal.hpp"
 #include <cstdio>
@@ -7,7 +9,6 @@
 #include <algorithm>
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 using namespace hpxhip;
-using namespace hpxhip::scan_detail;
 using T = int64_t;
 using Conv = unary_fn<HPXHIP_U_IDENTITY, T>;
 
@@ -25,33 +26,30 @@ int main() {
     std::sort(t.begin(), t.end());
     const double B = 16.0 * N;
     printf("%-34s min %7.3f ms med %7.3f ms  %7.1f GB/s (med %7.1f)\n", name, t[0], t[7], B / t[0] / 1e6, B / t[7] / 1e6);
+    fflush(stdout);
   };
   auto variant = [&](auto rounds_c, auto threads_c, auto lb_c, const char* name) {
     constexpr int R = decltype(rounds_c)::value;
     constexpr int TH = decltype(threads_c)::value;
     constexpr bool LB = decltype(lb_c)::value;
-    const uint64_t tile = tile_elems<T, R, TH>();
+    const uint64_t tile = scan_detail::tile_elems<T, R, TH>();
     const uint64_t ntiles = (N + tile - 1) / tile;
-    const size_t flags_off = 256, agg_off = align_up(flags_off + ntiles * 4, 256);
-    const size_t incl_off = align_up(agg_off + ntiles * 8, 256);
-    tile_state<T> st{reinterpret_cast<uint32_t*>(ws + flags_off), reinterpret_cast<T*>(ws + agg_off),
-                     reinterpret_cast<T*>(ws + incl_off), err};
+    const size_t total = align_up(256 + ntiles * tile_state<T>::bytes_per_tile(), 256);
+    tile_state<T> st{reinterpret_cast<uint64_t*>(ws + 256), err};
     run(name, [&] {
-      CK(hipMemsetAsync(ws, 0, agg_off, 0));
-      k_scan<T, Conv, op_plus, true, true, R, TH, LB><<<ntiles, TH>>>(in, out, N, Conv{0, 0}, op_plus{}, T(0), nullptr,
-                                                                   reinterpret_cast<uint32_t*>(ws), st);
+      CK(hipMemsetAsync(ws, 0, total, 0));
+      scan_detail::k_scan<T, Conv, op_plus, true, true, R, TH, LB><<<ntiles, TH>>>(
+            in, out, N, Conv{0, 0}, op_plus{}, T(0), nullptr, reinterpret_cast<uint32_t*>(ws), st);
     });
   };
-#define V_(R, TH, LB, NAME) variant(std::integral_constant<int, R>{}, std::integral_constant<int, TH>{}, std::integral_constant<bool, LB>{}, NAME)
-  V_(8, 256, true, "T256 R8 lookback");
-  V_(16, 256, true, "T256 R16 lookback");
-  V_(8, 512, true, "T512 R8 lookback");
-  V_(16, 512, true, "T512 R16 lookback");
-  V_(4, 1024, true, "T1024 R4 lookback");
-  V_(8, 1024, true, "T1024 R8 lookback");
-  V_(8, 1024, false, "T1024 R8 no-lookback");
-  V_(16, 1024, true, "T1024 R16 lookback");
-  V_(16, 512, false, "T512 R16 no-lookback");
+#define V_(R, TH, LB, NAME) variant(std::integral_constant<int, R>{}, std::integral_constant<int, TH>{}, \
+    std::integral_constant<bool, LB>{}, NAME)
+  for (int rep = 0; rep < 2; ++rep) {
+    V_(8, 1024, true, "T1024 R8 lookback");
+    V_(12, 1024, true, "T1024 R12 lookback");
+    V_(16, 1024, true, "T1024 R16 lookback (shipped)");
+    V_(16, 1024, false, "T1024 R16 no-lookback");
+  }
   uint32_t h = 0; CK(hipMemcpy(&h, err, 4, hipMemcpyDeviceToHost)); printf("deverr %u\n", h);
   return 0;
 }
