@@ -54,7 +54,7 @@ int main() {
     CK(hipMalloc(&start, 8 * 256 * 8));
     CK(hipMalloc(&counter, 256));
     CK(hipMalloc(&err, 64));
-    const size_t lb_bytes = (n / 2048 + 1) * 256 * 4;
+    const size_t lb_bytes = (n / 2048 + 1) * 256 * 4;  // >= ntiles * 256 granules for tiles >= 2048 keys
     CK(hipMalloc(&lb, lb_bytes));
     CK(hipMemset(err, 0, 64));
     CK(hipEventCreate(&e0));
@@ -80,8 +80,14 @@ int main() {
                            0, 0, kin, kout, (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, start,        \
                            (uint32_t*)lb, counter, err, X{});                                               \
     }, n)
-    PASS(512, 16, 4);
-    PASS(512, 16, 0);
+    for (int rep = 0; rep < 2; ++rep) {
+        PASS(512, 16, 4);
+        PASS(1024, 16, 4);
+        PASS(1024, 16, 8);
+        PASS(512, 24, 4);
+        PASS(768, 16, 4);
+        PASS(1024, 16, 0);
+    }
     uint32_t herr;
     CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
     printf("deverr %u\n", herr);
