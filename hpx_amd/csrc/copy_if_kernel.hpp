@@ -1,0 +1,145 @@
+// copy_if_kernel.hpp -- the single-pass stream compaction kernel (see
+// copy_if.hip for the algorithm notes).  Header so that scripts/ubench
+// instantiates exactly the shipped kernel with other tile shapes.
+#pragma once
+
+#include "common.hpp"
+#include "lookback.hpp"
+
+namespace hpxhip {
+namespace copy_if_detail {
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / kWave;
+
+template <typename T, int ROUNDS>
+constexpr uint64_t tile_elems() {
+    return static_cast<uint64_t>(kThreads) * ROUNDS * (16 / sizeof(T));
+}
+
+__device__ __forceinline__ uint32_t rank_below(uint64_t mask) {
+    // number of set bits of `mask` in lanes below this lane
+    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
+}
+
+// Hit bits of one lane: bit (r*V + e) for element e of round r.
+template <int BITS>
+using hit_word = std::conditional_t<(BITS <= 32), uint32_t, uint64_t>;
+
+// MINW: minimum waves per SIMD (8 = two 1024-thread workgroups per CU).
+template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4>
+__global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out, uint64_t n, Pred pred,
+                                                       uint64_t* count_dev, uint32_t* counter,
+                                                       tile_state<uint64_t> st, uint64_t ntiles) {
+    constexpr int V = 16 / sizeof(T);
+    constexpr uint64_t TILE = tile_elems<T, ROUNDS>();
+    constexpr uint64_t WAVE_ELEMS = TILE / kWaves;
+    using VT = vec<T, V>;
+    using H = hit_word<ROUNDS * V>;
+    static_assert(ROUNDS * V <= 64, "hit bits per lane");
+
+    __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_wave_total[kWaves];
+    __shared__ uint64_t s_prefix;
+    __shared__ T s_stage[kWaves][kWave * V];  // one wave round of hits, compacted
+
+    if (threadIdx.x == 0)
+        s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint64_t tile = s_tile;
+    const int wave = threadIdx.x / kWave;
+    const int lane = lane_id();
+    const uint64_t tile_base = tile * TILE;
+    const uint64_t wbase = tile_base + wave * WAVE_ELEMS;
+    const bool full = tile_base + TILE <= n;
+
+    VT x[ROUNDS];
+    H hit = 0;
+    if (ALIGNED && full) {
+        const VT* src = reinterpret_cast<const VT*>(in + wbase);
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) x[r] = ld_stream(&src[r * kWave + lane]);
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r)
+#pragma unroll
+            for (int e = 0; e < V; ++e) hit |= static_cast<H>(pred(x[r].v[e])) << (r * V + e);
+    } else {
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r)
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const uint64_t i = wbase + (static_cast<uint64_t>(r) * kWave + lane) * V + e;
+                const bool ok = i < n;
+                x[r].v[e] = ok ? in[i] : T(0);
+                hit |= static_cast<H>(ok && pred(x[r].v[e])) << (r * V + e);
+            }
+    }
+
+    // Hits of the wave's segment (segment order = round, lane, element): the
+    // per-element ranks are recomputed in the write-out from the hit bits,
+    // so no rank array is held across the look-back.
+    const uint32_t wave_count = wave_reduce(static_cast<uint32_t>(__builtin_popcountll(hit)), op_plus{});
+    if (lane == 0) s_wave_total[wave] = wave_count;
+    __syncthreads();
+    uint32_t wave_prefix = 0, agg = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        if (w < wave) wave_prefix += s_wave_total[w];
+        agg += s_wave_total[w];
+    }
+
+    if (wave == 0) {
+        uint64_t p = 0;
+        if (tile == 0) {
+            if (lane == 0) st.publish(0, static_cast<uint64_t>(agg), TILE_INCLUSIVE);
+        } else {
+            if (lane == 0) st.publish(tile, static_cast<uint64_t>(agg), TILE_AGGREGATE);
+            p = st.exclusive_prefix(tile, op_plus{});
+            if (lane == 0) st.publish(tile, p + agg, TILE_INCLUSIVE);
+        }
+        if (lane == 0) {
+            s_prefix = p;
+            if (tile == ntiles - 1) *count_dev = p + agg;
+        }
+    }
+    __syncthreads();
+    // Write-out: per wave round, the hits are compacted into LDS at their
+    // round-local rank and stored back by consecutive lanes, so each store
+    // instruction covers one contiguous run of the output (a direct
+    // out[base + rank] scatter leaves holes in every wave store).
+    const uint64_t base = s_prefix + wave_prefix;
+    T* stage = s_stage[wave];
+    uint32_t round_base = 0;
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        uint32_t cnt = 0, below = 0;
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            const uint64_t m = __ballot((hit >> (r * V + e)) & 1u);
+            below += rank_below(m);
+            cnt += static_cast<uint32_t>(__builtin_popcountll(m));
+        }
+        uint32_t lane_before = 0;
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+            if ((hit >> (r * V + e)) & 1u) stage[below + lane_before++] = x[r].v[e];
+        // LDS is in order within a wave; the wait + clobber keep the compiler
+        // from hoisting the reads above the writes of other lanes.
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const uint32_t j = k * kWave + lane;
+            if (j < cnt) out[base + round_base + j] = stage[j];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next round's writes
+        round_base += cnt;
+    }
+}
+
+__global__ void k_zero_count(uint64_t* c) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *c = 0;
+}
+
+}  // namespace copy_if_detail
+}  // namespace hpxhip

@@ -168,6 +168,30 @@ def test_reduce_fp_tolerance_and_determinism(pol, gpu_target, n, dt):
     assert P.reduce(pol, d.begin(), d.end(), 0.0, F.maximum) == a.max()
 
 
+def test_reduce_many_partials(pol, gpu_target):
+    """Past 16384 block partials the fold launch (k_reduce_partials) loops:
+    int64 at 2^28 + 3 (and a misaligned sub-range of it), int32 widened to
+    int64 at 2^29 + 5.  Inputs are iota ranges (lo + i), so the exact
+    results have closed forms and no multi-GiB host copy is needed."""
+    def iota_sum(lo, n):
+        return n * lo + n * (n - 1) // 2
+
+    n, lo = (1 << 28) + 3, -(1 << 27)
+    x = hpx.vector(n, dtype=np.int64, tgt=gpu_target)
+    P.generate(pol, x.begin(), x.end(), "iota", 0, lo)
+    assert x[0] == lo and x[n - 1] == lo + n - 1
+    assert P.reduce(pol, x.begin(), x.end(), 7, F.plus) == 7 + iota_sum(lo, n)
+    assert P.reduce(pol, x.begin() + 1, x.end(), 0, F.plus) == iota_sum(lo + 1, n - 1)
+    assert P.reduce(pol, x.begin(), x.end(), -(1 << 40), F.maximum) == lo + n - 1
+    assert P.reduce(pol, x.begin(), x.end(), 0, F.minimum) == lo
+    del x
+    n, lo = (1 << 29) + 5, -(1 << 28)
+    y = hpx.vector(n, dtype=np.int32, tgt=gpu_target)
+    P.generate(pol, y.begin(), y.end(), "iota", 0, lo)
+    got = P.transform_reduce(pol, y.begin(), y.end(), np.int64(3), F.plus, F.identity())
+    assert got == 3 + iota_sum(lo, n)
+
+
 def test_reduce_golden(pol, gpu_target):
     for case in golden_cases("reduce"):
         g = load_golden(case)
