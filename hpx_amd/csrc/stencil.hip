@@ -10,7 +10,12 @@
 // Kernel: each lane loads one 16-B vector (two points); the left/right
 // neighbours come from the adjacent lanes (ds_bpermute), the wave's edge
 // lanes read one extra point (or the halo at the partition ends).
-// Traffic: 16 B/point/step (read cur, write next).
+// Traffic: 16 B/point/step (read cur, write next).  Default cache policy:
+// the edge lanes' extra loads then hit the lines the adjacent wave just
+// fetched (nontemporal loads cost 12 %); nontemporal stores measured 1 %
+// faster in isolation but 4 % slower in the library probe, so they are not
+// used; 256-thread blocks beat 64-1024 (scripts/ubench/stencil.hip,
+// profiles/r01_ubench_stencil.log).
 #include "internal.hpp"
 
 using namespace hpxhip;
