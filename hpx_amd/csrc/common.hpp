@@ -203,6 +203,7 @@ enum : int {
     DPP_ROW_SHR3 = 0x113,
     DPP_ROW_SHR4 = 0x114,
     DPP_ROW_SHR8 = 0x118,
+    DPP_WAVE_SHL1 = 0x130,
     DPP_WAVE_SHR1 = 0x138,
     DPP_ROW_BCAST15 = 0x142,
     DPP_ROW_BCAST31 = 0x143,

@@ -64,6 +64,119 @@ __global__ __launch_bounds__(kThreads) void k_heat_scalar(const double* __restri
     next[i] = heat(l, cur[i], r, c);
 }
 
+// ------------------------------------------------------ temporal blocking
+// S fused steps per pass (S even, 2..8): each wave owns a window of WIN = 512
+// consecutive points held in registers as 4 rows x 64 lanes x 2 points (row
+// r, lane l -> window points 128r + 2l, +1; every load/store instruction is
+// one contiguous KiB), steps it S times with the neighbours taken from the
+// adjacent lanes by DPP wave shifts (row ends through readlane), and writes
+// the WIN - 2S points that are still exact (a point's value after S steps
+// depends on the S points each side).  Window w starts at out_lo + w*OUT - S,
+// OUT = WIN - 2S, so consecutive windows overlap by 2S points.
+// HBM traffic per pass: 8 B read x WIN/OUT + 8 B written per point, i.e.
+// 16.5 B per point for S steps at S = 8 instead of 16 B per point per step.
+// Every point sees exactly the single-step arithmetic (heat() above, same
+// association, -ffp-contract=off), so results are bit-identical to S single
+// steps.  Points outside [0, n) come from the halos: cur[-j] = lh[S - j],
+// cur[n + j] = rh[j] (j < S; for one periodic partition lh = cur + n - S,
+// rh = cur).
+constexpr int kFusedRows = 4;
+constexpr int kFusedWin = kFusedRows * 2 * kWave;  // 512 points
+
+template <int S>
+__global__ __launch_bounds__(kThreads) void k_heat_fused(const double* __restrict__ cur, double* __restrict__ next,
+                                                          uint64_t n, uint64_t out_lo, uint64_t out_hi,
+                                                          const double* __restrict__ lh,
+                                                          const double* __restrict__ rh, double c, bool aligned) {
+    static_assert(S >= 2 && S <= 8 && S % 2 == 0, "even fused step counts");
+    using V2 = vec<double, 2>;
+    constexpr uint64_t OUT = kFusedWin - 2 * S;
+    const uint64_t wave_g = (static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x) / kWave;
+    const uint64_t o0 = out_lo + wave_g * OUT;
+    if (o0 >= out_hi) return;  // wave-uniform
+    const uint64_t o1 = min(o0 + OUT, out_hi);
+    const int lane = lane_id();
+    const int64_t w0 = static_cast<int64_t>(o0) - S;  // window start (may be < 0)
+    const bool inside = aligned && w0 >= 0 && static_cast<uint64_t>(w0) + kFusedWin <= n;
+
+    V2 x[kFusedRows];
+    if (inside) {
+        const V2* src = reinterpret_cast<const V2*>(cur + w0);
+#pragma unroll
+        for (int r = 0; r < kFusedRows; ++r) x[r] = src[r * kWave + lane];
+    } else {
+#pragma unroll
+        for (int r = 0; r < kFusedRows; ++r)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int64_t i = w0 + r * 2 * kWave + 2 * lane + e;
+                double v = 0.0;  // beyond the halos: feeds only points that are not written
+                if (i < 0) {
+                    if (i >= -S) v = lh[S + i];
+                } else if (static_cast<uint64_t>(i) < n) {
+                    v = cur[i];
+                } else if (static_cast<uint64_t>(i) < n + S) {
+                    v = rh[static_cast<uint64_t>(i) - n];
+                }
+                x[r].v[e] = v;
+            }
+    }
+
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+        double L[kFusedRows], R[kFusedRows];
+#pragma unroll
+        for (int r = 0; r < kFusedRows; ++r) {
+            // left of point 0: lane-1's point 1; lane 0 takes lane 63's point 1 of row r-1
+            const double lfill = r > 0 ? readlane(x[r - 1].v[1], kWave - 1) : 0.0;
+            L[r] = dpp<DPP_WAVE_SHR1>(lfill, x[r].v[1]);
+            // right of point 1: lane+1's point 0; lane 63 takes lane 0's point 0 of row r+1
+            const double rfill = r + 1 < kFusedRows ? readlane(x[r + 1].v[0], 0) : 0.0;
+            R[r] = dpp<DPP_WAVE_SHL1>(rfill, x[r].v[0]);
+        }
+#pragma unroll
+        for (int r = 0; r < kFusedRows; ++r) {
+            const double m0 = x[r].v[0], m1 = x[r].v[1];
+            x[r].v[0] = heat(L[r], m0, m1, c);
+            x[r].v[1] = heat(m0, m1, R[r], c);
+        }
+    }
+
+#pragma unroll
+    for (int r = 0; r < kFusedRows; ++r) {
+        const int64_t i = w0 + r * 2 * kWave + 2 * lane;  // even when aligned
+        const bool ok0 = i >= static_cast<int64_t>(o0) && i < static_cast<int64_t>(o1);
+        const bool ok1 = i + 1 >= static_cast<int64_t>(o0) && i + 1 < static_cast<int64_t>(o1);
+        if (aligned && ok0 && ok1) {
+            reinterpret_cast<V2*>(next + i)[0] = x[r];
+        } else {
+            if (ok0) next[i] = x[r].v[0];
+            if (ok1) next[i + 1] = x[r].v[1];
+        }
+    }
+}
+
+int launch_fused(const double* cur, double* next, uint64_t n, uint64_t out_lo, uint64_t out_hi, const double* lh,
+                 const double* rh, int steps, double c, hipStream_t s) {
+    if (out_hi <= out_lo) return 0;
+    const uint64_t OUT = kFusedWin - 2 * steps;
+    const uint64_t waves = (out_hi - out_lo + OUT - 1) / OUT;
+    const uint64_t blocks = (waves * kWave + kThreads - 1) / kThreads;
+    // 16-B vector path: both buffers 16-B aligned and every window start even
+    const bool aligned = (reinterpret_cast<uintptr_t>(cur) % 16 == 0) && (reinterpret_cast<uintptr_t>(next) % 16 == 0) &&
+                         out_lo % 2 == 0;
+    const dim3 g(static_cast<unsigned>(blocks)), b(kThreads);
+    switch (steps) {
+        case 2: hipLaunchKernelGGL(k_heat_fused<2>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
+        case 4: hipLaunchKernelGGL(k_heat_fused<4>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
+        case 6: hipLaunchKernelGGL(k_heat_fused<6>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
+        case 8: hipLaunchKernelGGL(k_heat_fused<8>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
+        default: return HPXHIP_ERROR_INVALID_ARGUMENT;
+    }
+    HPXHIP_CHECK_LAUNCH();
+    return 0;
+}
+
 int launch_step(const double* cur, double* next, uint64_t n, const double* lh, const double* rh, double c,
                 hipStream_t s) {
     const bool aligned = (reinterpret_cast<uintptr_t>(cur) % 16 == 0) && (reinterpret_cast<uintptr_t>(next) % 16 == 0);
@@ -85,6 +198,60 @@ int launch_step(const double* cur, double* next, uint64_t n, const double* lh, c
     return 0;
 }
 
+// nt periodic steps ping-ponging u0/u1: passes of up to
+// HPXHIP_STENCIL_MAX_FUSED steps (even), a single step for an odd remainder;
+// tiny rings step one at a time.  match_parity: give every planned chunk a
+// pass count with the parity of its step count (an 8 becomes 6 + 2, or a 2
+// becomes 1 + 1), so the result lands in u0 for even nt and in u1 for odd nt
+// as hpxhip_stencil_heat_run promises; otherwise the fewest passes, and
+// *flips (one per pass) says where the result is.
+int run_passes(double* u0, double* u1, uint64_t n, uint64_t nt, double c, bool match_parity, hipStream_t s,
+               uint64_t* flips) {
+    const bool fuse = n >= 2 * static_cast<uint64_t>(kFusedWin);
+    uint64_t done = 0;
+    while (done < nt) {
+        uint64_t passes[64];
+        int np = 0;
+        const uint64_t cap = fuse ? 60 * HPXHIP_STENCIL_MAX_FUSED : 64;
+        const uint64_t chunk = nt - done < cap ? nt - done : cap;
+        uint64_t r = chunk;
+        while (fuse && r >= 2) {
+            const uint64_t st = r >= HPXHIP_STENCIL_MAX_FUSED ? HPXHIP_STENCIL_MAX_FUSED : (r & ~uint64_t(1));
+            passes[np++] = st;
+            r -= st;
+        }
+        while (r > 0) {
+            passes[np++] = 1;
+            --r;
+        }
+        if (match_parity && static_cast<uint64_t>(np) % 2 != chunk % 2) {  // then some pass is >= 2
+            int i = 0;
+            while (passes[i] < 4 && i + 1 < np) ++i;
+            const bool split_big = passes[i] >= 4;
+            if (!split_big) {
+                i = 0;
+                while (passes[i] != 2) ++i;
+            }
+            for (int j = np; j > i + 1; --j) passes[j] = passes[j - 1];
+            passes[i] -= split_big ? 2 : 1;
+            passes[i + 1] = split_big ? 2 : 1;
+            ++np;
+        }
+        for (int i = 0; i < np; ++i, ++*flips) {
+            const double* cur = (*flips % 2 == 0) ? u0 : u1;
+            double* nxt = (*flips % 2 == 0) ? u1 : u0;
+            const int st = static_cast<int>(passes[i]);
+            // periodic: left of point 0 is point n-1 (the last st points for
+            // a fused pass), right of point n-1 is point 0
+            const int rc = st == 1 ? launch_step(cur, nxt, n, cur + (n - 1), cur, c, s)
+                                   : launch_fused(cur, nxt, n, 0, n, cur + (n - st), cur, st, c, s);
+            if (rc) return rc;
+        }
+        done += chunk;
+    }
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -101,6 +268,26 @@ int hpxhip_stencil_heat_step(const double* cur, double* next, uint64_t n, const 
     return launch_step(cur, next, n, left_halo_dev, right_halo_dev, c, s);
 }
 
+int hpxhip_stencil_heat_steps(const double* cur, double* next, uint64_t n, uint64_t out_lo, uint64_t out_hi,
+                              const double* left_halo_dev, const double* right_halo_dev, int steps, double k,
+                              double dt, double dx, hpxhip_stream stream) {
+    if (out_hi > n || out_lo > out_hi) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    if (out_hi == out_lo) return 0;
+    if (!cur || !next || !left_halo_dev || !right_halo_dev || cur == next) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    if (steps < 1 || steps > HPXHIP_STENCIL_MAX_FUSED || (steps > 1 && steps % 2)) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    const double c = k * dt / (dx * dx);
+    if (steps == 1) {
+        // one step on [out_lo, out_hi): halos are the neighbouring points of cur or the halo arrays
+        const double* l = out_lo == 0 ? left_halo_dev : cur + out_lo - 1;
+        const double* r = out_hi == n ? right_halo_dev : cur + out_hi;
+        return launch_step(cur + out_lo, next + out_lo, out_hi - out_lo, l, r, c, s);
+    }
+    return launch_fused(cur, next, n, out_lo, out_hi, left_halo_dev, right_halo_dev, steps, c, s);
+}
+
 int hpxhip_stencil_heat_run(double* u0, double* u1, uint64_t n, uint64_t nt, double k, double dt, double dx,
                             hpxhip_stream stream) {
     if (n == 0 || nt == 0) return 0;
@@ -108,15 +295,23 @@ int hpxhip_stencil_heat_run(double* u0, double* u1, uint64_t n, uint64_t nt, dou
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     device_guard g(s);
     if (g.status) return g.status;
-    const double c = k * dt / (dx * dx);
-    for (uint64_t t = 0; t < nt; ++t) {
-        const double* cur = (t % 2 == 0) ? u0 : u1;
-        double* nxt = (t % 2 == 0) ? u1 : u0;
-        // periodic: left of point 0 is point n-1, right of point n-1 is point 0
-        int rc = launch_step(cur, nxt, n, cur + (n - 1), cur, c, s);
-        if (rc) return rc;
-    }
-    return 0;
+    uint64_t flips = 0;
+    return run_passes(u0, u1, n, nt, k * dt / (dx * dx), true, s, &flips);
+}
+
+int hpxhip_stencil_heat_run_fused(double* u0, double* u1, uint64_t n, uint64_t nt, double k, double dt, double dx,
+                                  int* result_in_u1, hpxhip_stream stream) {
+    if (!result_in_u1) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    *result_in_u1 = 0;
+    if (n == 0 || nt == 0) return 0;
+    if (!u0 || !u1 || u0 == u1) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    uint64_t flips = 0;
+    const int rc = run_passes(u0, u1, n, nt, k * dt / (dx * dx), false, s, &flips);
+    *result_in_u1 = static_cast<int>(flips % 2);
+    return rc;
 }
 
 }  // extern "C"

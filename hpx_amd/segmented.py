@@ -49,6 +49,9 @@ def partition_bounds(n: int, parts: int, k: int):
 
 
 # ----------------------------------------------------------------- comms
+HALO_MAX = L.STENCIL_MAX_FUSED  # widest 1d_stencil halo (points per side)
+
+
 class LocalComm:
     """World of one rank (no collectives)."""
     rank = 0
@@ -73,16 +76,19 @@ class LocalComm:
     def barrier(self):
         pass
 
-    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream):
-        # ring of one: left neighbour's last point is my last, right's first is my first
-        L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_left), ctypes.c_void_p(send_right), 8, L.D2D, stream)
-        L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_right), ctypes.c_void_p(send_left), 8, L.D2D, stream)
+    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream, count=1):
+        # ring of one: the left neighbour's last points are my last, the right's first are my first
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_left), ctypes.c_void_p(send_right), 8 * count, L.D2D,
+               stream)
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_right), ctypes.c_void_p(send_left), 8 * count, L.D2D,
+               stream)
 
 
 def ring_halo_ops(dist, rank, size, first, last, left_halo, right_halo):
-    """P2P ops of one periodic halo step (1d_stencil_4_parallel.cpp:147-150):
-    my last point becomes the right neighbour's left halo, my first point the
-    left neighbour's right halo.  Point-to-point messages between one pair of
+    """P2P ops of one periodic halo exchange (1d_stencil_4_parallel.cpp:147-150,
+    one point wide there, one fused pass's width here): my last points become
+    the right neighbour's left halo, my first points the left neighbour's
+    right halo.  Point-to-point messages between one pair of
     ranks match in posting order, and with two ranks the left and right
     neighbour are the same rank, so the order is fixed: send last (to the
     right) before first (to the left), receive from the left before the
@@ -111,7 +117,7 @@ class TorchComm:
         self.device = torch.device("cuda", tgt.device)
         self._send = torch.zeros(8, dtype=torch.int64, device=self.device)
         self._recv = torch.zeros(8 * self.size, dtype=torch.int64, device=self.device)
-        self._halo = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self._halo = torch.zeros(4 * HALO_MAX, dtype=torch.float64, device=self.device)
 
     def _stream(self, stream):
         return self.torch.cuda.ExternalStream(stream.value if hasattr(stream, "value") else int(stream),
@@ -159,22 +165,24 @@ class TorchComm:
         with self.torch.cuda.stream(self._stream(stream)):
             self.dist.all_to_all_single(dst, src, rb, sb)
 
-    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream):
-        """Ring halo: my first point goes to the left neighbour (its right
-        halo), my last point to the right neighbour (its left halo)."""
+    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream, count=1):
+        """Ring halo of `count` points: my first points go to the left
+        neighbour (its right halo), my last points to the right neighbour
+        (its left halo)."""
         torch, dist = self.torch, self.dist
-        left, right = (self.rank - 1) % self.size, (self.rank + 1) % self.size
+        c, M, nb = int(count), HALO_MAX, 8 * int(count)
         with torch.cuda.stream(self._stream(stream)):
             h = self._halo
-            L.call("hpxhip_memcpy_async", ctypes.c_void_p(h.data_ptr()), ctypes.c_void_p(send_left), 8, L.D2D, stream)
-            L.call("hpxhip_memcpy_async", ctypes.c_void_p(h.data_ptr() + 8), ctypes.c_void_p(send_right), 8, L.D2D,
+            base = h.data_ptr()
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(base), ctypes.c_void_p(send_left), nb, L.D2D, stream)
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(base + 8 * M), ctypes.c_void_p(send_right), nb, L.D2D,
                    stream)
-            for w in dist.batch_isend_irecv(ring_halo_ops(dist, self.rank, self.size, h[0:1], h[1:2], h[2:3],
-                                                           h[3:4])):
+            for w in dist.batch_isend_irecv(ring_halo_ops(dist, self.rank, self.size, h[0:c], h[M:M + c],
+                                                           h[2 * M:2 * M + c], h[3 * M:3 * M + c])):
                 w.wait()
-            L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_left), ctypes.c_void_p(h.data_ptr() + 16), 8, L.D2D,
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_left), ctypes.c_void_p(base + 16 * M), nb, L.D2D,
                    stream)
-            L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_right), ctypes.c_void_p(h.data_ptr() + 24), 8, L.D2D,
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_right), ctypes.c_void_p(base + 24 * M), nb, L.D2D,
                    stream)
 
 
@@ -264,7 +272,7 @@ class HipEngine:
         return [u0, vector(max(1, n), dtype=np.float64, tgt=self.tgt)]
 
     def halo_buffer(self):
-        return vector(4, dtype=np.float64, value=0.0, tgt=self.tgt)
+        return vector(4 * HALO_MAX, dtype=np.float64, value=0.0, tgt=self.tgt)
 
     def read_values(self, buf, n):
         out = np.empty(n, np.float64)
@@ -289,6 +297,14 @@ class HipEngine:
             L.call("hpxhip_stencil_heat_step", ctypes.c_void_p(cur.data() + 8 * c_off),
                    ctypes.c_void_p(nxt.data() + 8 * n_off), n, ctypes.c_void_p(left), ctypes.c_void_p(right),
                    ctypes.c_double(k), ctypes.c_double(dt), ctypes.c_double(dx), stream)
+
+    def heat_steps(self, cur, nxt, n, lo, hi, left, right, steps, k, dt, dx, stream):
+        """`steps` fused steps, next[lo, hi) from cur[0, n) and `steps`-point
+        halos (hpxhip_stencil_heat_steps)."""
+        if hi > lo:
+            L.call("hpxhip_stencil_heat_steps", ctypes.c_void_p(cur.data()), ctypes.c_void_p(nxt.data()), n, lo, hi,
+                   ctypes.c_void_p(left), ctypes.c_void_p(right), int(steps), ctypes.c_double(k),
+                   ctypes.c_double(dt), ctypes.c_double(dx), stream)
 
     def side_stream(self):
         s = getattr(self, "_side", None)
@@ -666,62 +682,84 @@ class heat_solver:
     each partition needs its neighbours' boundary points, periodic ring
     1d_stencil_4_parallel.cpp:147-150; U0[i] = global i, 1d_stencil_4.cpp:64-66).
 
-    Step t on partition [lo, hi) of n >= 4 points, with cur = U[t%2]:
-      main stream: edge points 0,1 and n-2,n-1 of next (they read the halos
-                   received for cur), event E_edges;
-      side stream: waits E_edges, sends next[0] left and next[n-1] right,
+    Temporal blocking: a pass advances s <= W steps at once
+    (hpxhip_stencil_heat_steps; W = min(HALO_MAX, smallest partition)), so
+    the halo is W points per side, exchanged once per pass instead of one
+    point per step.  Pass on partition [lo, hi) of n points, cur = current:
+      main stream: the edge ranges [0, W) and [n-W, n) of next (they read the
+                   halos received for cur), event E_edges;
+      side stream: waits E_edges, sends next[0:W] left and next[n-W:n] right,
                    receives the neighbours' points into the other halo slot
-                   (RCCL send/recv of 8 B each way), event E_halo;
-      main stream: the interior [2, n-2) of next, concurrent with the
-                   exchange; step t+1 waits E_halo before its edges.
-    The halo latency (~10-30 us for RCCL) hides behind the interior kernel
-    (1.4 ms at 2^29 points per GPU).  n < 4: one full step per partition."""
+                   (RCCL send/recv of 8W B each way), event E_halo;
+      main stream: the interior [W, n-W) of next, concurrent with the
+                   exchange; the next pass waits E_halo before its edges.
+    n < 2W: one whole-partition launch per pass, then the exchange.  Halo
+    slot layout (points): [slot][left block of HALO_MAX | right block of
+    HALO_MAX]; the left neighbour's last W points end the left block, the
+    right neighbour's first W points start the right block."""
 
-    def __init__(self, nx, comm, tgt=None, k=0.5, dt=1.0, dx=1.0, engine=None, init=None):
+    def __init__(self, nx, comm, tgt=None, k=0.5, dt=1.0, dx=1.0, engine=None, init=None, fuse=None):
         self.comm = comm
         self.tgt = tgt
         self.eng = engine or HipEngine(tgt)
         self.nx = int(nx)
         self.lo, self.hi = partition_bounds(self.nx, comm.size, comm.rank)
         self.n = self.hi - self.lo
-        if partition_bounds(self.nx, comm.size, comm.size - 1)[1] - partition_bounds(self.nx, comm.size,
-                                                                                      comm.size - 1)[0] <= 0:
+        sizes = [b - a for a, b in (partition_bounds(self.nx, comm.size, r) for r in range(comm.size))]
+        if min(sizes) <= 0:
             raise ValueError(f"1d_stencil: {self.nx} points leave an empty partition on {comm.size} ranks")
+        # halo width = steps per pass (1 or even); every rank derives the same W
+        w = min(HALO_MAX if fuse is None else int(fuse), min(sizes))
+        self.W = w if w <= 1 else w - (w % 2)
         self.k, self.dt, self.dx = k, dt, dx
         self.U = self.eng.heat_buffers(self.n, self.lo, None if init is None else init[self.lo:self.hi])
-        self.H = self.eng.halo_buffer()   # [left, right] x 2 slots
+        self.H = self.eng.halo_buffer()   # 2 slots x [left block | right block], HALO_MAX points each
         self.t = 0
+        self._cur = 0    # buffer holding step t
+        self._slot = 0   # halo slot holding cur's halos
         self._halo_ev = None
         self._exchange(self.U[0], 0, self.eng.stream)   # halos of U0 into slot 0
 
+    def _halo_at(self, slot, side, width):
+        """Device location of the `width` halo points of slot/side (left:
+        the last `width` of the left block; right: the first of the right)."""
+        base = slot * 2 * HALO_MAX
+        return self.eng.loc(self.H, base + HALO_MAX - width if side == 0 else base + HALO_MAX)
+
     def _exchange(self, buf, slot, after_stream):
-        eng, side = self.eng, self.eng.side_stream()
+        eng, side, W = self.eng, self.eng.side_stream(), self.W
         eng.wait(side, eng.record(after_stream))
-        self.comm.halo_exchange(eng.loc(buf, 0), eng.loc(buf, self.n - 1), eng.loc(self.H, 2 * slot),
-                                eng.loc(self.H, 2 * slot + 1), side)
+        self.comm.halo_exchange(eng.loc(buf, 0), eng.loc(buf, self.n - W), self._halo_at(slot, 0, W),
+                                self._halo_at(slot, 1, W), side, count=W)
         self._halo_ev = eng.record(side)
 
     @property
     def current(self):
-        return self.U[self.t % 2]
+        return self.U[self._cur]
 
     def do_work(self, nt):
-        eng, n, S = self.eng, self.n, self.eng.stream
+        eng, n, S, W = self.eng, self.n, self.eng.stream, self.W
         k, dt, dx = self.k, self.dt, self.dx
-        for _ in range(nt):
-            cur, nxt = self.U[self.t % 2], self.U[(self.t + 1) % 2]
-            slot = self.t % 2
-            left, right = eng.loc(self.H, 2 * slot), eng.loc(self.H, 2 * slot + 1)
+        left_steps = int(nt)
+        while left_steps > 0:
+            s = min(W, left_steps)
+            if s > 1 and s % 2:
+                s -= 1
+            cur, nxt = self.U[self._cur], self.U[1 - self._cur]
+            slot = self._slot
+            lh, rh = self._halo_at(slot, 0, s), self._halo_at(slot, 1, s)
             eng.wait(S, self._halo_ev)
-            if n >= 4:
-                eng.heat_step(cur, 0, nxt, 0, 2, left, eng.loc(cur, 2), k, dt, dx, S)
-                eng.heat_step(cur, n - 2, nxt, n - 2, 2, eng.loc(cur, n - 3), right, k, dt, dx, S)
+            if n >= 2 * W:
+                eng.heat_steps(cur, nxt, n, 0, W, lh, rh, s, k, dt, dx, S)
+                eng.heat_steps(cur, nxt, n, n - W, n, lh, rh, s, k, dt, dx, S)
                 self._exchange(nxt, 1 - slot, S)
-                eng.heat_step(cur, 2, nxt, 2, n - 4, eng.loc(cur, 1), eng.loc(cur, n - 2), k, dt, dx, S)
+                eng.heat_steps(cur, nxt, n, W, n - W, lh, rh, s, k, dt, dx, S)
             else:
-                eng.heat_step(cur, 0, nxt, 0, n, left, right, k, dt, dx, S)
+                eng.heat_steps(cur, nxt, n, 0, n, lh, rh, s, k, dt, dx, S)
                 self._exchange(nxt, 1 - slot, S)
-            self.t += 1
+            self._cur, self._slot = 1 - self._cur, 1 - slot
+            self.t += s
+            left_steps -= s
         return self.current
 
     def synchronize(self):
@@ -765,7 +803,7 @@ class heat_solver:
         self.k, self.dt, self.dx = k, dt, dx
         self.t = int(t)
         self.eng.write_values(self.current, vals)
-        self._exchange(self.current, self.t % 2, self.eng.stream)
+        self._exchange(self.current, self._slot, self.eng.stream)
         return self.t
 
 

@@ -311,10 +311,28 @@ int hpxhip_sorted_bounds(int dtype, const void* sorted, uint64_t n, const void* 
 int hpxhip_stencil_heat_step(const double* cur, double* next, uint64_t n,
                              const double* left_halo_dev, const double* right_halo_dev,
                              double k, double dt, double dx, hpxhip_stream stream);
+/* Temporal blocking: `steps` heat steps in one pass over HBM (steps = 1 or
+   an even number up to HPXHIP_STENCIL_MAX_FUSED), writing next[out_lo,
+   out_hi) from cur[0, n).  Points left of cur[0] are left_halo_dev[0..steps)
+   (left_halo_dev[steps-1] = cur[-1]), points right of cur[n-1] are
+   right_halo_dev[0..steps) (right_halo_dev[0] = cur[n]); device pointers.
+   Bit-identical to `steps` calls of hpxhip_stencil_heat_step.  Replaces the
+   per-step partition update of 1d_stencil_8.cpp:482-531 (the halo becomes
+   `steps` points wide, exchanged once per pass). */
+#define HPXHIP_STENCIL_MAX_FUSED 8
+int hpxhip_stencil_heat_steps(const double* cur, double* next, uint64_t n, uint64_t out_lo, uint64_t out_hi,
+                              const double* left_halo_dev, const double* right_halo_dev, int steps, double k,
+                              double dt, double dx, hpxhip_stream stream);
 /* nt periodic steps on one partition, ping-ponging u0/u1; the result is in
-   u0 if nt is even, else in u1 (1d_stencil_1.cpp:58-70). */
+   u0 if nt is even, else in u1 (1d_stencil_1.cpp:58-70).  Runs fused passes
+   of up to HPXHIP_STENCIL_MAX_FUSED steps for rings of >= 1024 points. */
 int hpxhip_stencil_heat_run(double* u0, double* u1, uint64_t n, uint64_t nt, double k,
                             double dt, double dx, hpxhip_stream stream);
+/* As hpxhip_stencil_heat_run with the fewest passes (nt = 8q + r -> q passes
+   of 8, then r's); *result_in_u1 (set on return, host memory) tells which
+   buffer holds the result. */
+int hpxhip_stencil_heat_run_fused(double* u0, double* u1, uint64_t n, uint64_t nt, double k, double dt,
+                                  double dx, int* result_in_u1, hpxhip_stream stream);
 
 #ifdef __cplusplus
 }

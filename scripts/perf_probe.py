@@ -34,6 +34,8 @@ timeit("reduce f64", lambda: lib.hpxhip_transform_reduce(L.F64, L.F64, L.PLUS, L
 timeit("incl scan f64", lambda: lib.hpxhip_scan(L.F64, L.PLUS, 1, L.U_IDENTITY, None, f0, None, x, y, N, st, None, 0), 16*N)
 cur = alloc(8*N); L.check(lib.hpxhip_generate(L.F64, L.GEN_IOTA, 0, 0, 0, cur, N, st))
 timeit("stencil step f64", lambda: lib.hpxhip_stencil_heat_step(cur, a, N, cur, cur, 0.5, 1.0, 1.0, st), 16*N)
+# temporal blocking: 8 steps in one pass (16.5 B/point of HBM traffic); GB/s column = 16 B/point/step model
+timeit("stencil 8 fused steps f64", lambda: lib.hpxhip_stencil_heat_steps(cur, a, N, 0, N, cur, cur, 8, 0.5, 1.0, 1.0, st), 8*16*N)
 keys = a
 def srt():
     L.check(lib.hpxhip_generate(L.U64, L.GEN_BITS, 7, 0, 0, keys, N, st))

@@ -63,14 +63,15 @@ class HostStagedComm:
         if dst.numel():
             self._h2d(recv_buf.data(), dst.numpy())
 
-    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream):
+    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream, count=1):
         from hpx_amd import _lib as L
+        nb = 8 * int(count)
         L.call("hpxhip_stream_synchronize", stream)
-        mine = np.concatenate([self._d2h(send_left, 8), self._d2h(send_right, 8)])
+        mine = np.concatenate([self._d2h(send_left, nb), self._d2h(send_right, nb)])
         got = self._allgather_bytes(mine)
         left, right = (self.rank - 1) % self.size, (self.rank + 1) % self.size
-        self._h2d(recv_left, got[left][8:16].copy())
-        self._h2d(recv_right, got[right][0:8].copy())
+        self._h2d(recv_left, got[left][nb:2 * nb].copy())
+        self._h2d(recv_right, got[right][0:nb].copy())
 
     def barrier(self):
         self.dist.barrier()

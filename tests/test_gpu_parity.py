@@ -426,5 +426,54 @@ def test_stencil_golden_and_random(gpu_target):
         np.testing.assert_array_equal(stencil.heat_run(u, nt, tgt=gpu_target), O.stencil_heat(u, nt))
 
 
+@pytest.mark.parametrize("nx", [1024, 4097, 100003])
+def test_stencil_fused_run_bit_exact(gpu_target, nx):
+    """hpxhip_stencil_heat_run with temporal blocking (passes of up to 8
+    steps, the pass count matched to nt's parity so the result lands in the
+    documented buffer) against the serial oracle, bit for bit."""
+    from hpx_amd import stencil
+    u = rnd(np.float64, nx, 31 + nx)
+    for nt in [1, 2, 3, 4, 5, 7, 8, 9, 10, 16, 17, 26]:
+        np.testing.assert_array_equal(stencil.heat_run(u, nt, tgt=gpu_target), O.stencil_heat(u, nt), err_msg=f"nt={nt}")
+    # hpxhip_stencil_heat_run keeps its buffer contract (u0 for even nt, u1 for odd)
+    import ctypes
+    from hpx_amd import _lib as L
+    for nt in [8, 9, 10]:
+        a, b = dev(u, gpu_target), hpx.vector(nx, dtype=np.float64, tgt=gpu_target)
+        L.call("hpxhip_stencil_heat_run", ctypes.c_void_p(a.data()), ctypes.c_void_p(b.data()), nx, nt,
+               ctypes.c_double(0.5), ctypes.c_double(1.0), ctypes.c_double(1.0), gpu_target.stream)
+        res = a if nt % 2 == 0 else b
+        np.testing.assert_array_equal(res.to_host(), O.stencil_heat(u, nt), err_msg=f"heat_run nt={nt}")
+
+
+@pytest.mark.parametrize("steps", [1, 2, 4, 6, 8])
+def test_stencil_heat_steps_halos_subranges(gpu_target, steps):
+    """hpxhip_stencil_heat_steps: explicit `steps`-point halos, output
+    sub-ranges (even and odd starts), misaligned buffers; expected = `steps`
+    single steps of the oracle on [halo | cur | halo], whose inner n points
+    are exact."""
+    import ctypes
+    from hpx_amd import _lib as L
+    rng = np.random.default_rng(40 + steps)
+    for n, off in [(5000, 0), (4099, 1), (700, 0)]:
+        cur = rng.standard_normal(n)
+        lh, rh = rng.standard_normal(steps), rng.standard_normal(steps)
+        ext = np.concatenate([lh, cur, rh])
+        for _ in range(steps):
+            ext = O.stencil_heat_step(ext, 0.0, 0.0)
+        exp = ext[steps:steps + n]
+        dcur = hpx.vector.from_host(np.concatenate([np.zeros(off), cur]), gpu_target)
+        dlh, drh = hpx.vector.from_host(lh, gpu_target), hpx.vector.from_host(rh, gpu_target)
+        for lo, hi in [(0, n), (1, n - 3), (n // 3, n // 3 + 1), (n - 1, n)]:
+            dnext = hpx.vector(n + off, dtype=np.float64, value=-7.0, tgt=gpu_target)
+            L.call("hpxhip_stencil_heat_steps", ctypes.c_void_p(dcur.data() + 8 * off),
+                   ctypes.c_void_p(dnext.data() + 8 * off), n, lo, hi, ctypes.c_void_p(dlh.data()),
+                   ctypes.c_void_p(drh.data()), steps, ctypes.c_double(0.5), ctypes.c_double(1.0),
+                   ctypes.c_double(1.0), gpu_target.stream)
+            got = dnext.to_host()[off:]
+            np.testing.assert_array_equal(got[lo:hi], exp[lo:hi], err_msg=f"n={n} off={off} [{lo},{hi})")
+            assert np.all(got[:lo] == -7.0) and np.all(got[hi:] == -7.0)
+
+
 def test_device_error_word_clear(gpu_target):
     hpx.compute.device_error_check(gpu_target.device)

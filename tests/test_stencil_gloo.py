@@ -3,7 +3,7 @@ ranks): the halo ring, the double-buffered halo slots and the edge /
 exchange / interior ordering of hpx_amd.segmented.heat_solver, against the
 serial oracle (1d_stencil_1.cpp:41-72).  Per-partition kernels are replaced
 by the oracle's one-step restatement *in this test only*; the product engine
-(HipEngine + hpxhip_stencil_heat_step) is exercised on the GPU by
+(HipEngine + hpxhip_stencil_heat_steps) is exercised on the GPU by
 tests/test_gpu_parity.py and tests/test_gpu_merge_sort.py."""
 import os
 import socket
@@ -24,20 +24,22 @@ class RingComm:
     def __init__(self):
         self.rank, self.size = dist.get_rank(), dist.get_world_size()
 
-    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream):
+    def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream, count=1):
         """The product's P2P message order (segmented.ring_halo_ops, used by
-        TorchComm over RCCL) on gloo point-to-point."""
+        TorchComm over RCCL) on gloo point-to-point, `count` points a side."""
+        c = int(count)
         (a0, i0), (a1, i1) = send_left, send_right
-        h = torch.tensor([a0[i0], a1[i1], 0.0, 0.0], dtype=torch.float64)
+        first = torch.tensor(a0[i0:i0 + c], dtype=torch.float64)
+        last = torch.tensor(a1[i1:i1 + c], dtype=torch.float64)
+        lh, rh = torch.zeros(c, dtype=torch.float64), torch.zeros(c, dtype=torch.float64)
         if self.size == 1:
-            h[2], h[3] = h[1], h[0]
+            lh, rh = last.clone(), first.clone()
         else:
-            for w in dist.batch_isend_irecv(S.ring_halo_ops(dist, self.rank, self.size, h[0:1], h[1:2], h[2:3],
-                                                            h[3:4])):
+            for w in dist.batch_isend_irecv(S.ring_halo_ops(dist, self.rank, self.size, first, last, lh, rh)):
                 w.wait()
         (b0, j0), (b1, j1) = recv_left, recv_right
-        b0[j0] = float(h[2])    # left neighbour's last point
-        b1[j1] = float(h[3])    # right neighbour's first point
+        b0[j0:j0 + c] = lh.numpy()    # left neighbour's last points
+        b1[j1:j1 + c] = rh.numpy()    # right neighbour's first points
 
 
 class HeatEngine:
@@ -48,15 +50,19 @@ class HeatEngine:
         return [u0, np.zeros(n)]
 
     def halo_buffer(self):
-        return np.zeros(4)
+        return np.zeros(4 * S.HALO_MAX)
 
     def loc(self, buf, idx):
         return (buf, int(idx))
 
-    def heat_step(self, cur, c_off, nxt, n_off, n, left, right, k, dt, dx, stream):
-        lv = left[0][left[1]]
-        rv = right[0][right[1]]
-        nxt[n_off:n_off + n] = O.stencil_heat_step(cur[c_off:c_off + n], lv, rv, k, dt, dx)
+    def heat_steps(self, cur, nxt, n, lo, hi, left, right, steps, k, dt, dx, stream):
+        """`steps` oracle single steps on [left halo | cur | right halo]; its
+        inner points [steps + lo, steps + hi) are exact."""
+        (lb, li), (rb, ri) = left, right
+        ext = np.concatenate([lb[li:li + steps], cur[:n], rb[ri:ri + steps]])
+        for _ in range(steps):
+            ext = O.stencil_heat_step(ext, 0.0, 0.0, k, dt, dx)
+        nxt[lo:hi] = ext[steps + lo:steps + hi]
 
     def read_values(self, buf, n):
         return buf[:n].copy()
@@ -77,7 +83,10 @@ class HeatEngine:
         pass
 
 
-CASES = [(1001, 25, "ramp"), (1001, 25, "random"), (9, 7, "random"), (64, 40, "random")]
+# (nx, nt, initial state, halo width cap: None = HALO_MAX fused steps per pass,
+# 1 = one step per exchange as in 1d_stencil_8, 4 = four)
+CASES = [(1001, 25, "ramp", None), (1001, 25, "random", None), (9, 7, "random", None), (64, 40, "random", None),
+         (1001, 11, "random", 1), (1001, 13, "random", 4), (37, 9, "random", None)]
 
 
 def _worker(rank, size, port, q, ckdir):
@@ -86,15 +95,15 @@ def _worker(rank, size, port, q, ckdir):
     try:
         comm = RingComm()
         res = {}
-        for nx, nt, kind in CASES:
+        for nx, nt, kind, fuse in CASES:
             init = None if kind == "ramp" else np.random.default_rng(nx).standard_normal(nx)
             try:
-                hs = S.heat_solver(nx, comm, engine=HeatEngine(), init=init)
+                hs = S.heat_solver(nx, comm, engine=HeatEngine(), init=init, fuse=fuse)
             except ValueError:
-                res[(nx, nt, kind)] = None   # empty partition: rejected on every rank
+                res[(nx, nt, kind, fuse)] = None   # empty partition: rejected on every rank
                 continue
             out = hs.do_work(nt)
-            res[(nx, nt, kind)] = (hs.lo, out.copy())
+            res[(nx, nt, kind, fuse)] = (hs.lo, out.copy())
         # checkpoint after 7 steps, restart in a fresh solver, 9 more steps
         nx = 1001
         init = np.random.default_rng(5).standard_normal(nx)
@@ -134,17 +143,18 @@ def test_heat_solver_ring_gloo(size, tmp_path):
         p.join(timeout=60)
     for r in range(size):
         assert not isinstance(results[r], Exception), results[r]
-    for nx, nt, kind in CASES:
+    for case in CASES:
+        nx, nt, kind, fuse = case
         u0 = np.arange(nx, dtype=np.float64) if kind == "ramp" else np.random.default_rng(nx).standard_normal(nx)
         exp = O.stencil_heat(u0, nt)
-        if results[0][(nx, nt, kind)] is None:
+        if results[0][case] is None:
             assert -(-nx // size) * (size - 1) >= nx
             continue
         got = np.zeros(nx)
         for r in range(size):
-            lo, loc = results[r][(nx, nt, kind)]
+            lo, loc = results[r][case]
             got[lo:lo + loc.size] = loc
-        np.testing.assert_array_equal(got, exp, err_msg=f"nx={nx} nt={nt} {kind} ranks={size}")
+        np.testing.assert_array_equal(got, exp, err_msg=f"nx={nx} nt={nt} {kind} fuse={fuse} ranks={size}")
     # restart from the step-7 checkpoint == an uninterrupted 16-step run
     exp = O.stencil_heat(np.random.default_rng(5).standard_normal(1001), 16)
     got = np.zeros(1001)
