@@ -66,22 +66,25 @@ __global__ __launch_bounds__(kThreads) void k_heat_scalar(const double* __restri
 
 // ------------------------------------------------------ temporal blocking
 // S fused steps per pass (S even, 2..8): each wave owns a window of WIN = 512
-// consecutive points held in registers as 4 rows x 64 lanes x 2 points (row
-// r, lane l -> window points 128r + 2l, +1; every load/store instruction is
-// one contiguous KiB), steps it S times with the neighbours taken from the
+// consecutive points held in registers as ROWS rows x 64 lanes x P points
+// (row r, lane l -> window points r*64P + l*P .. +P-1; loads and stores are
+// 16-B vectors), steps it S times with the neighbours taken from the
 // adjacent lanes by DPP wave shifts (row ends through readlane), and writes
 // the WIN - 2S points that are still exact (a point's value after S steps
 // depends on the S points each side).  Window w starts at out_lo + w*OUT - S,
-// OUT = WIN - 2S, so consecutive windows overlap by 2S points.
+// OUT = WIN - 2S, so consecutive windows overlap by 2S points.  P = 4 halves
+// the cross-lane moves per point of P = 2 (the pass is FP64-VALU bound at
+// S = 8).
 // HBM traffic per pass: 8 B read x WIN/OUT + 8 B written per point, i.e.
-// 16.5 B per point for S steps at S = 8 instead of 16 B per point per step.
+// 16.26 B per point for S = 8 steps instead of 16 B per point per step.
 // Every point sees exactly the single-step arithmetic (heat() above, same
 // association, -ffp-contract=off), so results are bit-identical to S single
 // steps.  Points outside [0, n) come from the halos: cur[-j] = lh[S - j],
 // cur[n + j] = rh[j] (j < S; for one periodic partition lh = cur + n - S,
 // rh = cur).
-constexpr int kFusedRows = 4;
-constexpr int kFusedWin = kFusedRows * 2 * kWave;  // 512 points
+constexpr int kFusedPts = 4;                                // points per lane per row
+constexpr int kFusedRows = 2;
+constexpr int kFusedWin = kFusedRows * kFusedPts * kWave;  // 512 points
 
 template <int S>
 __global__ __launch_bounds__(kThreads) void k_heat_fused(const double* __restrict__ cur, double* __restrict__ next,
@@ -89,6 +92,8 @@ __global__ __launch_bounds__(kThreads) void k_heat_fused(const double* __restric
                                                           const double* __restrict__ lh,
                                                           const double* __restrict__ rh, double c, bool aligned) {
     static_assert(S >= 2 && S <= 8 && S % 2 == 0, "even fused step counts");
+    constexpr int P = kFusedPts;
+    constexpr int ROW = P * kWave;
     using V2 = vec<double, 2>;
     constexpr uint64_t OUT = kFusedWin - 2 * S;
     const uint64_t wave_g = (static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x) / kWave;
@@ -99,17 +104,22 @@ __global__ __launch_bounds__(kThreads) void k_heat_fused(const double* __restric
     const int64_t w0 = static_cast<int64_t>(o0) - S;  // window start (may be < 0)
     const bool inside = aligned && w0 >= 0 && static_cast<uint64_t>(w0) + kFusedWin <= n;
 
-    V2 x[kFusedRows];
+    double x[kFusedRows][P];
     if (inside) {
-        const V2* src = reinterpret_cast<const V2*>(cur + w0);
 #pragma unroll
-        for (int r = 0; r < kFusedRows; ++r) x[r] = src[r * kWave + lane];
+        for (int r = 0; r < kFusedRows; ++r)
+#pragma unroll
+            for (int h = 0; h < P / 2; ++h) {
+                const V2 v = *reinterpret_cast<const V2*>(cur + w0 + r * ROW + lane * P + 2 * h);
+                x[r][2 * h] = v.v[0];
+                x[r][2 * h + 1] = v.v[1];
+            }
     } else {
 #pragma unroll
         for (int r = 0; r < kFusedRows; ++r)
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int64_t i = w0 + r * 2 * kWave + 2 * lane + e;
+            for (int e = 0; e < P; ++e) {
+                const int64_t i = w0 + r * ROW + lane * P + e;
                 double v = 0.0;  // beyond the halos: feeds only points that are not written
                 if (i < 0) {
                     if (i >= -S) v = lh[S + i];
@@ -118,7 +128,7 @@ __global__ __launch_bounds__(kThreads) void k_heat_fused(const double* __restric
                 } else if (static_cast<uint64_t>(i) < n + S) {
                     v = rh[static_cast<uint64_t>(i) - n];
                 }
-                x[r].v[e] = v;
+                x[r][e] = v;
             }
     }
 
@@ -127,33 +137,43 @@ __global__ __launch_bounds__(kThreads) void k_heat_fused(const double* __restric
         double L[kFusedRows], R[kFusedRows];
 #pragma unroll
         for (int r = 0; r < kFusedRows; ++r) {
-            // left of point 0: lane-1's point 1; lane 0 takes lane 63's point 1 of row r-1
-            const double lfill = r > 0 ? readlane(x[r - 1].v[1], kWave - 1) : 0.0;
-            L[r] = dpp<DPP_WAVE_SHR1>(lfill, x[r].v[1]);
-            // right of point 1: lane+1's point 0; lane 63 takes lane 0's point 0 of row r+1
-            const double rfill = r + 1 < kFusedRows ? readlane(x[r + 1].v[0], 0) : 0.0;
-            R[r] = dpp<DPP_WAVE_SHL1>(rfill, x[r].v[0]);
+            // left of point 0: lane-1's last point; lane 0 takes lane 63's last point of row r-1
+            const double lfill = r > 0 ? readlane(x[r - 1][P - 1], kWave - 1) : 0.0;
+            L[r] = dpp<DPP_WAVE_SHR1>(lfill, x[r][P - 1]);
+            // right of the last point: lane+1's point 0; lane 63 takes lane 0's point 0 of row r+1
+            const double rfill = r + 1 < kFusedRows ? readlane(x[r + 1][0], 0) : 0.0;
+            R[r] = dpp<DPP_WAVE_SHL1>(rfill, x[r][0]);
         }
 #pragma unroll
         for (int r = 0; r < kFusedRows; ++r) {
-            const double m0 = x[r].v[0], m1 = x[r].v[1];
-            x[r].v[0] = heat(L[r], m0, m1, c);
-            x[r].v[1] = heat(m0, m1, R[r], c);
+            double prev = L[r];
+#pragma unroll
+            for (int e = 0; e < P; ++e) {
+                const double m = x[r][e];
+                const double right = e + 1 < P ? x[r][e + 1] : R[r];
+                x[r][e] = heat(prev, m, right, c);
+                prev = m;
+            }
         }
     }
 
 #pragma unroll
-    for (int r = 0; r < kFusedRows; ++r) {
-        const int64_t i = w0 + r * 2 * kWave + 2 * lane;  // even when aligned
-        const bool ok0 = i >= static_cast<int64_t>(o0) && i < static_cast<int64_t>(o1);
-        const bool ok1 = i + 1 >= static_cast<int64_t>(o0) && i + 1 < static_cast<int64_t>(o1);
-        if (aligned && ok0 && ok1) {
-            reinterpret_cast<V2*>(next + i)[0] = x[r];
-        } else {
-            if (ok0) next[i] = x[r].v[0];
-            if (ok1) next[i + 1] = x[r].v[1];
+    for (int r = 0; r < kFusedRows; ++r)
+#pragma unroll
+        for (int h = 0; h < P / 2; ++h) {
+            const int64_t i = w0 + r * ROW + lane * P + 2 * h;  // even when aligned
+            const bool ok0 = i >= static_cast<int64_t>(o0) && i < static_cast<int64_t>(o1);
+            const bool ok1 = i + 1 >= static_cast<int64_t>(o0) && i + 1 < static_cast<int64_t>(o1);
+            if (aligned && ok0 && ok1) {
+                V2 v;
+                v.v[0] = x[r][2 * h];
+                v.v[1] = x[r][2 * h + 1];
+                *reinterpret_cast<V2*>(next + i) = v;
+            } else {
+                if (ok0) next[i] = x[r][2 * h];
+                if (ok1) next[i + 1] = x[r][2 * h + 1];
+            }
         }
-    }
 }
 
 int launch_fused(const double* cur, double* next, uint64_t n, uint64_t out_lo, uint64_t out_hi, const double* lh,
