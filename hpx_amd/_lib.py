@@ -27,7 +27,7 @@ P_LT, P_LE, P_GT, P_GE, P_EQ, P_NE, P_NOT_LT, P_BITS = range(8)
 H2H, H2D, D2H, D2D, DEFAULT = range(5)
 GEN_IOTA, GEN_BITS, GEN_RANGE, GEN_UNIT = range(4)
 ALGO_REDUCE, ALGO_SCAN, ALGO_COPY_IF, ALGO_SORT, ALGO_SORT_BY_KEY, ALGO_MERGE = range(6)
-STENCIL_MAX_FUSED = 8  # HPXHIP_STENCIL_MAX_FUSED
+STENCIL_MAX_FUSED = 16  # HPXHIP_STENCIL_MAX_FUSED
 
 SUCCESS = 0
 ERROR_INVALID_ARGUMENT = 10001

@@ -65,7 +65,7 @@ __global__ __launch_bounds__(kThreads) void k_heat_scalar(const double* __restri
 }
 
 // ------------------------------------------------------ temporal blocking
-// S fused steps per pass (S even, 2..8): each wave owns a window of WIN = 512
+// S fused steps per pass (S even, 2..16): each wave owns a window of WIN = 512
 // consecutive points held in registers as ROWS rows x 64 lanes x P points
 // (row r, lane l -> window points r*64P + l*P .. +P-1; loads and stores are
 // 16-B vectors), steps it S times with the neighbours taken from the
@@ -76,7 +76,8 @@ __global__ __launch_bounds__(kThreads) void k_heat_scalar(const double* __restri
 // the cross-lane moves per point of P = 2 (the pass is FP64-VALU bound at
 // S = 8).
 // HBM traffic per pass: 8 B read x WIN/OUT + 8 B written per point, i.e.
-// 16.26 B per point for S = 8 steps instead of 16 B per point per step.
+// 16.26 B per point for S = 8 steps (16.55 B for S = 16) instead of 16 B per
+// point per step.
 // Every point sees exactly the single-step arithmetic (heat() above, same
 // association, -ffp-contract=off), so results are bit-identical to S single
 // steps.  Points outside [0, n) come from the halos: cur[-j] = lh[S - j],
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(kThreads) void k_heat_fused(const double* __restric
                                                           uint64_t n, uint64_t out_lo, uint64_t out_hi,
                                                           const double* __restrict__ lh,
                                                           const double* __restrict__ rh, double c, bool aligned) {
-    static_assert(S >= 2 && S <= 8 && S % 2 == 0, "even fused step counts");
+    static_assert(S >= 2 && S <= 16 && S % 2 == 0, "even fused step counts");
     constexpr int P = kFusedPts;
     constexpr int ROW = P * kWave;
     using V2 = vec<double, 2>;
@@ -191,6 +192,10 @@ int launch_fused(const double* cur, double* next, uint64_t n, uint64_t out_lo, u
         case 4: hipLaunchKernelGGL(k_heat_fused<4>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
         case 6: hipLaunchKernelGGL(k_heat_fused<6>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
         case 8: hipLaunchKernelGGL(k_heat_fused<8>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
+        case 10: hipLaunchKernelGGL(k_heat_fused<10>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
+        case 12: hipLaunchKernelGGL(k_heat_fused<12>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
+        case 14: hipLaunchKernelGGL(k_heat_fused<14>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
+        case 16: hipLaunchKernelGGL(k_heat_fused<16>, g, b, 0, s, cur, next, n, out_lo, out_hi, lh, rh, c, aligned); break;
         default: return HPXHIP_ERROR_INVALID_ARGUMENT;
     }
     HPXHIP_CHECK_LAUNCH();

@@ -319,7 +319,7 @@ int hpxhip_stencil_heat_step(const double* cur, double* next, uint64_t n,
    Bit-identical to `steps` calls of hpxhip_stencil_heat_step.  Replaces the
    per-step partition update of 1d_stencil_8.cpp:482-531 (the halo becomes
    `steps` points wide, exchanged once per pass). */
-#define HPXHIP_STENCIL_MAX_FUSED 8
+#define HPXHIP_STENCIL_MAX_FUSED 16
 int hpxhip_stencil_heat_steps(const double* cur, double* next, uint64_t n, uint64_t out_lo, uint64_t out_hi,
                               const double* left_halo_dev, const double* right_halo_dev, int steps, double k,
                               double dt, double dx, hpxhip_stream stream);
@@ -328,8 +328,8 @@ int hpxhip_stencil_heat_steps(const double* cur, double* next, uint64_t n, uint6
    of up to HPXHIP_STENCIL_MAX_FUSED steps for rings of >= 1024 points. */
 int hpxhip_stencil_heat_run(double* u0, double* u1, uint64_t n, uint64_t nt, double k,
                             double dt, double dx, hpxhip_stream stream);
-/* As hpxhip_stencil_heat_run with the fewest passes (nt = 8q + r -> q passes
-   of 8, then r's); *result_in_u1 (set on return, host memory) tells which
+/* As hpxhip_stencil_heat_run with the fewest passes (nt = 16q + r -> q
+   passes of 16, then r's); *result_in_u1 (set on return, host memory) tells which
    buffer holds the result. */
 int hpxhip_stencil_heat_run_fused(double* u0, double* u1, uint64_t n, uint64_t nt, double k, double dt,
                                   double dx, int* result_in_u1, hpxhip_stream stream);

@@ -36,6 +36,7 @@ cur = alloc(8*N); L.check(lib.hpxhip_generate(L.F64, L.GEN_IOTA, 0, 0, 0, cur, N
 timeit("stencil step f64", lambda: lib.hpxhip_stencil_heat_step(cur, a, N, cur, cur, 0.5, 1.0, 1.0, st), 16*N)
 # temporal blocking: 8 steps in one pass (16.5 B/point of HBM traffic); GB/s column = 16 B/point/step model
 timeit("stencil 8 fused steps f64", lambda: lib.hpxhip_stencil_heat_steps(cur, a, N, 0, N, cur, cur, 8, 0.5, 1.0, 1.0, st), 8*16*N)
+timeit("stencil 16 fused steps f64", lambda: lib.hpxhip_stencil_heat_steps(cur, a, N, 0, N, cur, cur, 16, 0.5, 1.0, 1.0, st), 16*16*N)
 keys = a
 def srt():
     L.check(lib.hpxhip_generate(L.U64, L.GEN_BITS, 7, 0, 0, keys, N, st))

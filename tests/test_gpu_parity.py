@@ -428,12 +428,12 @@ def test_stencil_golden_and_random(gpu_target):
 
 @pytest.mark.parametrize("nx", [1024, 4097, 100003])
 def test_stencil_fused_run_bit_exact(gpu_target, nx):
-    """hpxhip_stencil_heat_run with temporal blocking (passes of up to 8
+    """hpxhip_stencil_heat_run with temporal blocking (passes of up to 16
     steps, the pass count matched to nt's parity so the result lands in the
     documented buffer) against the serial oracle, bit for bit."""
     from hpx_amd import stencil
     u = rnd(np.float64, nx, 31 + nx)
-    for nt in [1, 2, 3, 4, 5, 7, 8, 9, 10, 16, 17, 26]:
+    for nt in [1, 2, 3, 4, 5, 7, 8, 9, 10, 16, 17, 26, 33, 48]:
         np.testing.assert_array_equal(stencil.heat_run(u, nt, tgt=gpu_target), O.stencil_heat(u, nt), err_msg=f"nt={nt}")
     # hpxhip_stencil_heat_run keeps its buffer contract (u0 for even nt, u1 for odd)
     import ctypes
@@ -446,7 +446,7 @@ def test_stencil_fused_run_bit_exact(gpu_target, nx):
         np.testing.assert_array_equal(res.to_host(), O.stencil_heat(u, nt), err_msg=f"heat_run nt={nt}")
 
 
-@pytest.mark.parametrize("steps", [1, 2, 4, 6, 8])
+@pytest.mark.parametrize("steps", [1, 2, 4, 6, 8, 10, 16])
 def test_stencil_heat_steps_halos_subranges(gpu_target, steps):
     """hpxhip_stencil_heat_steps: explicit `steps`-point halos, output
     sub-ranges (even and odd starts), misaligned buffers; expected = `steps`
