@@ -10,6 +10,8 @@
 // round's hits are compacted through LDS and stored by consecutive lanes.
 // Input loads are nontemporal.  Traffic: 8 B read + 8 B x selectivity
 // written per int64 element.
+#include <cstdlib>
+
 #include "internal.hpp"
 #include "copy_if_kernel.hpp"
 
@@ -40,16 +42,30 @@ size_t scratch_total(uint64_t n) {
     return align_up(kSlotsOff + ntiles_for<T, 8>(n) * tile_state<uint64_t>::bytes_per_tile(), 256);
 }
 
-template <typename T, bool ALIGNED, typename P>
-int launch_copy_if(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev, char* ws, hipStream_t s) {
+// Look-back values are hit counts, at most n: below 2^32 elements they travel
+// as 32-bit values (one granule per slot instead of two).  That is what
+// brings the kernel to 64 VGPRs, i.e. two 1024-thread workgroups per CU, so
+// one workgroup's look-back and write-out overlap the other's loads: 2^30
+// int64 at 50 % hits 2.55 -> 2.32 ms (profiles/r01_ubench_copyif_state.log).
+template <typename T, bool ALIGNED, typename SV, typename P>
+int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev, char* ws, hipStream_t s) {
     constexpr int R = rounds_for<ALIGNED>();
     const uint64_t ntiles = ntiles_for<T, R>(n);
-    HPXHIP_CHECK(hipMemsetAsync(ws, 0, align_up(kSlotsOff + ntiles * tile_state<uint64_t>::bytes_per_tile(), 256), s));
-    tile_state<uint64_t> st{reinterpret_cast<uint64_t*>(ws + kSlotsOff), device_error_word(s)};
-    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads), 0, s, in,
-                       out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles);
+    HPXHIP_CHECK(hipMemsetAsync(ws, 0, align_up(kSlotsOff + ntiles * tile_state<SV>::bytes_per_tile(), 256), s));
+    tile_state<SV> st{reinterpret_cast<uint64_t*>(ws + kSlotsOff), device_error_word(s)};
+    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, 4, 0, SV>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads), 0,
+                       s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles);
     HPXHIP_CHECK_LAUNCH();
     return 0;
+}
+
+template <typename T, bool ALIGNED, typename P>
+int launch_copy_if(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev, char* ws, hipStream_t s) {
+    // HPXHIP_COPY_IF_STATE64=1 forces the 64-bit form at any n (tests; read per call).
+    const char* e = getenv("HPXHIP_COPY_IF_STATE64");
+    const bool force64 = e && e[0] == '1';
+    if (n < (uint64_t{1} << 32) && !force64) return launch_copy_if_sv<T, ALIGNED, uint32_t>(in, out, n, p, count_dev, ws, s);
+    return launch_copy_if_sv<T, ALIGNED, uint64_t>(in, out, n, p, count_dev, ws, s);
 }
 
 }  // namespace

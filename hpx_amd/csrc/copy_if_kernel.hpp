@@ -28,10 +28,15 @@ template <int BITS>
 using hit_word = std::conditional_t<(BITS <= 32), uint32_t, uint64_t>;
 
 // MINW: minimum waves per SIMD (8 = two 1024-thread workgroups per CU).
-template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4>
+// ABL: ablation bits for scripts/ubench/copyif.hip only (wrong output):
+//   1 = no look-back (tile prefix 0), 2 = hits stored straight from
+//   registers at their ranks (no LDS compaction), 4 = no write-out at all.
+// SV: tile-state value type (uint32_t halves the look-back granules; valid
+// while n < 2^32).
+template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4, int ABL = 0, typename SV = uint64_t>
 __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out, uint64_t n, Pred pred,
                                                        uint64_t* count_dev, uint32_t* counter,
-                                                       tile_state<uint64_t> st, uint64_t ntiles) {
+                                                       tile_state<SV> st, uint64_t ntiles) {
     constexpr int V = 16 / sizeof(T);
     constexpr uint64_t TILE = tile_elems<T, ROUNDS>();
     constexpr uint64_t WAVE_ELEMS = TILE / kWaves;
@@ -90,17 +95,17 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out,
     }
 
     if (wave == 0) {
-        uint64_t p = 0;
+        SV p = 0;
         if (tile == 0) {
-            if (lane == 0) st.publish(0, static_cast<uint64_t>(agg), TILE_INCLUSIVE);
-        } else {
-            if (lane == 0) st.publish(tile, static_cast<uint64_t>(agg), TILE_AGGREGATE);
+            if (lane == 0) st.publish(0, static_cast<SV>(agg), TILE_INCLUSIVE);
+        } else if constexpr ((ABL & 1) == 0) {
+            if (lane == 0) st.publish(tile, static_cast<SV>(agg), TILE_AGGREGATE);
             p = st.exclusive_prefix(tile, op_plus{});
-            if (lane == 0) st.publish(tile, p + agg, TILE_INCLUSIVE);
+            if (lane == 0) st.publish(tile, static_cast<SV>(p + agg), TILE_INCLUSIVE);
         }
         if (lane == 0) {
             s_prefix = p;
-            if (tile == ntiles - 1) *count_dev = p + agg;
+            if (tile == ntiles - 1) *count_dev = static_cast<uint64_t>(p) + agg;
         }
     }
     __syncthreads();
@@ -109,6 +114,26 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out,
     // instruction covers one contiguous run of the output (a direct
     // out[base + rank] scatter leaves holes in every wave store).
     const uint64_t base = s_prefix + wave_prefix;
+    if constexpr ((ABL & 4) != 0) return;
+    if constexpr ((ABL & 2) != 0) {
+        uint32_t rb = 0;
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) {
+            uint32_t cnt = 0, below = 0;
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const uint64_t m = __ballot((hit >> (r * V + e)) & 1u);
+                below += rank_below(m);
+                cnt += static_cast<uint32_t>(__builtin_popcountll(m));
+            }
+            uint32_t lb = 0;
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+                if ((hit >> (r * V + e)) & 1u) out[base + rb + below + lb++] = x[r].v[e];
+            rb += cnt;
+        }
+        return;
+    }
     T* stage = s_stage[wave];
     uint32_t round_base = 0;
 #pragma unroll

@@ -40,8 +40,8 @@ constexpr uint64_t tile_elems() {
 }
 
 template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED, int ROUNDS = kRounds,
-          int THREADS = kThreads, bool LOOKBACK = true>
-__global__ __launch_bounds__(THREADS) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init,
+          int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1>
+__global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init,
                                                    const T* prefix_dev, uint32_t* counter, tile_state<T> st) {
     constexpr int V = 16 / sizeof(T);
     constexpr int WAVES = THREADS / kWave;

@@ -12,6 +12,11 @@ using namespace hpxhip::copy_if_detail;
 using T = int64_t;
 using P = pred_fn<HPXHIP_P_NOT_LT, T>;
 
+__global__ void k_fill_blocky(T* p, uint64_t n) {  // sign constant over aligned 128-element blocks
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i < n) { uint64_t z = (i >> 7) * 0x9E3779B97F4A7C15ull; z ^= z >> 31; z *= 0xBF58476D1CE4E5B9ull; z ^= z >> 29;
+    p[i] = (z >> 63) ? -(T)(i + 1) : (T)i; }
+}
 __global__ void k_fill(T* p, uint64_t n) {
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i < n) { uint64_t z = i * 0x9E3779B97F4A7C15ull; z ^= z >> 31; z *= 0xBF58476D1CE4E5B9ull; z ^= z >> 29; p[i] = (T)z; }
@@ -22,6 +27,8 @@ int main() {
   T *in, *out; char* ws; uint32_t* err; uint64_t* cnt;
   CK(hipMalloc(&in, N * 8)); CK(hipMalloc(&out, N * 8)); CK(hipMalloc(&ws, 64 << 20)); CK(hipMalloc(&err, 64));
   CK(hipMalloc(&cnt, 64));
+  T* blocky; CK(hipMalloc(&blocky, N * 8));
+  hipLaunchKernelGGL(k_fill_blocky, dim3(N / 256), dim3(256), 0, 0, blocky, N);
   hipLaunchKernelGGL(k_fill, dim3(N / 256), dim3(256), 0, 0, in, N);
   CK(hipMemset(err, 0, 64));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -37,22 +44,38 @@ int main() {
            B / t[7] / 1e6, double(c) / N);
     fflush(stdout);
   };
-  auto variant = [&](auto rounds_c, auto minw_c, const char* name) {
+  auto variant = [&](auto rounds_c, auto abl_c, const char* name) {
     constexpr int R = decltype(rounds_c)::value;
-    constexpr int W = decltype(minw_c)::value;
+    constexpr int A = decltype(abl_c)::value;
     const uint64_t ntiles = (N + tile_elems<T, R>() - 1) / tile_elems<T, R>();
     const size_t total = align_up(256 + ntiles * tile_state<uint64_t>::bytes_per_tile(), 256);
     tile_state<uint64_t> st{reinterpret_cast<uint64_t*>(ws + 256), err};
     run(name, [&] {
       CK(hipMemsetAsync(ws, 0, total, 0));
-      k_copy_if<T, P, true, R, W><<<ntiles, kThreads>>>(in, out, N, P{0}, cnt, reinterpret_cast<uint32_t*>(ws), st, ntiles);
+      k_copy_if<T, P, true, R, 4, A><<<ntiles, kThreads>>>(in, out, N, P{0}, cnt, reinterpret_cast<uint32_t*>(ws), st, ntiles);
     });
   };
+  auto ovariant = [&](auto minw_c, auto sv_c, const char* name) {
+    constexpr int R = 8;
+    constexpr int W = decltype(minw_c)::value;
+    using SV = typename decltype(sv_c)::type;
+    const uint64_t ntiles = (N + tile_elems<T, R>() - 1) / tile_elems<T, R>();
+    const size_t total = align_up(256 + ntiles * tile_state<SV>::bytes_per_tile(), 256);
+    tile_state<SV> st{reinterpret_cast<uint64_t*>(ws + 256), err};
+    run(name, [&] {
+      CK(hipMemsetAsync(ws, 0, total, 0));
+      k_copy_if<T, P, true, R, W, 0, SV><<<ntiles, kThreads>>>(in, out, N, P{0}, cnt, reinterpret_cast<uint32_t*>(ws), st, ntiles);
+    });
+  };
+  using I4 = std::integral_constant<int, 4>;
+  using I8 = std::integral_constant<int, 8>;
+  using U64 = std::type_identity<uint64_t>;
+  using U32 = std::type_identity<uint32_t>;
   for (int rep = 0; rep < 2; ++rep) {
-    variant(std::integral_constant<int, 8>{}, std::integral_constant<int, 4>{}, "copy_if R8");
-    variant(std::integral_constant<int, 8>{}, std::integral_constant<int, 8>{}, "copy_if R8 2/CU");
-    variant(std::integral_constant<int, 12>{}, std::integral_constant<int, 4>{}, "copy_if R12");
-    variant(std::integral_constant<int, 16>{}, std::integral_constant<int, 4>{}, "copy_if R16");
+    ovariant(I4{}, U64{}, "R8 minw4 u64 (shipped)");
+    ovariant(I8{}, U64{}, "R8 minw8 u64");
+    ovariant(I4{}, U32{}, "R8 minw4 u32");
+    ovariant(I8{}, U32{}, "R8 minw8 u32");
   }
   uint32_t h = 0; CK(hipMemcpy(&h, err, 4, hipMemcpyDeviceToHost)); printf("deverr %u\n", h);
   return 0;

@@ -28,7 +28,8 @@ int main() {
     printf("%-34s min %7.3f ms med %7.3f ms  %7.1f GB/s (med %7.1f)\n", name, t[0], t[7], B / t[0] / 1e6, B / t[7] / 1e6);
     fflush(stdout);
   };
-  auto variant = [&](auto rounds_c, auto threads_c, auto lb_c, const char* name) {
+  auto variant = [&](auto rounds_c, auto threads_c, auto lb_c, const char* name, auto minw_c) {
+    constexpr int MW = decltype(minw_c)::value;
     constexpr int R = decltype(rounds_c)::value;
     constexpr int TH = decltype(threads_c)::value;
     constexpr bool LB = decltype(lb_c)::value;
@@ -38,17 +39,20 @@ int main() {
     tile_state<T> st{reinterpret_cast<uint64_t*>(ws + 256), err};
     run(name, [&] {
       CK(hipMemsetAsync(ws, 0, total, 0));
-      scan_detail::k_scan<T, Conv, op_plus, true, true, R, TH, LB><<<ntiles, TH>>>(
+      scan_detail::k_scan<T, Conv, op_plus, true, true, R, TH, LB, MW><<<ntiles, TH>>>(
             in, out, N, Conv{0, 0}, op_plus{}, T(0), nullptr, reinterpret_cast<uint32_t*>(ws), st);
     });
   };
 #define V_(R, TH, LB, NAME) variant(std::integral_constant<int, R>{}, std::integral_constant<int, TH>{}, \
-    std::integral_constant<bool, LB>{}, NAME)
+    std::integral_constant<bool, LB>{}, NAME, std::integral_constant<int, 1>{})
+#define VW(R, TH, LB, NAME, MW) variant(std::integral_constant<int, R>{}, std::integral_constant<int, TH>{}, \
+    std::integral_constant<bool, LB>{}, NAME, std::integral_constant<int, MW>{})
   for (int rep = 0; rep < 2; ++rep) {
-    V_(8, 1024, true, "T1024 R8 lookback");
-    V_(12, 1024, true, "T1024 R12 lookback");
     V_(16, 1024, true, "T1024 R16 lookback (shipped)");
-    V_(16, 1024, false, "T1024 R16 no-lookback");
+    V_(8, 1024, true, "T1024 R8 lookback");
+    VW(8, 1024, true, "T1024 R8 lookback minw8", 8);
+    VW(8, 512, true, "T512 R8 lookback minw8", 8);
+    VW(16, 512, true, "T512 R16 lookback minw8", 8);
   }
   uint32_t h = 0; CK(hipMemcpy(&h, err, 4, hipMemcpyDeviceToHost)); printf("deverr %u\n", h);
   return 0;

@@ -477,3 +477,15 @@ def test_stencil_heat_steps_halos_subranges(gpu_target, steps):
 
 def test_device_error_word_clear(gpu_target):
     hpx.compute.device_error_check(gpu_target.device)
+
+
+@pytest.mark.parametrize("n", [0, 1, 65, 4097, 100003, (1 << 20) + 17, 1 << 23])
+def test_copy_if_state64(pol, gpu_target, n, monkeypatch):
+    """The 64-bit look-back form (used from 2^32 elements on) at small n."""
+    monkeypatch.setenv("HPXHIP_COPY_IF_STATE64", "1")
+    a = rnd(np.int64, n, 23, -1000, 1000)
+    d, o = dev(a, gpu_target), hpx.vector(max(n, 1), dtype=np.int64, tgt=gpu_target)
+    _, end = P.copy_if(pol, d.begin(), d.end(), o.begin(), F.not_less_than(0))
+    exp = O.copy_if(a, "not_less_than", 0)
+    assert end - o.begin() == exp.size
+    np.testing.assert_array_equal(o.to_host()[: exp.size], exp)
