@@ -18,6 +18,8 @@ calls one whole-algorithm entry point of the C ABI (include/hpxhip.h):
   transform_exclusive_scan   transform_exclusive_scan.hpp:317
   sort / sort_by_key         sort.hpp:364, sort_by_key.hpp:42-78
   generate (splitmix/iota)   generate.hpp (device generator functors)
+  for_loop / for_loop_n      for_loop.hpp:808 (inductions: for_loop_induction.hpp;
+                             reductions: for_loop_reduction.hpp:35-231)
 
 A policy must be rebound to a hip executor (``par.on(hip_exec)``) or all
 iterators must be device iterators of one target (then that target's
@@ -399,21 +401,135 @@ class induction:
         self.value, self.stride = value, int(stride)
 
 
+class reduction:
+    """for_loop_reduction.hpp:35-132 reduction(var, identity, combiner).
+
+    ``var`` is the live-out object: a one-element (or 0-d) numpy array, the
+    Python stand-in for the reference's ``T&``.  The reference gives every OS
+    thread a view initialised with ``identity`` and, at loop exit, folds
+    ``var = op(var, view_k)`` over the views (62-66).  Here one launch forms a
+    single view, ``identity (op) f(x_0) (op) ... (op) f(x_{n-1})`` (the
+    transform_reduce kernel with init = identity), and the exit folds it into
+    ``var``.  With a neutral identity -- every reduction_* helper without an
+    explicit identity -- this equals the reference's result for any thread
+    count; with a non-neutral explicit identity the reference's result
+    depends on its OS thread count, and ours is the one-view result."""
+    __slots__ = ("var", "identity", "op")
+
+    def __init__(self, var, identity, op):
+        if not (isinstance(var, np.ndarray) and var.size == 1):
+            raise TypeError("reduction: the live-out variable must be a one-element numpy array (T&)")
+        self.var, self.identity, self.op = var, identity, F.require(op, F.BinaryOp, "reduction")
+
+
+def _ident(var, value):
+    if not isinstance(var, np.ndarray):
+        raise TypeError("reduction: the live-out variable must be a one-element numpy array (T&)")
+    return var.dtype.type(value)
+
+
+def reduction_plus(var, identity=None):
+    """for_loop_reduction.hpp:135-147 (identity T())."""
+    return reduction(var, _ident(var, 0) if identity is None else identity, F.plus)
+
+
+def reduction_multiplies(var, identity=None):
+    """for_loop_reduction.hpp:149-161 (identity T(1))."""
+    return reduction(var, _ident(var, 1) if identity is None else identity, F.multiplies)
+
+
+def reduction_bit_and(var, identity=None):
+    """for_loop_reduction.hpp:163-175 (identity ~T())."""
+    return reduction(var, ~_ident(var, 0) if identity is None else identity, F.bit_and)
+
+
+def reduction_bit_or(var, identity=None):
+    """for_loop_reduction.hpp:177-189 (identity T())."""
+    return reduction(var, _ident(var, 0) if identity is None else identity, F.bit_or)
+
+
+def reduction_bit_xor(var, identity=None):
+    """for_loop_reduction.hpp:191-203 (identity T())."""
+    return reduction(var, _ident(var, 0) if identity is None else identity, F.bit_xor)
+
+
+def reduction_min(var, identity=None):
+    """for_loop_reduction.hpp:205-217 (identity = var's current value)."""
+    return reduction(var, _ident(var, var.reshape(-1)[0]) if identity is None else identity, F.minimum)
+
+
+def reduction_max(var, identity=None):
+    """for_loop_reduction.hpp:219-231 (identity = var's current value)."""
+    return reduction(var, _ident(var, var.reshape(-1)[0]) if identity is None else identity, F.maximum)
+
+
+def _for_loop_reduce(pol, n, vars_, red, body):
+    """The for_loop with one reduction: the body's inputs feed the
+    transform_reduce kernels (unary or binary map), and the loop exit folds
+    the single view into the live-out variable (for_loop_reduction.hpp:60-66)."""
+    try:
+        ins = [vars_[i] for i in body.ins]
+    except IndexError:
+        raise IndexError("for_loop_n: loop body refers to a variable that is not passed") from None
+    if not all(isinstance(v, iterator) for v in ins):
+        raise TypeError("for_loop_n: the reduction body must read device iterators")
+    stream, tgt, is_task = _context(pol, *ins)
+    adt = dtype_code(red.var.dtype)
+    dev, host = _slots_for(tgt).next()
+    fn = body.fn
+    if isinstance(fn, F.Unary):
+        L.call("hpxhip_transform_reduce", ins[0].dtype, adt, red.op.kind, fn.kind, L.scalars_buf(adt, fn.scalars),
+               L.scalar_buf(adt, red.identity), _vp(ins[0].address), n, _vp(dev), stream, None, 0)
+    else:
+        if ins[0].dtype != ins[1].dtype:
+            raise TypeError("for_loop_n: both inputs of a binary body must have one dtype")
+        L.call("hpxhip_transform_reduce_binary", ins[0].dtype, adt, red.op.kind, fn.kind,
+               L.scalars_buf(adt, fn.scalars), L.scalar_buf(adt, red.identity), _vp(ins[0].address),
+               _vp(ins[1].address), n, _vp(dev), stream, None, 0)
+    L.call("hpxhip_memcpy_async", _vp(host), _vp(dev), 8, L.D2H, stream)
+
+    def exit_iteration():
+        flat = red.var.reshape(-1)
+        with np.errstate(over="ignore"):  # integer combiners wrap like the kernels (and T in C++)
+            flat[0] = red.op(flat[0], red.var.dtype.type(_read_host(host, adt)))
+
+    return _finish(is_task, stream, tgt, exit_iteration)
+
+
 def for_loop_n(pol, first, count, *args):
     """for_loop.hpp:808 for_loop_n(policy, first, size, inductions..., f) as
     for_loop_compute.cu uses it: the loop iterator and pointer inductions
     (stride 1) walk device ranges in lock step and the body writes one of
     them from one or two others (functional.assign).  The iteration space
     maps onto the elementwise transform kernels; returns None (future<void>
-    under par(task))."""
+    under par(task)).  With one ``reduction`` argument
+    (for_loop_reduction.hpp) the body is a functional.accumulate and the
+    loop runs on the transform_reduce kernels."""
     if not args:
         raise TypeError("for_loop_n: missing loop body")
     *inds, body = args
+    reds = [a for a in inds if isinstance(a, reduction)]
+    if reds:
+        if len(reds) > 1:
+            raise TypeError("for_loop_n: one reduction per loop is carried by the C ABI")
+        body = F.require(body, F.Accumulate, "for_loop_n")
+        if not isinstance(first, iterator):
+            raise TypeError("for_loop_n: the loop variable must be a device iterator")
+        for ind in inds:
+            if isinstance(ind, induction) and ind.stride != 1:
+                raise ValueError("for_loop_n: pointer inductions with stride != 1 are not supported")
+        n = int(count)
+        if n < 0:
+            raise ValueError("for_loop_n: negative count")
+        vars_ = [first] + [a.value if isinstance(a, induction) else a for a in inds]
+        if not (0 <= body.red < len(vars_)) or vars_[body.red] is not reds[0]:
+            raise IndexError("for_loop_n: accumulate() must name the reduction's position")
+        return _for_loop_reduce(pol, n, vars_, reds[0], body)
     body = F.require(body, F.LoopBody, "for_loop_n")
     for ind in inds:
         if not isinstance(ind, induction):
-            raise TypeError("for_loop_n: extra arguments must be hpx::parallel::induction objects "
-                            "(reductions are not carried by the C ABI)")
+            raise TypeError("for_loop_n: extra arguments must be hpx::parallel::induction or "
+                            "hpx::parallel::reduction objects")
         if not isinstance(ind.value, iterator):
             raise TypeError("for_loop_n: inductions over device iterators only")
         if ind.stride != 1:

@@ -228,6 +228,24 @@ def assign(out: int, fn, *ins) -> LoopBody:
     raise TypeError("assign: a Unary functor takes one loop variable, a Binary functor two")
 
 
+@dataclass(frozen=True)
+class Accumulate:
+    """Body of for_loop / for_loop_n with a reduction: folds
+    ``fn(*vars[ins[0]] [, *vars[ins[1]]])`` into the reduction variable at
+    position ``red`` with the reduction's combiner.
+    for_loop_reduction.cpp:37-44's ``[](iterator it, std::size_t& sum) { sum
+    += *it; }`` is ``accumulate(1, identity(), 0)``."""
+    red: int
+    fn: object
+    ins: tuple
+
+
+def accumulate(red: int, fn, *ins) -> Accumulate:
+    if isinstance(fn, Unary) and len(ins) == 1 or isinstance(fn, Binary) and len(ins) == 2:
+        return Accumulate(int(red), fn, tuple(int(i) for i in ins))
+    raise TypeError("accumulate: a Unary functor takes one loop variable, a Binary functor two")
+
+
 # ------------------------------------------------------------------ compare
 @dataclass(frozen=True)
 class Compare:

@@ -56,3 +56,106 @@ def test_for_loop_argument_checks(gpu_target):
         P.for_loop_n(pol, d.begin(), 16, F.assign(3, F.add_value(1), 0))
     with pytest.raises(TypeError):
         F.assign(0, F.add_value(1), 0, 1)
+
+
+# ------------------------------------------------------- for_loop reductions
+# tests/unit/parallel/algorithms/for_loop_reduction.cpp:20-140 restated:
+# 10007 size_t iotas from a random start, body ``r op= *it``, checked against
+# std::accumulate (integer results, bit-exact; products wrap modulo 2^64).
+_N = 10007
+
+
+def _iota(seed, dtype=np.uint64):
+    start = int(np.random.default_rng(seed).integers(0, 1 << 31))
+    return np.arange(start, start + _N, dtype=dtype)
+
+
+def _fold(op, init, xs, mask=(1 << 64) - 1):
+    acc = int(init)
+    for x in xs.tolist():
+        acc = op(acc, int(x)) & mask
+    return acc
+
+
+@pytest.mark.parametrize("task", [False, True])
+def test_for_loop_reduction_plus(gpu_target, task):
+    c = _iota(1)
+    d = hpx.vector.from_host(c, gpu_target)
+    pol = (ex.par(ex.task) if task else ex.par).on(hpx.default_executor(gpu_target))
+    s = np.zeros(1, np.uint64)
+    r = P.for_loop(pol, d.begin(), d.end(), P.reduction_plus(s), F.accumulate(1, F.identity(), 0))
+    if task:
+        r.get()
+    assert int(s[0]) == _fold(lambda a, b: a + b, 0, c)
+
+
+def test_for_loop_reduction_multiplies(gpu_target):
+    c = _iota(2)
+    d = hpx.vector.from_host(c, gpu_target)
+    pol = ex.par.on(hpx.default_executor(gpu_target))
+    # for_loop_reduction.cpp:60: prod starts at 0, so the live-out stays 0
+    prod = np.zeros(1, np.uint64)
+    P.for_loop(pol, d.begin(), d.end(), P.reduction_multiplies(prod), F.accumulate(1, F.identity(), 0))
+    assert int(prod[0]) == 0
+    prod = np.ones(1, np.uint64)
+    P.for_loop(pol, d.begin(), d.end(), P.reduction_multiplies(prod), F.accumulate(1, F.identity(), 0))
+    assert int(prod[0]) == _fold(lambda a, b: a * b, 1, c)
+
+
+@pytest.mark.parametrize("which", ["min", "max"])
+def test_for_loop_reduction_minmax(gpu_target, which):
+    c = _iota(3)
+    np.random.default_rng(3).shuffle(c)
+    d = hpx.vector.from_host(c, gpu_target)
+    pol = ex.par.on(hpx.default_executor(gpu_target))
+    v = np.array([c[0]], np.uint64)   # for_loop_reduction.cpp:96: minval = c[0]
+    red = P.reduction_min(v) if which == "min" else P.reduction_max(v)
+    P.for_loop(pol, d.begin(), d.end(), red, F.accumulate(1, F.identity(), 0))
+    assert int(v[0]) == int(c.min() if which == "min" else c.max())
+
+
+@pytest.mark.parametrize("which", ["and", "or", "xor"])
+def test_for_loop_reduction_bits(gpu_target, which):
+    c = np.random.default_rng(4).integers(0, 2**63, _N, dtype=np.int64) | np.int64(1 << 40)
+    d = hpx.vector.from_host(c, gpu_target)
+    pol = ex.par.on(hpx.default_executor(gpu_target))
+    v = np.zeros(1, np.int64)
+    if which == "and":
+        v[0] = -1
+        red, op, ident = P.reduction_bit_and(v), np.bitwise_and, -1
+    elif which == "or":
+        red, op, ident = P.reduction_bit_or(v), np.bitwise_or, 0
+    else:
+        red, op, ident = P.reduction_bit_xor(v), np.bitwise_xor, 0
+    P.for_loop_n(pol, d.begin(), _N, red, F.accumulate(1, F.identity(), 0))
+    assert int(v[0]) == int(op.reduce(c, initial=ident))
+
+
+def test_for_loop_reduction_inner_product_and_empty(gpu_target):
+    """A reduction body reading the loop iterator and an induction
+    (transform_reduce_binary kernels); an empty loop leaves var op identity."""
+    rng = np.random.default_rng(5)
+    a = rng.integers(-1000, 1000, 1 << 16, dtype=np.int64)
+    b = rng.integers(-1000, 1000, 1 << 16, dtype=np.int64)
+    da, db = hpx.vector.from_host(a, gpu_target), hpx.vector.from_host(b, gpu_target)
+    pol = ex.par.on(hpx.default_executor(gpu_target))
+    s = np.array([7], np.int64)
+    P.for_loop_n(pol, da.begin(), a.size, P.induction(db.begin()), P.reduction_plus(s),
+                 F.accumulate(2, F.multiply(), 0, 1))
+    assert int(s[0]) == 7 + int(np.dot(a, b))
+    e = np.array([11], np.int64)
+    P.for_loop_n(pol, da.begin(), 0, P.reduction_plus(e), F.accumulate(1, F.identity(), 0))
+    assert int(e[0]) == 11
+
+
+def test_for_loop_reduction_argument_checks(gpu_target):
+    d = hpx.vector(16, dtype=np.int64, tgt=gpu_target)
+    pol = ex.par.on(hpx.default_executor(gpu_target))
+    s = np.zeros(1, np.int64)
+    with pytest.raises(TypeError):   # a reduction needs an accumulate body
+        P.for_loop_n(pol, d.begin(), 16, P.reduction_plus(s), F.assign(0, F.add_value(1), 0))
+    with pytest.raises(IndexError):  # accumulate must name the reduction's position
+        P.for_loop_n(pol, d.begin(), 16, P.reduction_plus(s), F.accumulate(0, F.identity(), 0))
+    with pytest.raises(TypeError):
+        P.for_loop_n(pol, d.begin(), 16, P.reduction_plus(s), P.reduction_plus(s),
+                     F.accumulate(1, F.identity(), 0))
