@@ -109,6 +109,16 @@ struct loop_assign {
     }
 };
 
+// loop_accumulate<Red, F, In...> is the body of a for_loop with a reduction:
+// `r = op(r, f(*v[In]...))` where r is the reduction at position Red;
+// for_loop_reduction.cpp:37-44's `[](iterator it, std::size_t& sum) { sum +=
+// *it; }` is loop_accumulate<1, identity, 0>{}.
+template <std::size_t Red, typename F, std::size_t... In>
+struct loop_accumulate {
+    static_assert(sizeof...(In) == 1 || sizeof...(In) == 2, "loop_accumulate: one or two inputs");
+    F f;
+};
+
 // ---- reduction operators not in <functional> ------------------------------
 struct minimum {
     template <typename T> T operator()(T x, T y) const { return y < x ? y : x; }

@@ -484,9 +484,57 @@ induction_stride_helper<It> induction(It it, std::size_t stride = 1) {
     return induction_stride_helper<It>{it, stride};
 }
 
+// for_loop_reduction.hpp:35-132: reduction(var, identity, combiner).  The
+// reference keeps one view per OS thread and folds `var = op(var, view_k)`
+// at loop exit (62-66); here one launch forms a single view (the
+// transform_reduce kernel with init = identity) and the exit folds it into
+// var.  Equal to the reference for a neutral identity (every helper below
+// without an explicit identity); with a non-neutral explicit identity the
+// reference's result depends on its OS thread count.
+template <typename T, typename Op>
+struct reduction_helper {
+    T& var_;
+    T identity_;
+    Op op_;
+};
+template <typename T, typename Op>
+reduction_helper<T, typename std::decay<Op>::type> reduction(T& var, T const& identity, Op&& combiner) {
+    return {var, identity, std::forward<Op>(combiner)};
+}
+template <typename T> reduction_helper<T, std::plus<T>> reduction_plus(T& var) { return {var, T(), {}}; }
+template <typename T> reduction_helper<T, std::plus<T>> reduction_plus(T& var, T const& id) { return {var, id, {}}; }
+template <typename T> reduction_helper<T, std::multiplies<T>> reduction_multiplies(T& var) { return {var, T(1), {}}; }
+template <typename T> reduction_helper<T, std::multiplies<T>> reduction_multiplies(T& var, T const& id) {
+    return {var, id, {}};
+}
+template <typename T> reduction_helper<T, std::bit_and<T>> reduction_bit_and(T& var) { return {var, ~T(), {}}; }
+template <typename T> reduction_helper<T, std::bit_and<T>> reduction_bit_and(T& var, T const& id) {
+    return {var, id, {}};
+}
+template <typename T> reduction_helper<T, std::bit_or<T>> reduction_bit_or(T& var) { return {var, T(), {}}; }
+template <typename T> reduction_helper<T, std::bit_or<T>> reduction_bit_or(T& var, T const& id) { return {var, id, {}}; }
+template <typename T> reduction_helper<T, std::bit_xor<T>> reduction_bit_xor(T& var) { return {var, T(), {}}; }
+template <typename T> reduction_helper<T, std::bit_xor<T>> reduction_bit_xor(T& var, T const& id) {
+    return {var, id, {}};
+}
+template <typename T> reduction_helper<T, compute::hip::functional::minimum> reduction_min(T& var) {
+    return {var, var, {}};
+}
+template <typename T> reduction_helper<T, compute::hip::functional::minimum> reduction_min(T& var, T const& id) {
+    return {var, id, {}};
+}
+template <typename T> reduction_helper<T, compute::hip::functional::maximum> reduction_max(T& var) {
+    return {var, var, {}};
+}
+template <typename T> reduction_helper<T, compute::hip::functional::maximum> reduction_max(T& var, T const& id) {
+    return {var, id, {}};
+}
+
 namespace detail {
 template <typename It>
 It loop_var(It it) { return it; }
+template <typename T, typename Op>
+reduction_helper<T, Op> const& loop_var(reduction_helper<T, Op> const& r) { return r; }
 template <typename It>
 It loop_var(induction_stride_helper<It> const& h) {
     if (h.stride_ != 1)
@@ -494,6 +542,45 @@ It loop_var(induction_stride_helper<It> const& h) {
                              "for_loop_n: pointer inductions with stride != 1 are not supported by the contiguous "
                              "elementwise kernels");
     return h.var_;
+}
+template <typename P, typename Vars, std::size_t Red, typename F, std::size_t... In>
+result_t<P, void> for_loop_body(P&& p, Vars const& v, uint64_t n,
+                                compute::hip::functional::loop_accumulate<Red, F, In...> const& b) {
+    auto const& red = std::get<Red>(v);
+    using T = std::decay_t<decltype(red.identity_)>;
+    using Op = std::decay_t<decltype(red.op_)>;
+    static_assert(std::is_same<std::decay_t<decltype(red)>, reduction_helper<T, Op>>::value,
+                  "loop_accumulate: position Red must name the loop's reduction");
+    auto ins = std::make_tuple(std::get<In>(v)...);
+    auto in0 = std::get<0>(ins);
+    using TI = value_t<decltype(in0)>;
+    auto const& t = target_of(p, in0);
+    T s[2] = {};
+    T init = red.identity_;
+    auto slot = t.result_slot();
+    if constexpr (sizeof...(In) == 1) {
+        tr::unary_t<F>::scalars(b.f, s);
+        check(hpxhip_transform_reduce(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::unary_t<F>::kind, s, &init,
+                                      in0.device_ptr(), n, slot.first, t.stream(), nullptr, 0),
+              "for_loop_n");
+    } else {
+        auto in1 = std::get<1>(ins);
+        static_assert(std::is_same<TI, value_t<decltype(in1)>>::value, "for_loop_n: both inputs need one element type");
+        tr::binary_t<F>::scalars(b.f, s);
+        check(hpxhip_transform_reduce_binary(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::binary_t<F>::kind, s, &init,
+                                             in0.device_ptr(), in1.device_ptr(), n, slot.first, t.stream(), nullptr, 0),
+              "for_loop_n");
+    }
+    check(hpxhip_memcpy_async(slot.second, slot.first, sizeof(T), HPXHIP_D2H, t.stream()), "for_loop_n result");
+    void* host = slot.second;
+    T* var = &red.var_;
+    Op op = red.op_;
+    // exit_iteration (for_loop_reduction.hpp:60-66): fold the view into var
+    return finish<void>(p, t, [host, var, op] {
+        T view;
+        std::memcpy(&view, host, sizeof(T));
+        *var = op(*var, view);
+    });
 }
 template <typename P, typename Vars, std::size_t Out, typename F, std::size_t In0>
 result_t<P, void> for_loop_body(P&& p, Vars const& v, uint64_t n, compute::hip::functional::loop_assign<Out, F, In0> const& b) {
@@ -568,6 +655,14 @@ using parallel::v1::for_each_n;
 using parallel::v1::for_loop;
 using parallel::v1::for_loop_n;
 using parallel::v1::induction;
+using parallel::v1::reduction;
+using parallel::v1::reduction_bit_and;
+using parallel::v1::reduction_bit_or;
+using parallel::v1::reduction_bit_xor;
+using parallel::v1::reduction_max;
+using parallel::v1::reduction_min;
+using parallel::v1::reduction_multiplies;
+using parallel::v1::reduction_plus;
 using parallel::v1::merge;
 using parallel::v1::inclusive_scan;
 using parallel::v1::reduce;
