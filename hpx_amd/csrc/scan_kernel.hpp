@@ -39,8 +39,36 @@ constexpr uint64_t tile_elems() {
     return static_cast<uint64_t>(THREADS) * ROUNDS * (16 / sizeof(T));
 }
 
+// Wave 0 of a tile: scans the WAVES wave totals in s_wave_total with DPP,
+// publishes the tile (aggregate, look-back, inclusive) and leaves in
+// s_wave_total[w] the tile prefix (op) the exclusive prefix of wave w.
+template <typename T, typename Op, int WAVES, bool LOOKBACK>
+__device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& st, Op op, const T* prefix_dev, T init,
+                                            T* s_wave_total) {
+    const T id = Op::template identity<T>();
+    const int lane = lane_id();
+    const T wt = lane < WAVES ? s_wave_total[lane] : id;
+    const T wi = wave_inclusive_scan(wt, op);
+    const T agg = readlane(wi, WAVES - 1);
+    const T wex = wave_shift_right<T, Op>(wi);
+    T p;
+    if (tile == 0) {
+        p = prefix_dev ? *prefix_dev : init;
+        if (lane == 0) st.publish(0, op(p, agg), TILE_INCLUSIVE);
+    } else {
+        if constexpr (LOOKBACK) {
+            if (lane == 0) st.publish(tile, agg, TILE_AGGREGATE);
+            p = st.exclusive_prefix(tile, op);
+            if (lane == 0) st.publish(tile, op(p, agg), TILE_INCLUSIVE);
+        } else {
+            p = id;  // ablation only: measures the pass without the tile hand-off
+        }
+    }
+    if (lane < WAVES) s_wave_total[lane] = op(p, wex);
+}
+
 template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED, int ROUNDS = kRounds,
-          int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1>
+          int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false>
 __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init,
                                                    const T* prefix_dev, uint32_t* counter, tile_state<T> st) {
     constexpr int V = 16 / sizeof(T);
@@ -84,6 +112,23 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
             }
     }
 
+    // EARLY (ablation, associative integer ops only): the tile aggregate is
+    // formed from per-lane folds before the per-round scans, so wave 0
+    // publishes it and walks the look-back while the other waves scan their
+    // rounds.  Measured slower at every tile shape (2.91-2.95 ms vs 2.82-2.84
+    // for 2^30 int64, profiles/r01_ubench_scan_early_agg.log): not shipped.
+    if constexpr (EARLY) {
+        T lt = id;
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r)
+#pragma unroll
+            for (int e = 0; e < V; ++e) lt = op(lt, x[r].v[e]);
+        const T wt = wave_reduce(lt, op);
+        if (lane == 0) s_wave_total[wave] = wt;
+        __syncthreads();
+        if (wave == 0) tile_prefix<T, Op, WAVES, LOOKBACK>(tile, st, op, prefix_dev, init, s_wave_total);
+    }
+
     // ---- per-round lane scan + wave scan; x becomes the wave-local result
     T carry = id;
 #pragma unroll
@@ -103,30 +148,10 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
         for (int e = 0; e < V; ++e) x[r].v[e] = op(pre, local[e]);
         carry = op(carry, readlane(incl, kWave - 1));
     }
-    if (lane == 0) s_wave_total[wave] = carry;
-    __syncthreads();
-
-    // wave prefixes within the tile: wave 0 scans the WAVES totals with DPP
-    if (wave == 0) {
-        const T wt = lane < WAVES ? s_wave_total[lane] : id;
-        const T wi = wave_inclusive_scan(wt, op);
-        const T agg = readlane(wi, WAVES - 1);
-        const T wex = wave_shift_right<T, Op>(wi);
-        T p;
-        if (tile == 0) {
-            p = prefix_dev ? *prefix_dev : init;
-            if (lane == 0) st.publish(0, op(p, agg), TILE_INCLUSIVE);
-        } else {
-            if constexpr (LOOKBACK) {
-                if (lane == 0) st.publish(tile, agg, TILE_AGGREGATE);
-                p = st.exclusive_prefix(tile, op);
-                if (lane == 0) st.publish(tile, op(p, agg), TILE_INCLUSIVE);
-            } else {
-                p = id;  // ablation only: measures the pass without the tile hand-off
-            }
-        }
-        // s_wave_total[w] <- tile prefix (op) exclusive prefix of wave w
-        if (lane < WAVES) s_wave_total[lane] = op(p, wex);
+    if constexpr (!EARLY) {
+        if (lane == 0) s_wave_total[wave] = carry;
+        __syncthreads();
+        if (wave == 0) tile_prefix<T, Op, WAVES, LOOKBACK>(tile, st, op, prefix_dev, init, s_wave_total);
     }
     __syncthreads();
     const T pre = s_wave_total[wave];

@@ -1,0 +1,7 @@
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s22_tests.log 2>&1
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s22_smoke.log 2>&1
+timeout -k 10 300 python -u bench.py > gpurun_out/s22_bench.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/s22_prof -o run -- python3 -u bench.py --no-pmc --no-cpu > gpurun_out/s22_bench_under_rocprof.log 2>&1
