@@ -120,6 +120,9 @@ SIGNATURES = {
     "hpxhip_for_each": [_i, _i, _vp, _vp, _u64, _vp],
     "hpxhip_transform": [_i, _i, _i, _i, _vp, _vp, _vp, _u64, _vp],
     "hpxhip_transform_binary": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _u64, _vp],
+    "hpxhip_transform_strided": [_i, _i, _i, _i, _vp, _vp, ctypes.c_int64, _vp, ctypes.c_int64, _u64, _vp],
+    "hpxhip_transform_binary_strided": [_i, _i, _i, _i, _vp, _vp, ctypes.c_int64, _vp, ctypes.c_int64, _vp,
+                                        ctypes.c_int64, _u64, _vp],
     "hpxhip_transform_reduce": [_i, _i, _i, _i, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _sz],
     "hpxhip_transform_reduce_binary": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _sz],
     "hpxhip_fold": [_i, _i, _vp, _vp, _u64, _vp, _vp],

@@ -398,7 +398,7 @@ class induction:
     __slots__ = ("value", "stride")
 
     def __init__(self, value, stride: int = 1):
-        self.value, self.stride = value, int(stride)
+        self.value, self.stride = value, int(stride)   # stride may be negative (a difference type)
 
 
 class reduction:
@@ -499,10 +499,11 @@ def _for_loop_reduce(pol, n, vars_, red, body):
 def for_loop_n(pol, first, count, *args):
     """for_loop.hpp:808 for_loop_n(policy, first, size, inductions..., f) as
     for_loop_compute.cu uses it: the loop iterator and pointer inductions
-    (stride 1) walk device ranges in lock step and the body writes one of
-    them from one or two others (functional.assign).  The iteration space
-    maps onto the elementwise transform kernels; returns None (future<void>
-    under par(task)).  With one ``reduction`` argument
+    walk device ranges in lock step (induction i's value at iteration k is
+    base + stride*k, for_loop_induction.hpp:210-219) and the body writes one
+    of them from one or two others (functional.assign).  All-stride-1 loops
+    run on the vectorised elementwise transform kernels, others on the
+    strided ones; returns None (future<void> under par(task)).  With one ``reduction`` argument
     (for_loop_reduction.hpp) the body is a functional.accumulate and the
     loop runs on the transform_reduce kernels."""
     if not args:
@@ -517,7 +518,8 @@ def for_loop_n(pol, first, count, *args):
             raise TypeError("for_loop_n: the loop variable must be a device iterator")
         for ind in inds:
             if isinstance(ind, induction) and ind.stride != 1:
-                raise ValueError("for_loop_n: pointer inductions with stride != 1 are not supported")
+                raise ValueError("for_loop_n: a reduction loop reads its inductions with stride 1 "
+                                 "(the transform_reduce kernels are contiguous)")
         n = int(count)
         if n < 0:
             raise ValueError("for_loop_n: negative count")
@@ -532,32 +534,50 @@ def for_loop_n(pol, first, count, *args):
                             "hpx::parallel::reduction objects")
         if not isinstance(ind.value, iterator):
             raise TypeError("for_loop_n: inductions over device iterators only")
-        if ind.stride != 1:
-            raise ValueError("for_loop_n: pointer inductions with stride != 1 are not supported by the "
-                             "contiguous elementwise kernels")
     if not isinstance(first, iterator):
         raise TypeError("for_loop_n: the loop variable must be a device iterator")
     n = int(count)
     if n < 0:
         raise ValueError("for_loop_n: negative count")
     vars_ = [first] + [ind.value for ind in inds]
+    strides = [1] + [ind.stride for ind in inds]
     try:
-        out = vars_[body.out]
+        out, so = vars_[body.out], strides[body.out]
         ins = [vars_[i] for i in body.ins]
+        sis = [strides[i] for i in body.ins]
     except IndexError:
         raise IndexError("for_loop_n: loop body refers to a variable that is not passed") from None
+    if n > 0:
+        # every iteration's element must lie inside its vector (value_proxy
+        # semantics: the reference would run off the end of the allocation)
+        for it, st in zip([out] + ins, [so] + sis):
+            lo, hi = it.pos, it.pos + st * (n - 1)
+            if min(lo, hi) < 0 or max(lo, hi) >= it.vec.size():
+                raise ValueError("for_loop_n: an induction walks outside its vector")
+        if so == 0 and n > 1:
+            raise ValueError("for_loop_n: the written induction has stride 0")
     stream, tgt, is_task = _context(pol, out, *ins)
     fn = body.fn
+    strided = any(st != 1 for st in [so] + sis)
     if isinstance(fn, F.Unary):
         cdt = _compute_dtype(ins[0].dtype, fn)
-        L.call("hpxhip_transform", ins[0].dtype, cdt, out.dtype, fn.kind, L.scalars_buf(cdt, fn.scalars),
-               _vp(ins[0].address), _vp(out.address), n, stream)
+        if strided:
+            L.call("hpxhip_transform_strided", ins[0].dtype, cdt, out.dtype, fn.kind, L.scalars_buf(cdt, fn.scalars),
+                   _vp(ins[0].address), sis[0], _vp(out.address), so, n, stream)
+        else:
+            L.call("hpxhip_transform", ins[0].dtype, cdt, out.dtype, fn.kind, L.scalars_buf(cdt, fn.scalars),
+                   _vp(ins[0].address), _vp(out.address), n, stream)
     else:
         if ins[0].dtype != ins[1].dtype:
             raise TypeError("for_loop_n: both inputs of a binary body must have one dtype")
         cdt = _compute_dtype(ins[0].dtype, fn)
-        L.call("hpxhip_transform_binary", ins[0].dtype, cdt, out.dtype, fn.kind, L.scalars_buf(cdt, fn.scalars),
-               _vp(ins[0].address), _vp(ins[1].address), _vp(out.address), n, stream)
+        if strided:
+            L.call("hpxhip_transform_binary_strided", ins[0].dtype, cdt, out.dtype, fn.kind,
+                   L.scalars_buf(cdt, fn.scalars), _vp(ins[0].address), sis[0], _vp(ins[1].address), sis[1],
+                   _vp(out.address), so, n, stream)
+        else:
+            L.call("hpxhip_transform_binary", ins[0].dtype, cdt, out.dtype, fn.kind, L.scalars_buf(cdt, fn.scalars),
+                   _vp(ins[0].address), _vp(ins[1].address), _vp(out.address), n, stream)
     return _finish(is_task, stream, tgt, lambda: None)
 
 

@@ -167,6 +167,29 @@ int launch_binary(const TI* a, const TI* b, TO* out, uint64_t n, F f, hipStream_
     return 0;
 }
 
+// Strided pointer inductions: grid-stride loop, one element per thread per
+// trip.  Strided accesses cannot be vectorised; at |stride| = 1 the entry
+// points below use the contiguous kernels instead.
+template <typename TI, typename C, typename TO, typename F>
+__global__ __launch_bounds__(kThreads) void k_unary_strided(const TI* in, int64_t si, TO* out, int64_t so, uint64_t n,
+                                                            F f) {
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * kThreads;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += step) {
+        const int64_t k = static_cast<int64_t>(i);
+        out[k * so] = static_cast<TO>(f(static_cast<C>(in[k * si])));
+    }
+}
+
+template <typename TI, typename C, typename TO, typename F>
+__global__ __launch_bounds__(kThreads) void k_binary_strided(const TI* a, int64_t sa, const TI* b, int64_t sb,
+                                                             TO* out, int64_t so, uint64_t n, F f) {
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * kThreads;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += step) {
+        const int64_t k = static_cast<int64_t>(i);
+        out[k * so] = static_cast<TO>(f(static_cast<C>(a[k * sa]), static_cast<C>(b[k * sb])));
+    }
+}
+
 // (in, compute, out) combinations that are built: compute == in or F64;
 // out == in or == compute.
 template <typename TI, typename F>
@@ -330,6 +353,59 @@ int hpxhip_transform_binary(int in_dtype, int compute_dtype, int out_dtype, int 
             return with_binary<C>(binary_kind, scalars, [&](auto f) -> int {
                 return launch_binary<TI, C, TO>(static_cast<const TI*>(in1), static_cast<const TI*>(in2),
                                                 static_cast<TO*>(out), n, f, s);
+            });
+        });
+    });
+}
+
+int hpxhip_transform_strided(int in_dtype, int compute_dtype, int out_dtype, int unary_kind, const void* scalars,
+                             const void* in, int64_t in_stride, void* out, int64_t out_stride, uint64_t n,
+                             hpxhip_stream stream) {
+    if (n == 0) return 0;
+    if (!in || !out || (out_stride == 0 && n > 1)) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    if (in_stride == 1 && out_stride == 1)
+        return hpxhip_transform(in_dtype, compute_dtype, out_dtype, unary_kind, scalars, in, out, n, stream);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    return with_dtype(in_dtype, [&](auto ti) -> int {
+        using TI = typename decltype(ti)::type;
+        return with_compute_out<TI>(compute_dtype, out_dtype, [&](auto ct, auto ot) -> int {
+            using C = typename decltype(ct)::type;
+            using TO = typename decltype(ot)::type;
+            return with_unary<C>(unary_kind, scalars, [&](auto f) -> int {
+                hipLaunchKernelGGL((k_unary_strided<TI, C, TO, decltype(f)>), dim3(grid_for(n)), dim3(kThreads), 0, s,
+                                   static_cast<const TI*>(in), in_stride, static_cast<TO*>(out), out_stride, n, f);
+                HPXHIP_CHECK_LAUNCH();
+                return 0;
+            });
+        });
+    });
+}
+
+int hpxhip_transform_binary_strided(int in_dtype, int compute_dtype, int out_dtype, int binary_kind,
+                                    const void* scalars, const void* in1, int64_t in1_stride, const void* in2,
+                                    int64_t in2_stride, void* out, int64_t out_stride, uint64_t n,
+                                    hpxhip_stream stream) {
+    if (n == 0) return 0;
+    if (!in1 || !in2 || !out || (out_stride == 0 && n > 1)) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    if (in1_stride == 1 && in2_stride == 1 && out_stride == 1)
+        return hpxhip_transform_binary(in_dtype, compute_dtype, out_dtype, binary_kind, scalars, in1, in2, out, n,
+                                       stream);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    return with_dtype(in_dtype, [&](auto ti) -> int {
+        using TI = typename decltype(ti)::type;
+        return with_compute_out<TI>(compute_dtype, out_dtype, [&](auto ct, auto ot) -> int {
+            using C = typename decltype(ct)::type;
+            using TO = typename decltype(ot)::type;
+            return with_binary<C>(binary_kind, scalars, [&](auto f) -> int {
+                hipLaunchKernelGGL((k_binary_strided<TI, C, TO, decltype(f)>), dim3(grid_for(n)), dim3(kThreads), 0,
+                                   s, static_cast<const TI*>(in1), in1_stride, static_cast<const TI*>(in2), in2_stride,
+                                   static_cast<TO*>(out), out_stride, n, f);
+                HPXHIP_CHECK_LAUNCH();
+                return 0;
             });
         });
     });

@@ -235,6 +235,20 @@ int hpxhip_transform(int in_dtype, int compute_dtype, int out_dtype, int unary_k
 int hpxhip_transform_binary(int in_dtype, int compute_dtype, int out_dtype, int binary_kind,
                             const void* scalars, const void* in1, const void* in2, void* out,
                             uint64_t n, hpxhip_stream stream);
+/* for_loop_n with strided pointer inductions (for_loop_induction.hpp:210-219:
+ * value at iteration i = base + stride * i):
+ *   out[i*out_stride] = (out_t) f((compute_t) in[i*in_stride])              (unary)
+ *   out[i*out_stride] = (out_t) f((compute_t) in1[i*s1], (compute_t) in2[i*s2]) (binary)
+ * Strides are in elements and may be negative; an input stride may be 0.  An
+ * output stride of 0 with n > 1 is HPXHIP_ERROR_INVALID_ARGUMENT (every
+ * iteration would write one element). */
+int hpxhip_transform_strided(int in_dtype, int compute_dtype, int out_dtype, int unary_kind,
+                             const void* scalars, const void* in, int64_t in_stride, void* out,
+                             int64_t out_stride, uint64_t n, hpxhip_stream stream);
+int hpxhip_transform_binary_strided(int in_dtype, int compute_dtype, int out_dtype, int binary_kind,
+                                    const void* scalars, const void* in1, int64_t in1_stride,
+                                    const void* in2, int64_t in2_stride, void* out,
+                                    int64_t out_stride, uint64_t n, hpxhip_stream stream);
 
 /* --------------------------------------------------------- reductions */
 /* transform_reduce.hpp:254: *out_dev = init (op) conv(in[0]) (op) ... (op) conv(in[n-1]),

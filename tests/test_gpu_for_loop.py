@@ -159,3 +159,46 @@ def test_for_loop_reduction_argument_checks(gpu_target):
     with pytest.raises(TypeError):
         P.for_loop_n(pol, d.begin(), 16, P.reduction_plus(s), P.reduction_plus(s),
                      F.accumulate(1, F.identity(), 0))
+
+
+# ---------------------------------------------- strided pointer inductions
+# for_loop_induction.hpp:210-219: induction(it, stride) has the value
+# it + stride * i at iteration i (for_loop_induction.cpp's stride-2 cases).
+@pytest.mark.parametrize("dtype", [np.int32, np.int64, np.float64])
+def test_for_loop_strided_inductions(gpu_target, dtype):
+    n = 10007
+    rng = np.random.default_rng(7)
+    a = rng.integers(-1000, 1000, 3 * n).astype(dtype)
+    b = rng.integers(-1000, 1000, 2 * n).astype(dtype)
+    da, db = hpx.vector.from_host(a, gpu_target), hpx.vector.from_host(b, gpu_target)
+    dc = hpx.vector.from_host(np.zeros(2 * n, dtype), gpu_target)
+    pol = ex.par.on(hpx.default_executor(gpu_target))
+    # unary: c[2i] = a[3i] + 5 (loop variable over the first n of b, unused)
+    P.for_loop_n(pol, db.begin(), n, P.induction(da.begin(), 3), P.induction(dc.begin(), 2),
+                 F.assign(2, F.add_value(5), 1))
+    ref = np.zeros(2 * n, dtype)
+    ref[0::2] = a[0::3] + dtype(5)
+    np.testing.assert_array_equal(dc.to_host(), ref)
+    # binary, negative stride on one input: c[i] = b[i] + 3*a[3n-1-i] ... via triad(b, a_rev)
+    dd = hpx.vector.from_host(np.zeros(n, dtype), gpu_target)
+    P.for_loop_n(pol, dd.begin(), n, P.induction(db.begin()), P.induction(da.begin() + (3 * n - 1), -1),
+                 F.assign(0, F.add_step(), 1, 2))
+    np.testing.assert_array_equal(dd.to_host(), b[:n] + a[::-1][:n])
+    # task form, stride 0 on an input (broadcast of a[0])
+    de = hpx.vector.from_host(np.zeros(n, dtype), gpu_target)
+    f = P.for_loop_n(ex.par(ex.task).on(hpx.default_executor(gpu_target)), de.begin(), n,
+                     P.induction(da.begin(), 0), F.assign(0, F.add_value(1), 1))
+    f.get()
+    np.testing.assert_array_equal(de.to_host(), np.full(n, a[0] + dtype(1), dtype))
+
+
+def test_for_loop_strided_bounds(gpu_target):
+    d = hpx.vector(100, dtype=np.int64, tgt=gpu_target)
+    pol = ex.par.on(hpx.default_executor(gpu_target))
+    with pytest.raises(ValueError):   # 10 + 10*9 = 100 is one past the end
+        P.for_loop_n(pol, d.begin(), 10, P.induction(d.begin() + 10, 10), F.assign(0, F.add_value(1), 1))
+    with pytest.raises(ValueError):   # walks below the start
+        P.for_loop_n(pol, d.begin(), 10, P.induction(d.begin() + 5, -1), F.assign(0, F.add_value(1), 1))
+    with pytest.raises(ValueError):   # every iteration writes one element
+        P.for_loop_n(pol, d.begin(), 10, P.induction(d.begin(), 0), F.assign(1, F.add_value(1), 0))
+    P.for_loop_n(pol, d.begin(), 10, P.induction(d.begin() + 9, 10), F.assign(0, F.add_value(1), 1))
