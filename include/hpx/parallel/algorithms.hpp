@@ -34,6 +34,7 @@
 #include <hpx/parallel/execution.hpp>
 
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <iterator>
 #include <type_traits>
@@ -536,16 +537,23 @@ It loop_var(It it) { return it; }
 template <typename T, typename Op>
 reduction_helper<T, Op> const& loop_var(reduction_helper<T, Op> const& r) { return r; }
 template <typename It>
-It loop_var(induction_stride_helper<It> const& h) {
-    if (h.stride_ != 1)
-        throw hpx::exception(HPXHIP_ERROR_UNSUPPORTED,
-                             "for_loop_n: pointer inductions with stride != 1 are not supported by the contiguous "
-                             "elementwise kernels");
-    return h.var_;
-}
-template <typename P, typename Vars, std::size_t Red, typename F, std::size_t... In>
-result_t<P, void> for_loop_body(P&& p, Vars const& v, uint64_t n,
+It loop_var(induction_stride_helper<It> const& h) { return h.var_; }
+// the stride of each loop variable (for_loop_induction.hpp:210-219)
+template <typename It>
+int64_t loop_stride(It const&) { return 1; }
+template <typename It>
+int64_t loop_stride(induction_stride_helper<It> const& h) { return static_cast<int64_t>(h.stride_); }
+template <typename T, typename Op>
+int64_t loop_stride(reduction_helper<T, Op> const&) { return 1; }
+template <std::size_t N>
+using strides_t = std::array<int64_t, N>;
+template <typename P, typename Vars, std::size_t N, std::size_t Red, typename F, std::size_t... In>
+result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n,
                                 compute::hip::functional::loop_accumulate<Red, F, In...> const& b) {
+    if (((st[In] != 1) || ...))
+        throw hpx::exception(HPXHIP_ERROR_UNSUPPORTED,
+                             "for_loop_n: a reduction loop reads its inductions with stride 1 (the transform_reduce "
+                             "kernels are contiguous)");
     auto const& red = std::get<Red>(v);
     using T = std::decay_t<decltype(red.identity_)>;
     using Op = std::decay_t<decltype(red.op_)>;
@@ -582,8 +590,9 @@ result_t<P, void> for_loop_body(P&& p, Vars const& v, uint64_t n,
         *var = op(*var, view);
     });
 }
-template <typename P, typename Vars, std::size_t Out, typename F, std::size_t In0>
-result_t<P, void> for_loop_body(P&& p, Vars const& v, uint64_t n, compute::hip::functional::loop_assign<Out, F, In0> const& b) {
+template <typename P, typename Vars, std::size_t N, std::size_t Out, typename F, std::size_t In0>
+result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n,
+                                compute::hip::functional::loop_assign<Out, F, In0> const& b) {
     auto in = std::get<In0>(v);
     auto out = std::get<Out>(v);
     using TI = value_t<decltype(in)>;
@@ -593,12 +602,13 @@ result_t<P, void> for_loop_body(P&& p, Vars const& v, uint64_t n, compute::hip::
     auto const& t = target_of(p, in);
     C s[2] = {};
     Tr::scalars(b.f, s);
-    check(hpxhip_transform(dt<TI>, dt<C>, dt<TO>, Tr::kind, s, in.device_ptr(), out.device_ptr(), n, t.stream()),
+    check(hpxhip_transform_strided(dt<TI>, dt<C>, dt<TO>, Tr::kind, s, in.device_ptr(), st[In0], out.device_ptr(),
+                                   st[Out], n, t.stream()),
           "for_loop_n");
     return finish<void>(p, t, [] {});
 }
-template <typename P, typename Vars, std::size_t Out, typename F, std::size_t In0, std::size_t In1>
-result_t<P, void> for_loop_body(P&& p, Vars const& v, uint64_t n,
+template <typename P, typename Vars, std::size_t N, std::size_t Out, typename F, std::size_t In0, std::size_t In1>
+result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n,
                                 compute::hip::functional::loop_assign<Out, F, In0, In1> const& b) {
     auto in0 = std::get<In0>(v);
     auto in1 = std::get<In1>(v);
@@ -611,8 +621,8 @@ result_t<P, void> for_loop_body(P&& p, Vars const& v, uint64_t n,
     auto const& t = target_of(p, in0);
     C s[2] = {};
     Tr::scalars(b.f, s);
-    check(hpxhip_transform_binary(dt<TI>, dt<C>, dt<TO>, Tr::kind, s, in0.device_ptr(), in1.device_ptr(),
-                                  out.device_ptr(), n, t.stream()),
+    check(hpxhip_transform_binary_strided(dt<TI>, dt<C>, dt<TO>, Tr::kind, s, in0.device_ptr(), st[In0],
+                                          in1.device_ptr(), st[In1], out.device_ptr(), st[Out], n, t.stream()),
           "for_loop_n");
     return finish<void>(p, t, [] {});
 }
@@ -620,7 +630,8 @@ template <typename P, typename It, typename Tuple, std::size_t... I>
 auto for_loop_dispatch(P&& p, It first, uint64_t n, Tuple&& args, std::index_sequence<I...>) {
     constexpr std::size_t last = std::tuple_size<std::decay_t<Tuple>>::value - 1;
     auto vars = std::make_tuple(first, loop_var(std::get<I>(args))...);
-    return for_loop_body(std::forward<P>(p), vars, n, std::get<last>(args));
+    strides_t<sizeof...(I) + 1> st{1, loop_stride(std::get<I>(args))...};
+    return for_loop_body(std::forward<P>(p), vars, st, n, std::get<last>(args));
 }
 }  // namespace detail
 
