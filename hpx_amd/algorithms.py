@@ -18,7 +18,8 @@ calls one whole-algorithm entry point of the C ABI (include/hpxhip.h):
   transform_exclusive_scan   transform_exclusive_scan.hpp:317
   sort / sort_by_key         sort.hpp:364, sort_by_key.hpp:42-78
   generate (splitmix/iota)   generate.hpp (device generator functors)
-  for_loop / for_loop_n      for_loop.hpp:808 (inductions: for_loop_induction.hpp;
+  for_loop / for_loop_n      for_loop.hpp:808; for_loop_strided 604,
+  for_loop_n_strided         1014 (inductions: for_loop_induction.hpp;
                              reductions: for_loop_reduction.hpp:35-231)
 
 A policy must be rebound to a hip executor (``par.on(hip_exec)``) or all
@@ -497,6 +498,31 @@ def _for_loop_reduce(pol, n, vars_, red, body):
 
 
 def for_loop_n(pol, first, count, *args):
+    return _for_loop(pol, first, 1, count, *args)
+
+
+def for_loop_strided(pol, first, last, stride, *args):
+    """for_loop.hpp:604 for_loop_strided(policy, first, last, stride, args..., f):
+    the loop variable visits first, first + stride, ... while it precedes
+    last (follows it for a negative stride); inductions take their ordinal
+    value (base + induction stride * k at the k-th application)."""
+    stride = int(stride)
+    if stride == 0:
+        raise ValueError("for_loop_strided: stride must not be 0")
+    n = _check_range(first, last) if stride > 0 else _check_range(last, first)
+    count = (n + abs(stride) - 1) // abs(stride)
+    return _for_loop(pol, first, stride, count, *args)
+
+
+def for_loop_n_strided(pol, first, count, stride, *args):
+    """for_loop.hpp:1014 for_loop_n_strided(policy, first, size, stride, args..., f)."""
+    stride = int(stride)
+    if stride == 0:
+        raise ValueError("for_loop_n_strided: stride must not be 0")
+    return _for_loop(pol, first, stride, count, *args)
+
+
+def _for_loop(pol, first, first_stride, count, *args):
     """for_loop.hpp:808 for_loop_n(policy, first, size, inductions..., f) as
     for_loop_compute.cu uses it: the loop iterator and pointer inductions
     walk device ranges in lock step (induction i's value at iteration k is
@@ -510,6 +536,8 @@ def for_loop_n(pol, first, count, *args):
         raise TypeError("for_loop_n: missing loop body")
     *inds, body = args
     reds = [a for a in inds if isinstance(a, reduction)]
+    if reds and first_stride != 1:
+        raise ValueError("for_loop_n: a reduction loop walks its loop variable with stride 1")
     if reds:
         if len(reds) > 1:
             raise TypeError("for_loop_n: one reduction per loop is carried by the C ABI")
@@ -540,7 +568,7 @@ def for_loop_n(pol, first, count, *args):
     if n < 0:
         raise ValueError("for_loop_n: negative count")
     vars_ = [first] + [ind.value for ind in inds]
-    strides = [1] + [ind.stride for ind in inds]
+    strides = [first_stride] + [ind.stride for ind in inds]
     try:
         out, so = vars_[body.out], strides[body.out]
         ins = [vars_[i] for i in body.ins]

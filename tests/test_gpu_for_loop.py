@@ -202,3 +202,37 @@ def test_for_loop_strided_bounds(gpu_target):
     with pytest.raises(ValueError):   # every iteration writes one element
         P.for_loop_n(pol, d.begin(), 10, P.induction(d.begin(), 0), F.assign(1, F.add_value(1), 0))
     P.for_loop_n(pol, d.begin(), 10, P.induction(d.begin() + 9, 10), F.assign(0, F.add_value(1), 1))
+
+
+# tests/unit/parallel/algorithms/for_loop_strided.cpp:29-74 restated: 10007
+# size_t iotas (42 replaced by 43), every stride-th element set to 42.
+@pytest.mark.parametrize("stride", [1, 2, 7, 100, 10007, 20000])
+def test_for_loop_strided(gpu_target, stride):
+    c = np.arange(1000, 1000 + 10007, dtype=np.uint64)
+    d = hpx.vector.from_host(c, gpu_target)
+    pol = ex.par.on(hpx.default_executor(gpu_target))
+    P.for_loop_strided(pol, d.begin(), d.end(), stride, F.assign(0, F.affine(0, 42), 0))
+    got = d.to_host()
+    idx = np.arange(c.size)
+    assert np.all(got[idx % stride == 0] == 42) and np.all(got[idx % stride != 0] != 42)
+
+
+def test_for_loop_strided_negative_and_inductions(gpu_target):
+    n = 1000
+    a = np.arange(n, dtype=np.int64)
+    da = hpx.vector.from_host(a, gpu_target)
+    dout = hpx.vector.from_host(np.zeros(n, np.int64), gpu_target)
+    pol = ex.par(ex.task).on(hpx.default_executor(gpu_target))
+    # loop variable walks a backwards by 3 from the end; induction of out walks forward (ordinal)
+    f = P.for_loop_strided(pol, da.begin() + (n - 1), da.begin() - 0, -3, P.induction(dout.begin()),
+                           F.assign(1, F.add_value(1), 0))
+    f.get()
+    k = (n - 1 + 2) // 3
+    ref = np.zeros(n, np.int64)
+    ref[:k] = a[n - 1::-3][:k] + 1
+    np.testing.assert_array_equal(dout.to_host(), ref)
+    P.for_loop_n_strided(ex.par.on(hpx.default_executor(gpu_target)), dout.begin(), 5, 2,
+                         F.assign(0, F.affine(0, 7), 0))
+    assert list(dout.to_host()[:10:2]) == [7] * 5
+    with pytest.raises(ValueError):
+        P.for_loop_strided(pol, da.begin(), da.end(), 0, F.assign(0, F.add_value(1), 0))
