@@ -627,10 +627,10 @@ result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, ui
     return finish<void>(p, t, [] {});
 }
 template <typename P, typename It, typename Tuple, std::size_t... I>
-auto for_loop_dispatch(P&& p, It first, uint64_t n, Tuple&& args, std::index_sequence<I...>) {
+auto for_loop_dispatch(P&& p, It first, int64_t first_stride, uint64_t n, Tuple&& args, std::index_sequence<I...>) {
     constexpr std::size_t last = std::tuple_size<std::decay_t<Tuple>>::value - 1;
     auto vars = std::make_tuple(first, loop_var(std::get<I>(args))...);
-    strides_t<sizeof...(I) + 1> st{1, loop_stride(std::get<I>(args))...};
+    strides_t<sizeof...(I) + 1> st{first_stride, loop_stride(std::get<I>(args))...};
     return for_loop_body(std::forward<P>(p), vars, st, n, std::get<last>(args));
 }
 }  // namespace detail
@@ -642,12 +642,35 @@ detail::result_t<P, void> for_loop_n(P&& p, It first, Size count, Args&&... args
     static_assert(sizeof...(Args) >= 1, "for_loop_n: missing loop body");
     static_assert(detail::is_dev<It>, "for_loop_n: the loop variable must be a device iterator");
     uint64_t n = count > 0 ? static_cast<uint64_t>(count) : 0;
-    return detail::for_loop_dispatch(std::forward<P>(p), first, n, std::forward_as_tuple(args...),
+    return detail::for_loop_dispatch(std::forward<P>(p), first, 1, n, std::forward_as_tuple(args...),
                                      std::make_index_sequence<sizeof...(Args) - 1>{});
 }
 template <typename P, typename It, typename... Args>
 detail::result_t<P, void> for_loop(P&& p, It first, It last, Args&&... args) {
     return for_loop_n(std::forward<P>(p), first, detail::distance(first, last), std::forward<Args>(args)...);
+}
+
+// for_loop.hpp:1014 for_loop_n_strided(policy, first, size, stride, args..., f):
+// the loop variable advances by `stride` per application, inductions by
+// their own stride per application (ordinal position).
+template <typename P, typename It, typename Size, typename S, typename... Args>
+detail::result_t<P, void> for_loop_n_strided(P&& p, It first, Size count, S stride, Args&&... args) {
+    static_assert(sizeof...(Args) >= 1, "for_loop_n_strided: missing loop body");
+    static_assert(detail::is_dev<It>, "for_loop_n_strided: the loop variable must be a device iterator");
+    if (stride == 0) throw hpx::exception(HPXHIP_ERROR_INVALID_ARGUMENT, "for_loop_n_strided: zero stride");
+    uint64_t n = count > 0 ? static_cast<uint64_t>(count) : 0;
+    return detail::for_loop_dispatch(std::forward<P>(p), first, static_cast<int64_t>(stride), n,
+                                     std::forward_as_tuple(args...), std::make_index_sequence<sizeof...(Args) - 1>{});
+}
+// for_loop.hpp:604 for_loop_strided(policy, first, last, stride, args..., f):
+// first, first + stride, ... while before last (after it for stride < 0).
+template <typename P, typename It, typename S, typename... Args>
+detail::result_t<P, void> for_loop_strided(P&& p, It first, It last, S stride, Args&&... args) {
+    if (stride == 0) throw hpx::exception(HPXHIP_ERROR_INVALID_ARGUMENT, "for_loop_strided: zero stride");
+    const int64_t st = static_cast<int64_t>(stride);
+    const uint64_t len = st > 0 ? detail::distance(first, last) : detail::distance(last, first);
+    const uint64_t a = static_cast<uint64_t>(st > 0 ? st : -st);
+    return for_loop_n_strided(std::forward<P>(p), first, (len + a - 1) / a, stride, std::forward<Args>(args)...);
 }
 
 }  // namespace v1
@@ -665,6 +688,8 @@ using parallel::v1::for_each;
 using parallel::v1::for_each_n;
 using parallel::v1::for_loop;
 using parallel::v1::for_loop_n;
+using parallel::v1::for_loop_n_strided;
+using parallel::v1::for_loop_strided;
 using parallel::v1::induction;
 using parallel::v1::reduction;
 using parallel::v1::reduction_bit_and;

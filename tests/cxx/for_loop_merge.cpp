@@ -118,6 +118,27 @@ void test_for_loop_reduction(std::mt19937& gen) {
     HPX_TEST_EQ(ip, std::inner_product(c.begin(), c.end(), e.begin(), T(5)));
 }
 
+// for_loop_strided.cpp:29-74 restated: every stride-th element set to 42.
+void test_for_loop_strided(std::mt19937& gen) {
+    using T = std::uint64_t;
+    std::vector<T> c(10007);
+    std::iota(c.begin(), c.end(), T(1000));
+    hip::target t;
+    hip::allocator<T> alloc(t);
+    hip::default_executor exec(t);
+    for (int stride : {1, 2, 7, int(gen() % 100) + 1, 10007, 20000}) {
+        dvec<T> d(c.size(), alloc);
+        hpx::parallel::copy(ex::par, c.begin(), c.end(), d.begin());
+        fn::loop_assign<0, fn::affine<T>, 0> set42{{T(0), T(42)}};
+        hpx::parallel::for_loop_strided(ex::par.on(exec), d.begin(), d.end(), stride, set42);
+        std::vector<T> h = to_host(d);
+        for (std::size_t i = 0; i != h.size(); ++i) {
+            if (i % stride == 0) HPX_TEST_EQ(h[i], T(42));
+            else HPX_TEST_NEQ(h[i], T(42));
+        }
+    }
+}
+
 template <typename T, typename Comp>
 void test_merge(std::mt19937& gen, std::size_t n1, std::size_t n2, Comp comp) {
     std::uniform_int_distribution<int> dis(0, 50);
@@ -147,6 +168,7 @@ int hpx_main(int, char**) {
     std::mt19937 gen(42);
     for (int n : {100, 1, 4097, 1 << 20}) test_for_loop(gen, n);
     test_for_loop_reduction(gen);
+    test_for_loop_strided(gen);
     test_merge<int64_t>(gen, 10007, 5003, std::less<int64_t>());
     test_merge<uint32_t>(gen, 1 << 20, (1 << 19) + 3, std::greater<uint32_t>());
     test_merge<double>(gen, 4096, 0, std::less<double>());
