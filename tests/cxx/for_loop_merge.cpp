@@ -91,6 +91,7 @@ void test_for_loop_reduction(std::mt19937& gen) {
     hpx::future<void> f = hpx::parallel::for_loop(ex::par(ex::task).on(exec), d.begin(), d.end(),
                                                   hpx::parallel::reduction_multiplies(prod), body);
     f.get();
+    t.synchronize();  // the completion host function has returned before the target can go away
     HPX_TEST_EQ(prod, std::accumulate(c.begin(), c.end(), T(1), std::multiplies<T>()));
 
     std::shuffle(c.begin(), c.end(), gen);
@@ -116,6 +117,7 @@ void test_for_loop_reduction(std::mt19937& gen) {
     hpx::parallel::for_loop_n(ex::par.on(exec), d.begin(), c.size(), hpx::parallel::induction(de.begin()),
                               hpx::parallel::reduction_plus(ip), dot);
     HPX_TEST_EQ(ip, std::inner_product(c.begin(), c.end(), e.begin(), T(5)));
+    t.synchronize();
 }
 
 // for_loop_strided.cpp:29-74 restated: every stride-th element set to 42.
