@@ -198,7 +198,12 @@ class target {
         void* host_slots = nullptr;
         unsigned next_slot = 0;
         ~handle() {
-            if (stream) hpxhip_stream_destroy(stream);
+            // drain first: queued kernels may still write the result slots and
+            // a completion host function may still be reading them
+            if (stream) {
+                hpxhip_stream_synchronize(stream);
+                hpxhip_stream_destroy(stream);
+            }
             if (dev_slots) hpxhip_free(dev_slots);
             if (host_slots) hpxhip_free_host(host_slots);
         }

@@ -59,86 +59,6 @@ void test_for_loop(std::mt19937& gen, int N) {
     std::vector<int> h_D = to_host(d_D);
     for (int i = 0; i < N; ++i) HPX_TEST_EQ(h_D[i], h_A[i] + 5);
 
-    // strided induction (for_loop_induction.hpp:210-219): *C = *A + 3.0 * B[2i]
-    if (N >= 2) {
-        int M = N / 2;
-        dvec<int> d_E(M, allocA);
-        hpx::parallel::for_loop_n(ex::par.on(exec), d_A.begin(), M, hpx::parallel::induction(d_B.begin(), 2),
-                                  hpx::parallel::induction(d_E.begin()), body);
-        std::vector<int> h_E = to_host(d_E);
-        for (int i = 0; i < M; ++i) HPX_TEST_EQ(h_E[i], static_cast<int>(h_A[i] + 3.0 * h_B[2 * i]));
-    }
-}
-
-// for_loop_reduction.cpp:20-140 restated over device iterators: 10007 size_t
-// iotas from a random start, `r op= *it`, checked against std::accumulate.
-void test_for_loop_reduction(std::mt19937& gen) {
-    using T = std::uint64_t;
-    std::vector<T> c(10007);
-    std::iota(c.begin(), c.end(), T(gen()));
-    hip::target t;
-    hip::allocator<T> alloc(t);
-    dvec<T> d(c.size(), alloc);
-    hpx::parallel::copy(ex::par, c.begin(), c.end(), d.begin());
-    hip::default_executor exec(t);
-    fn::loop_accumulate<1, fn::identity, 0> body{};
-
-    T sum = 0;
-    hpx::parallel::for_loop(ex::par.on(exec), d.begin(), d.end(), hpx::parallel::reduction_plus(sum), body);
-    HPX_TEST_EQ(sum, std::accumulate(c.begin(), c.end(), T(0)));
-
-    T prod = 1;
-    hpx::future<void> f = hpx::parallel::for_loop(ex::par(ex::task).on(exec), d.begin(), d.end(),
-                                                  hpx::parallel::reduction_multiplies(prod), body);
-    f.get();
-    t.synchronize();  // the completion host function has returned before the target can go away
-    HPX_TEST_EQ(prod, std::accumulate(c.begin(), c.end(), T(1), std::multiplies<T>()));
-
-    std::shuffle(c.begin(), c.end(), gen);
-    hpx::parallel::copy(ex::par, c.begin(), c.end(), d.begin());
-    T mn = c[0], mx = c[0];
-    hpx::parallel::for_loop_n(ex::par.on(exec), d.begin(), c.size(), hpx::parallel::reduction_min(mn), body);
-    hpx::parallel::for_loop_n(ex::par.on(exec), d.begin(), c.size(), hpx::parallel::reduction_max(mx), body);
-    HPX_TEST_EQ(mn, *std::min_element(c.begin(), c.end()));
-    HPX_TEST_EQ(mx, *std::max_element(c.begin(), c.end()));
-
-    T x = 0;
-    hpx::parallel::for_loop_n(ex::par.on(exec), d.begin(), c.size(), hpx::parallel::reduction_bit_xor(x), body);
-    T xr = 0;
-    for (T v : c) xr ^= v;
-    HPX_TEST_EQ(x, xr);
-
-    // inner product: loop iterator and an induction feed a binary body
-    std::vector<T> e(c.size(), T(3));
-    dvec<T> de(e.size(), alloc);
-    hpx::parallel::copy(ex::par, e.begin(), e.end(), de.begin());
-    T ip = 5;
-    fn::loop_accumulate<2, fn::multiply, 0, 1> dot{};
-    hpx::parallel::for_loop_n(ex::par.on(exec), d.begin(), c.size(), hpx::parallel::induction(de.begin()),
-                              hpx::parallel::reduction_plus(ip), dot);
-    HPX_TEST_EQ(ip, std::inner_product(c.begin(), c.end(), e.begin(), T(5)));
-    t.synchronize();
-}
-
-// for_loop_strided.cpp:29-74 restated: every stride-th element set to 42.
-void test_for_loop_strided(std::mt19937& gen) {
-    using T = std::uint64_t;
-    std::vector<T> c(10007);
-    std::iota(c.begin(), c.end(), T(1000));
-    hip::target t;
-    hip::allocator<T> alloc(t);
-    hip::default_executor exec(t);
-    for (int stride : {1, 2, 7, int(gen() % 100) + 1, 10007, 20000}) {
-        dvec<T> d(c.size(), alloc);
-        hpx::parallel::copy(ex::par, c.begin(), c.end(), d.begin());
-        fn::loop_assign<0, fn::affine<T>, 0> set42{{T(0), T(42)}};
-        hpx::parallel::for_loop_strided(ex::par.on(exec), d.begin(), d.end(), stride, set42);
-        std::vector<T> h = to_host(d);
-        for (std::size_t i = 0; i != h.size(); ++i) {
-            if (i % stride == 0) HPX_TEST_EQ(h[i], T(42));
-            else HPX_TEST_NEQ(h[i], T(42));
-        }
-    }
 }
 
 template <typename T, typename Comp>
@@ -169,8 +89,6 @@ void test_merge(std::mt19937& gen, std::size_t n1, std::size_t n2, Comp comp) {
 int hpx_main(int, char**) {
     std::mt19937 gen(42);
     for (int n : {100, 1, 4097, 1 << 20}) test_for_loop(gen, n);
-    test_for_loop_reduction(gen);
-    test_for_loop_strided(gen);
     test_merge<int64_t>(gen, 10007, 5003, std::less<int64_t>());
     test_merge<uint32_t>(gen, 1 << 20, (1 << 19) + 3, std::greater<uint32_t>());
     test_merge<double>(gen, 4096, 0, std::less<double>());
