@@ -44,11 +44,20 @@ $(ORACLE): oracle/oracle.cpp oracle/oracle.h
 	@mkdir -p $(dir $@)
 	$(CXX) $(OFLAGS) -shared -o $@ oracle/oracle.cpp
 
-cxxtests: $(CXXTBIN)
+# ... and the hipcc-compiled ones (device closures, HPX_HOST_DEVICE lambdas)
+HIPT     := device_closures
+HIPTBIN  := $(HIPT:%=tests/cxx/bin/%)
+HTFLAGS  := -O2 -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-parameter -Iinclude
+
+cxxtests: $(CXXTBIN) $(HIPTBIN)
 
 tests/cxx/bin/%: tests/cxx/%.cpp $(CXXHDR) $(LIB)
 	@mkdir -p $(dir $@)
 	$(CXX) $(TFLAGS) $< -o $@ $(TLINK)
+
+tests/cxx/bin/%: tests/cxx/%.hip $(CXXHDR) $(LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HTFLAGS) $< -o $@ $(TLINK)
 
 clean:
 	rm -rf $(BUILD) $(LIB) oracle/_build tests/cxx/bin

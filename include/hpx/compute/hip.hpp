@@ -5,7 +5,7 @@
 //                                           src/compute/cuda/cuda_target.cpp:97-317
 //   hpx::compute::hip::get_local_targets <- src/compute/cuda/get_cuda_targets.cpp:30-65
 //   hpx::compute::hip::allocator<T>      <- hpx/compute/cuda/allocator.hpp:36-259
-//   hpx::compute::hip::default_executor  <- hpx/compute/cuda/default_executor.hpp:42-260
+//   (executors: <hpx/compute/hip/default_executor.hpp>, concurrent_executor.hpp)
 //   hpx::compute::vector<T, Alloc>       <- hpx/compute/vector.hpp:28-372
 //   device iterator + value_proxy        <- hpx/compute/detail/iterator.hpp:23-85,
 //                                           cuda/value_proxy.hpp:25-124
@@ -18,6 +18,7 @@
 
 #include <hpxhip.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
@@ -73,6 +74,10 @@ struct shared_state {
     std::condition_variable cv;
     bool ready = false;
     std::exception_ptr exc;
+    // Result bytes of a device computation, copied out of the pinned result
+    // slot by the completion callback itself: the state owns what get() reads,
+    // nothing is borrowed from the target that launched the work.
+    alignas(16) unsigned char raw[64] = {};
     std::function<T()> value_fn;  // run once the device work is done
     typename std::conditional<std::is_void<T>::value, int, T>::type value{};
     std::vector<std::function<void()>> continuations;
@@ -171,20 +176,169 @@ inline future<void> make_ready_future() {
     return future<void>(st);
 }
 
-// when_all over a vector of futures: ready when all are (values via get()).
+// when_all over a vector of futures (hpx/lcos/when_all.hpp): ready once every
+// input is ready (counted down by continuations on the inputs' completions);
+// get() returns the input futures, whose values are then read with get().
 template <typename T>
 future<std::vector<future<T>>> when_all(std::vector<future<T>>&& fs) {
-    auto st = std::make_shared<lcos::detail::shared_state<std::vector<future<T>>>>();
+    using S = lcos::detail::shared_state<std::vector<future<T>>>;
+    auto st = std::make_shared<S>();
     auto v = std::make_shared<std::vector<future<T>>>(std::move(fs));
-    st->value_fn = [v]() {
-        for (auto& f : *v) f.wait();
-        return std::move(*v);
+    st->value_fn = [v]() { return std::move(*v); };
+    auto pending = std::make_shared<std::atomic<std::size_t>>(v->size() + 1);
+    auto count_down = [st, pending] {
+        if (pending->fetch_sub(1) == 1) st->set_ready(0);
     };
-    st->set_ready(0);
+    for (auto& f : *v) {
+        auto const& in = f.shared();
+        std::unique_lock<std::mutex> lk(in->mtx);
+        if (in->ready) {
+            lk.unlock();
+            count_down();
+        } else {
+            in->continuations.push_back(count_down);
+        }
+    }
+    count_down();
     return future<std::vector<future<T>>>(st);
 }
 
 namespace compute { namespace hip {
+
+namespace detail {
+// Per-device resources shared by every target copy of a process: the pinned
+// result slots through which reduce / copy_if / for_loop results travel back,
+// and a pool of non-blocking streams.  Both outlive any one target, so a
+// future never depends on the lifetime of the (often temporary) policy,
+// executor or target that launched its work -- the role the intrusive
+// refcount pinned across the stream callback plays in the reference
+// (cuda_target.cpp:123-142).  Pools live for the whole process (never freed:
+// a completion callback may still run during static destruction).
+class device_pool {
+public:
+    static constexpr unsigned kChunkSlots = 256, kSlotBytes = 64, kMaxIdleStreams = 32;
+
+    static device_pool& get(int device) {
+        static std::mutex m;
+        static std::vector<device_pool*>* pools = new std::vector<device_pool*>();
+        std::lock_guard<std::mutex> lk(m);
+        if (device < 0) throw hpx::exception(HPXHIP_ERROR_INVALID_ARGUMENT, "negative device id");
+        if (pools->size() <= static_cast<std::size_t>(device)) pools->resize(device + 1, nullptr);
+        if (!(*pools)[device]) (*pools)[device] = new device_pool(device);
+        return *(*pools)[device];
+    }
+
+    struct slot_ref {
+        unsigned id;
+        void* dev;
+        void* host;
+    };
+
+    slot_ref acquire() {
+        std::lock_guard<std::mutex> lk(mtx_);
+        if (free_.empty()) grow();
+        unsigned id = free_.back();
+        free_.pop_back();
+        auto const& c = chunks_[id / kChunkSlots];
+        std::size_t off = std::size_t(id % kChunkSlots) * kSlotBytes;
+        return {id, static_cast<char*>(c.first) + off, static_cast<char*>(c.second) + off};
+    }
+    // No HIP call: safe from a stream callback.
+    void release(unsigned id) {
+        std::lock_guard<std::mutex> lk(mtx_);
+        free_.push_back(id);
+    }
+
+    hpxhip_stream take_stream() {
+        {
+            std::lock_guard<std::mutex> lk(mtx_);
+            if (!streams_.empty()) {
+                hpxhip_stream s = streams_.back();
+                streams_.pop_back();
+                return s;
+            }
+        }
+        hpxhip_stream s = nullptr;
+        check(hpxhip_stream_create(device_, &s), "hpxhip_stream_create");
+        return s;
+    }
+    // A stream handed back may still have queued work: whoever takes it next
+    // is ordered behind that work, which is at least as strong as the
+    // reference's destroy-while-busy (cudaStreamDestroy returns at once).
+    void give_stream(hpxhip_stream s) {
+        {
+            std::lock_guard<std::mutex> lk(mtx_);
+            if (streams_.size() < kMaxIdleStreams) {
+                streams_.push_back(s);
+                return;
+            }
+        }
+        hpxhip_stream_destroy(s);
+    }
+
+private:
+    explicit device_pool(int device) : device_(device) {}
+    void grow() {  // called with mtx_ held
+        void* d = nullptr;
+        void* h = nullptr;
+        check(hpxhip_malloc(device_, &d, std::size_t(kChunkSlots) * kSlotBytes), "result slots");
+        int rc = hpxhip_malloc_host(&h, std::size_t(kChunkSlots) * kSlotBytes);
+        if (rc != HPXHIP_SUCCESS) {
+            hpxhip_free(d);
+            check(rc, "result slots");
+        }
+        unsigned base = static_cast<unsigned>(chunks_.size()) * kChunkSlots;
+        chunks_.emplace_back(d, h);
+        for (unsigned i = kChunkSlots; i-- > 0;) free_.push_back(base + i);
+    }
+
+    int device_;
+    std::mutex mtx_;
+    std::vector<std::pair<void*, void*>> chunks_;  // (device, pinned host) per chunk
+    std::vector<unsigned> free_;
+    std::vector<hpxhip_stream> streams_;
+};
+}  // namespace detail
+
+// One 64-byte (device, pinned host) result slot, returned to its device pool
+// when the owner goes away.  Algorithms queue `kernel -> D2H copy into host()`
+// and hand the slot to the completion (target::async_result), which copies
+// the bytes into the future's shared state before releasing it.
+class result_slot {
+    detail::device_pool* pool_ = nullptr;
+    detail::device_pool::slot_ref ref_{};
+
+public:
+    result_slot() = default;
+    result_slot(detail::device_pool& p) : pool_(&p), ref_(p.acquire()) {}
+    result_slot(result_slot&& o) noexcept : pool_(o.pool_), ref_(o.ref_) { o.pool_ = nullptr; }
+    result_slot& operator=(result_slot&& o) noexcept {
+        if (this != &o) {
+            reset();
+            pool_ = o.pool_;
+            ref_ = o.ref_;
+            o.pool_ = nullptr;
+        }
+        return *this;
+    }
+    result_slot(result_slot const&) = delete;
+    result_slot& operator=(result_slot const&) = delete;
+    ~result_slot() { reset(); }
+
+    explicit operator bool() const { return pool_ != nullptr; }
+    void* device() const { return ref_.dev; }
+    void const* host() const { return ref_.host; }
+    void reset() {
+        if (pool_) pool_->release(ref_.id);
+        pool_ = nullptr;
+    }
+    // ownership moves to a completion callback (released there)
+    std::pair<detail::device_pool*, detail::device_pool::slot_ref> detach() {
+        auto r = std::make_pair(pool_, ref_);
+        pool_ = nullptr;
+        return r;
+    }
+};
 
 // ------------------------------------------------------------------ target
 class target {
@@ -192,24 +346,20 @@ class target {
         int device = 0;
         hpxhip_stream stream = nullptr;
         std::mutex mtx;  // lazy stream creation, cuda_target.cpp:257 spinlock
-        // Ring of 64-byte result slots (device + pinned host) through which
-        // reduce/copy_if results travel back without a per-call allocation.
-        void* dev_slots = nullptr;
-        void* host_slots = nullptr;
-        unsigned next_slot = 0;
         ~handle() {
-            // drain first: queued kernels may still write the result slots and
-            // a completion host function may still be reading them
-            if (stream) {
-                hpxhip_stream_synchronize(stream);
-                hpxhip_stream_destroy(stream);
-            }
-            if (dev_slots) hpxhip_free(dev_slots);
-            if (host_slots) hpxhip_free_host(host_slots);
+            // the stream goes back to the device pool, queued work and all
+            if (stream) detail::device_pool::get(device).give_stream(stream);
         }
     };
-    static constexpr unsigned kSlots = 1024, kSlotBytes = 64;
     std::shared_ptr<handle> h_;
+
+    template <typename S>
+    struct completion {
+        std::shared_ptr<S> st;
+        detail::device_pool* pool = nullptr;
+        detail::device_pool::slot_ref slot{};
+        std::function<void(unsigned char const*)> on_ready;
+    };
 
 public:
     target() : target(0) {}
@@ -231,8 +381,13 @@ public:
         int get_device() const { return h->device; }
         hpxhip_stream get_stream() const {
             std::lock_guard<std::mutex> lk(h->mtx);
-            if (!h->stream) detail::check(hpxhip_stream_create(h->device, &h->stream), "hpxhip_stream_create");
+            if (!h->stream) h->stream = detail::device_pool::get(h->device).take_stream();
             return h->stream;
+        }
+        std::size_t processing_units() const {
+            hpxhip_device_props p;
+            detail::check(hpxhip_device_props_get(h->device, &p), "hpxhip_device_props_get");
+            return static_cast<std::size_t>(p.compute_units);
         }
     };
     native_handle_type native_handle() const { return native_handle_type{h_.get()}; }
@@ -249,62 +404,65 @@ public:
     // cuda_target.cpp:307-317: a future that becomes ready when all work queued
     // so far on the stream is done; completed from the HIP callback thread.
     future<void> get_future() const {
-        return async_result<void>([] {});
+        return async_result<void>([](unsigned char const*) {});
     }
 
     // A future completed from a stream callback once all work queued so far
-    // is done; fn() (e.g. reading a pinned result slot) runs on the first
-    // get(), after the device error word is checked.
+    // is done.  With a result slot, the callback copies the slot's bytes into
+    // the shared state and releases the slot; then on_ready(bytes) runs (still
+    // on the callback thread, no HIP calls: e.g. a for_loop reduction folding
+    // its view into the live-out variable, for_loop_reduction.hpp:60-66) and
+    // the state becomes ready.  value(bytes) runs on the first get(), after
+    // the device error word is checked.
     template <typename R>
-    future<R> async_result(std::function<R()> fn) const {
+    future<R> async_result(std::function<R(unsigned char const*)> value, result_slot slot = {},
+                           std::function<void(unsigned char const*)> on_ready = {}) const {
         using S = lcos::detail::shared_state<R>;
         auto st = std::make_shared<S>();
         int dev = h_->device;
-        st->value_fn = [dev, fn = std::move(fn)]() -> R {
+        S* self = st.get();  // value_fn is owned by the state it reads
+        st->value_fn = [dev, self, value = std::move(value)]() -> R {
             uint32_t code = 0;
             detail::check(hpxhip_device_error(dev, &code), "hpxhip_device_error");
             if (code) throw kernel_error(HPXHIP_ERROR_DEVICE_TIMEOUT, "device kernel error word set");
-            return fn();
+            return value(self->raw);
         };
-        auto* keep = new std::shared_ptr<S>(st);  // owned by the callback
+        hpxhip_stream s = stream();
+        auto* c = new completion<S>{st, nullptr, {}, std::move(on_ready)};
+        if (slot) {
+            auto d = slot.detach();
+            c->pool = d.first;
+            c->slot = d.second;
+        }
         int rc = hpxhip_stream_add_callback(
-            stream(),
+            s,
             [](void* p, int status) {
-                auto* sp = static_cast<std::shared_ptr<S>*>(p);
-                (*sp)->set_ready(status);
-                delete sp;
+                auto* cp = static_cast<completion<S>*>(p);
+                if (cp->pool) {
+                    std::memcpy(cp->st->raw, cp->slot.host, sizeof(cp->st->raw));
+                    cp->pool->release(cp->slot.id);
+                }
+                if (status == 0 && cp->on_ready) cp->on_ready(cp->st->raw);
+                cp->st->set_ready(status);
+                delete cp;
             },
-            keep);
+            c);
         if (rc != HPXHIP_SUCCESS) {
-            delete keep;
+            if (c->pool) c->pool->release(c->slot.id);
+            delete c;
             detail::check(rc, "hpxhip_stream_add_callback");
         }
         return future<R>(st);
     }
 
-    // (device slot, host slot) pair; the host slot is filled by an async D2H
-    // copy queued after the kernel that writes the device slot.
-    std::pair<void*, void*> result_slot() const {
-        std::lock_guard<std::mutex> lk(h_->mtx);
-        if (!h_->dev_slots) {
-            detail::check(hpxhip_malloc(h_->device, &h_->dev_slots, kSlots * kSlotBytes), "result slots");
-            detail::check(hpxhip_malloc_host(&h_->host_slots, kSlots * kSlotBytes), "result slots");
-        }
-        unsigned i = h_->next_slot++ % kSlots;
-        return {static_cast<char*>(h_->dev_slots) + i * kSlotBytes,
-                static_cast<char*>(h_->host_slots) + i * kSlotBytes};
-    }
+    // A (device, pinned host) slot from this device's pool; see result_slot.
+    result_slot make_result_slot() const { return result_slot(detail::device_pool::get(h_->device)); }
 
-    std::size_t processing_units() const {
-        hpxhip_device_props p;
-        detail::check(hpxhip_device_props_get(h_->device, &p), "hpxhip_device_props_get");
-        return static_cast<std::size_t>(p.compute_units);
-    }
+    std::size_t processing_units() const { return native_handle().processing_units(); }
 
     friend bool operator==(target const& a, target const& b) { return a.h_->device == b.h_->device; }
     friend bool operator!=(target const& a, target const& b) { return !(a == b); }
 };
-
 inline std::vector<target> get_local_targets() {
     int n = 0;
     detail::check(hpxhip_get_device_count(&n), "hpxhip_get_device_count");
@@ -433,22 +591,6 @@ template <typename It>
 struct is_device_iterator : std::false_type {};
 template <typename T>
 struct is_device_iterator<device_iterator<T>> : std::true_type {};
-
-// ----------------------------------------------------------------- executors
-class default_executor {
-    hip::target target_;
-
-public:
-    using execution_category = struct parallel_execution_tag {};
-    using executor_parameters_type = void;
-
-    default_executor() = default;
-    explicit default_executor(hip::target const& t) : target_(t) {}
-    hip::target const& target() const { return target_; }
-    hip::target const& context() const { return target_; }
-    std::size_t processing_units_count() const { return target_.processing_units(); }
-    friend bool operator==(default_executor const& a, default_executor const& b) { return a.target_ == b.target_; }
-};
 
 }}  // namespace compute::hip
 

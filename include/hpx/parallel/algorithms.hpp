@@ -30,7 +30,10 @@
 #pragma once
 
 #include <hpx/compute/hip.hpp>
+#include <hpx/compute/hip/concurrent_executor.hpp>
+#include <hpx/compute/hip/default_executor.hpp>
 #include <hpx/compute/hip/functional.hpp>
+#include <hpx/parallel/detail/device_closures.hpp>
 #include <hpx/parallel/execution.hpp>
 
 #include <algorithm>
@@ -61,8 +64,25 @@ constexpr bool is_task = policy_t<P>::is_task;
 
 template <typename P, typename It>
 hip::target const& target_of(P const& p, It const& it) {
-    if constexpr (policy_t<P>::has_executor) return p.executor().target();
-    else return it.target();
+    if constexpr (policy_t<P>::has_executor) {
+        return p.executor().target();
+    } else {
+        static_assert(is_dev<It>, "raw device pointers need a policy with a HIP executor (par.on(exec))");
+        return it.target();
+    }
+}
+
+template <typename F>
+constexpr bool is_complete_binary = tr::detail::is_complete<tr::binary_t<F>>::value;
+
+template <typename P>
+constexpr bool is_concurrent =
+    std::is_same<typename policy_t<P>::executor_type, hip::concurrent_executor>::value;
+
+template <typename It>
+auto raw_ptr(It it) {
+    if constexpr (std::is_pointer<It>::value) return it;
+    else return it.device_ptr();
 }
 
 template <typename P, typename R>
@@ -72,13 +92,86 @@ using result_t = typename util::detail::algorithm_result<P, R>::type;
 template <typename R, typename P, typename Fn>
 result_t<P, R> finish(P const&, hip::target const& t, Fn&& fn) {
     if constexpr (is_task<P>) {
-        return t.template async_result<R>(std::function<R()>(std::forward<Fn>(fn)));
+        return t.template async_result<R>(
+            [fn = std::forward<Fn>(fn)](unsigned char const*) mutable -> R { return fn(); });
     } else {
         t.synchronize();
         if constexpr (std::is_void<R>::value) fn();
         else return fn();
     }
 }
+
+// Finish an algorithm whose result (<= 64 bytes) is queued as `kernel ->
+// D2H copy into slot.host()`.  value(bytes) forms the result; on_ready(bytes)
+// (optional) runs as soon as the bytes are there -- for a task policy on the
+// completion callback, before the future becomes ready.  The slot is owned by
+// the completion, never by the target (whose stream may belong to a
+// temporary policy).
+struct no_on_ready {
+    void operator()(unsigned char const*) const {}
+};
+template <typename R, typename P, typename Value, typename OnReady = no_on_ready>
+result_t<P, R> finish_slot(P const&, hip::target const& t, hip::result_slot slot, Value value,
+                           OnReady on_ready = OnReady()) {
+    if constexpr (is_task<P>) {
+        return t.template async_result<R>(std::function<R(unsigned char const*)>(std::move(value)), std::move(slot),
+                                          std::function<void(unsigned char const*)>(std::move(on_ready)));
+    } else {
+        t.synchronize();
+        auto const* bytes = static_cast<unsigned char const*>(slot.host());
+        on_ready(bytes);
+        if constexpr (std::is_void<R>::value) value(bytes);
+        else return value(bytes);
+    }
+}
+
+// An elementwise algorithm over n items: launch(target, offset, count) queues
+// the kernel(s) for items [offset, offset + count).  With a concurrent_executor
+// the range is cut into one chunk per stream (concurrent_executor_parameters:
+// chunk = ceil(n / streams)) and the result is ready when every stream is;
+// otherwise one launch on the policy's (or the iterator's) target.
+template <typename R, typename P, typename It, typename Launch, typename Fn>
+result_t<P, R> run_elementwise(P const& p, It const& it, uint64_t n, Launch&& launch, Fn&& fn) {
+    if constexpr (is_concurrent<P>) {
+        auto const& ex = p.executor().executors();
+        uint64_t k = ex.size();
+        uint64_t chunk = (n + k - 1) / k;
+        std::size_t used = 0;
+        for (uint64_t off = 0; off < n; off += chunk, ++used)
+            launch(ex[used].target(), off, std::min<uint64_t>(chunk, n - off));
+        if constexpr (is_task<P>) {
+            std::vector<hpx::future<void>> fs;
+            for (std::size_t i = 0; i < std::max<std::size_t>(used, 1); ++i) fs.push_back(ex[i].target().get_future());
+            return hpx::when_all(std::move(fs)).then(
+                [fn = std::forward<Fn>(fn)](hpx::future<std::vector<hpx::future<void>>>& all) mutable -> R {
+                    for (auto& f : all.get()) f.get();
+                    return fn();
+                });
+        } else {
+            for (std::size_t i = 0; i < used; ++i) ex[i].target().synchronize();
+            if constexpr (std::is_void<R>::value) fn();
+            else return fn();
+        }
+    } else {
+        auto const& t = target_of(p, it);
+        launch(t, uint64_t(0), n);
+        return finish<R>(p, t, std::forward<Fn>(fn));
+    }
+}
+
+// Queue the D2H copy of a result slot's first `bytes` bytes.
+inline void fetch_slot(hip::target const& t, hip::result_slot const& slot, std::size_t bytes, char const* what) {
+    check(hpxhip_memcpy_async(const_cast<void*>(slot.host()), slot.device(), bytes, HPXHIP_D2H, t.stream()), what);
+}
+
+template <typename T>
+struct load_value {
+    T operator()(unsigned char const* b) const {
+        T v;
+        std::memcpy(&v, b, sizeof(T));
+        return v;
+    }
+};
 
 template <typename It>
 uint64_t distance(It first, It last) {
@@ -96,17 +189,28 @@ auto host_ptr(It it) {
 }  // namespace detail
 
 // ------------------------------------------------------------- for_each
+// A function object with a traits::unary mapping runs on the library kernel;
+// any other callable runs on a kernel instantiated for it when the TU is
+// compiled by hipcc (detail/device_closures.hpp), else it does not compile.
 template <typename P, typename It, typename F>
 detail::result_t<P, It> for_each(P&& p, It first, It last, F&& f) {
     static_assert(detail::is_dev<It>, "for_each: device iterators required");
     using T = detail::value_t<It>;
-    using Tr = detail::tr::unary_t<F>;
-    auto const& t = detail::target_of(p, first);
     uint64_t n = detail::distance(first, last);
-    T s[2] = {};
-    Tr::scalars(f, s);
-    detail::check(hpxhip_for_each(detail::dt<T>, Tr::kind, s, first.device_ptr(), n, t.stream()), "for_each");
-    return detail::finish<It>(p, t, [last] { return last; });
+    T* base = first.device_ptr();
+    return detail::run_elementwise<It>(
+        p, first, n,
+        [&](auto const& t, uint64_t off, uint64_t cnt) {
+            if constexpr (detail::tr::is_unary<F>) {
+                using Tr = detail::tr::unary_t<F>;
+                T s[2] = {};
+                Tr::scalars(f, s);
+                detail::check(hpxhip_for_each(detail::dt<T>, Tr::kind, s, base + off, cnt, t.stream()), "for_each");
+            } else {
+                detail::device_for_each(t, f, base + off, cnt);
+            }
+        },
+        [last] { return last; });
 }
 
 template <typename P, typename It, typename Size, typename F>
@@ -123,23 +227,30 @@ template <typename P, typename It, typename T>
 detail::result_t<P, void> fill(P&& p, It first, It last, T value) {
     static_assert(detail::is_dev<It>, "fill: device iterators required");
     using V = detail::value_t<It>;
-    auto const& t = detail::target_of(p, first);
     V v = static_cast<V>(value);
-    detail::check(hpxhip_fill(detail::dt<V>, &v, first.device_ptr(), detail::distance(first, last), t.stream()),
-                  "fill");
-    return detail::finish<void>(p, t, [] {});
+    V* base = first.device_ptr();
+    return detail::run_elementwise<void>(
+        p, first, detail::distance(first, last),
+        [&](auto const& t, uint64_t off, uint64_t cnt) {
+            detail::check(hpxhip_fill(detail::dt<V>, &v, base + off, cnt, t.stream()), "fill");
+        },
+        [] {});
 }
 
 template <typename P, typename It, typename Size, typename T>
 detail::result_t<P, It> fill_n(P&& p, It first, Size count, T value) {
     static_assert(detail::is_dev<It>, "fill_n: device iterators required");
     using V = detail::value_t<It>;
-    auto const& t = detail::target_of(p, first);
     uint64_t n = count > 0 ? static_cast<uint64_t>(count) : 0;
     V v = static_cast<V>(value);
-    detail::check(hpxhip_fill(detail::dt<V>, &v, first.device_ptr(), n, t.stream()), "fill_n");
+    V* base = first.device_ptr();
     It end = first + static_cast<std::ptrdiff_t>(n);
-    return detail::finish<It>(p, t, [end] { return end; });
+    return detail::run_elementwise<It>(
+        p, first, n,
+        [&](auto const& t, uint64_t off, uint64_t cnt) {
+            detail::check(hpxhip_fill(detail::dt<V>, &v, base + off, cnt, t.stream()), "fill_n");
+        },
+        [end] { return end; });
 }
 
 // ------------------------------------------------------------------ copy
@@ -150,10 +261,15 @@ detail::result_t<P, util::tagged_pair<In, Out>> copy(P&& p, In first, In last, O
     if constexpr (detail::is_dev<In> && detail::is_dev<Out>) {
         using T = detail::value_t<In>;
         static_assert(std::is_same<T, detail::value_t<Out>>::value, "copy: element types must match");
-        auto const& t = detail::target_of(p, first);
-        detail::check(hpxhip_copy(detail::dt<T>, first.device_ptr(), dest.device_ptr(), n, t.stream()), "copy");
+        T const* in = first.device_ptr();
+        T* out = dest.device_ptr();
         Out end = dest + static_cast<std::ptrdiff_t>(n);
-        return detail::finish<R>(p, t, [last, end] { return R{last, end}; });
+        return detail::run_elementwise<R>(
+            p, first, n,
+            [&](auto const& t, uint64_t off, uint64_t cnt) {
+                detail::check(hpxhip_copy(detail::dt<T>, in + off, out + off, cnt, t.stream()), "copy");
+            },
+            [last, end] { return R{last, end}; });
     } else if constexpr (detail::is_dev<In>) {  // device -> host
         using T = detail::value_t<In>;
         auto const& t = detail::target_of(p, first);
@@ -192,38 +308,45 @@ detail::result_t<P, util::tagged_pair<In, Out>> copy_if(P&& p, In first, In last
     auto const& t = detail::target_of(p, first);
     uint64_t n = detail::distance(first, last);
     T arg = static_cast<T>(Tr::arg(f));
-    auto slot = t.result_slot();
+    auto slot = t.make_result_slot();
     detail::check(hpxhip_copy_if(detail::dt<T>, Tr::kind, &arg, first.device_ptr(), dest.device_ptr(), n,
-                                 static_cast<uint64_t*>(slot.first), t.stream(), nullptr, 0),
+                                 static_cast<uint64_t*>(slot.device()), t.stream(), nullptr, 0),
                   "copy_if");
-    detail::check(hpxhip_memcpy_async(slot.second, slot.first, 8, HPXHIP_D2H, t.stream()), "copy_if count");
-    void* host = slot.second;
-    return detail::finish<R>(p, t, [last, dest, host] {
+    detail::fetch_slot(t, slot, 8, "copy_if count");
+    return detail::finish_slot<R>(p, t, std::move(slot), [last, dest](unsigned char const* b) {
         uint64_t c;
-        std::memcpy(&c, host, 8);
+        std::memcpy(&c, b, 8);
         return R{last, dest + static_cast<std::ptrdiff_t>(c)};
     });
 }
 
 // ------------------------------------------------------------- transform
-template <typename P, typename In, typename Out, typename F,
-          typename = typename std::enable_if<detail::tr::is_unary<F>>::type>
+template <typename P, typename In, typename Out, typename F>
 detail::result_t<P, util::tagged_pair<In, Out>> transform(P&& p, In first, In last, Out dest, F&& f) {
     static_assert(detail::is_dev<In> && detail::is_dev<Out>, "transform: device iterators required");
     using TI = detail::value_t<In>;
     using TO = detail::value_t<Out>;
-    using Tr = detail::tr::unary_t<F>;
-    using C = detail::tr::compute_t<Tr, F, TI>;
     using R = util::tagged_pair<In, Out>;
-    auto const& t = detail::target_of(p, first);
     uint64_t n = detail::distance(first, last);
-    C s[2] = {};
-    Tr::scalars(f, s);
-    detail::check(hpxhip_transform(detail::dt<TI>, detail::dt<C>, detail::dt<TO>, Tr::kind, s, first.device_ptr(),
-                                   dest.device_ptr(), n, t.stream()),
-                  "transform");
+    TI const* in = first.device_ptr();
+    TO* out = dest.device_ptr();
     Out end = dest + static_cast<std::ptrdiff_t>(n);
-    return detail::finish<R>(p, t, [last, end] { return R{last, end}; });
+    return detail::run_elementwise<R>(
+        p, first, n,
+        [&](auto const& t, uint64_t off, uint64_t cnt) {
+            if constexpr (detail::tr::is_unary<F>) {
+                using Tr = detail::tr::unary_t<F>;
+                using C = detail::tr::compute_t<Tr, F, TI>;
+                C s[2] = {};
+                Tr::scalars(f, s);
+                detail::check(hpxhip_transform(detail::dt<TI>, detail::dt<C>, detail::dt<TO>, Tr::kind, s, in + off,
+                                               out + off, cnt, t.stream()),
+                              "transform");
+            } else {
+                detail::device_transform(t, f, in + off, out + off, cnt);
+            }
+        },
+        [last, end] { return R{last, end}; });
 }
 
 namespace detail {
@@ -232,27 +355,38 @@ result_t<P, util::tagged_tuple<In1, In2, Out>> transform_binary(P&& p, In1 first
                                                                 F&& f) {
     static_assert(is_dev<In1> && is_dev<In2> && is_dev<Out>, "transform: device iterators required");
     using T = value_t<In1>;
-    static_assert(std::is_same<T, value_t<In2>>::value, "transform: input element types must match");
+    using T2 = value_t<In2>;
     using TO = value_t<Out>;
-    using Tr = tr::binary_t<F>;
-    using C = tr::compute_t<Tr, F, T>;
     using R = util::tagged_tuple<In1, In2, Out>;
-    auto const& t = target_of(p, first1);
-    C s[2] = {};
-    Tr::scalars(f, s);
-    check(hpxhip_transform_binary(dt<T>, dt<C>, dt<TO>, Tr::kind, s, first1.device_ptr(), first2.device_ptr(),
-                                  dest.device_ptr(), n, t.stream()),
-          "transform");
+    T const* a = first1.device_ptr();
+    T2 const* b = first2.device_ptr();
+    TO* out = dest.device_ptr();
     auto d = static_cast<std::ptrdiff_t>(n);
     In1 e1 = first1 + d;
     In2 e2 = first2 + d;
     Out eo = dest + d;
-    return finish<R>(p, t, [e1, e2, eo] { return R{e1, e2, eo}; });
+    return run_elementwise<R>(
+        p, first1, n,
+        [&](auto const& t, uint64_t off, uint64_t cnt) {
+            if constexpr (is_complete_binary<F>) {
+                static_assert(std::is_same<T, T2>::value, "transform: input element types must match");
+                using Tr = tr::binary_t<F>;
+                using C = tr::compute_t<Tr, F, T>;
+                C s[2] = {};
+                Tr::scalars(f, s);
+                check(hpxhip_transform_binary(dt<T>, dt<C>, dt<TO>, Tr::kind, s, a + off, b + off, out + off, cnt,
+                                              t.stream()),
+                      "transform");
+            } else {
+                device_transform2(t, f, a + off, b + off, out + off, cnt);
+            }
+        },
+        [e1, e2, eo] { return R{e1, e2, eo}; });
 }
 }  // namespace detail
 
 template <typename P, typename In1, typename In2, typename Out, typename F,
-          typename = typename std::enable_if<!detail::tr::is_unary<F> && detail::is_dev<Out>>::type>
+          typename = typename std::enable_if<detail::is_dev<Out>>::type>
 detail::result_t<P, util::tagged_tuple<In1, In2, Out>> transform(P&& p, In1 first1, In1 last1, In2 first2, Out dest,
                                                                 F&& f) {
     return detail::transform_binary(std::forward<P>(p), first1, detail::distance(first1, last1), first2, dest,
@@ -275,17 +409,12 @@ result_t<P, T> reduce_impl(P&& p, It first, It last, T init, Op&& op, Conv&& con
     auto const& t = target_of(p, first);
     T s[2] = {};
     tr::unary_t<Conv>::scalars(conv, s);
-    auto slot = t.result_slot();
+    auto slot = t.make_result_slot();
     check(hpxhip_transform_reduce(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::unary_t<Conv>::kind, s, &init,
-                                  first.device_ptr(), distance(first, last), slot.first, t.stream(), nullptr, 0),
+                                  first.device_ptr(), distance(first, last), slot.device(), t.stream(), nullptr, 0),
           "transform_reduce");
-    check(hpxhip_memcpy_async(slot.second, slot.first, sizeof(T), HPXHIP_D2H, t.stream()), "reduce result");
-    void* host = slot.second;
-    return finish<T>(p, t, [host] {
-        T v;
-        std::memcpy(&v, host, sizeof(T));
-        return v;
-    });
+    fetch_slot(t, slot, sizeof(T), "reduce result");
+    return finish_slot<T>(p, t, std::move(slot), load_value<T>{});
 }
 }  // namespace detail
 
@@ -320,18 +449,13 @@ result_t<P, T> reduce_binary_impl(P&& p, It1 first1, It1 last1, It2 first2, T in
     auto const& t = target_of(p, first1);
     T s[2] = {};
     tr::binary_t<Comb>::scalars(comb, s);
-    auto slot = t.result_slot();
+    auto slot = t.make_result_slot();
     check(hpxhip_transform_reduce_binary(dt<TI>, dt<T>, tr::binop_t<Red>::kind, tr::binary_t<Comb>::kind, s, &init,
                                          first1.device_ptr(), first2.device_ptr(), distance(first1, last1),
-                                         slot.first, t.stream(), nullptr, 0),
+                                         slot.device(), t.stream(), nullptr, 0),
           "transform_reduce");
-    check(hpxhip_memcpy_async(slot.second, slot.first, sizeof(T), HPXHIP_D2H, t.stream()), "reduce result");
-    void* host = slot.second;
-    return finish<T>(p, t, [host] {
-        T v;
-        std::memcpy(&v, host, sizeof(T));
-        return v;
-    });
+    fetch_slot(t, slot, sizeof(T), "reduce result");
+    return finish_slot<T>(p, t, std::move(slot), load_value<T>{});
 }
 }  // namespace detail
 
@@ -565,30 +689,32 @@ result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, ui
     auto const& t = target_of(p, in0);
     T s[2] = {};
     T init = red.identity_;
-    auto slot = t.result_slot();
+    auto slot = t.make_result_slot();
     if constexpr (sizeof...(In) == 1) {
         tr::unary_t<F>::scalars(b.f, s);
         check(hpxhip_transform_reduce(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::unary_t<F>::kind, s, &init,
-                                      in0.device_ptr(), n, slot.first, t.stream(), nullptr, 0),
+                                      raw_ptr(in0), n, slot.device(), t.stream(), nullptr, 0),
               "for_loop_n");
     } else {
         auto in1 = std::get<1>(ins);
         static_assert(std::is_same<TI, value_t<decltype(in1)>>::value, "for_loop_n: both inputs need one element type");
         tr::binary_t<F>::scalars(b.f, s);
         check(hpxhip_transform_reduce_binary(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::binary_t<F>::kind, s, &init,
-                                             in0.device_ptr(), in1.device_ptr(), n, slot.first, t.stream(), nullptr, 0),
+                                             raw_ptr(in0), raw_ptr(in1), n, slot.device(), t.stream(), nullptr, 0),
               "for_loop_n");
     }
-    check(hpxhip_memcpy_async(slot.second, slot.first, sizeof(T), HPXHIP_D2H, t.stream()), "for_loop_n result");
-    void* host = slot.second;
+    fetch_slot(t, slot, sizeof(T), "for_loop_n result");
     T* var = &red.var_;
     Op op = red.op_;
     // exit_iteration (for_loop_reduction.hpp:60-66): fold the view into var
-    return finish<void>(p, t, [host, var, op] {
-        T view;
-        std::memcpy(&view, host, sizeof(T));
-        *var = op(*var, view);
-    });
+    // as soon as the view is back -- under par(task) on the completion, so
+    // var is final once the future is ready (not only after get()).
+    return finish_slot<void>(p, t, std::move(slot), [](unsigned char const*) {},
+                             [var, op](unsigned char const* b) {
+                                 T view;
+                                 std::memcpy(&view, b, sizeof(T));
+                                 *var = op(*var, view);
+                             });
 }
 template <typename P, typename Vars, std::size_t N, std::size_t Out, typename F, std::size_t In0>
 result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n,
@@ -599,13 +725,19 @@ result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, ui
     using TO = value_t<decltype(out)>;
     using Tr = tr::unary_t<F>;
     using C = tr::compute_t<Tr, F, TI>;
-    auto const& t = target_of(p, in);
     C s[2] = {};
     Tr::scalars(b.f, s);
-    check(hpxhip_transform_strided(dt<TI>, dt<C>, dt<TO>, Tr::kind, s, in.device_ptr(), st[In0], out.device_ptr(),
-                                   st[Out], n, t.stream()),
-          "for_loop_n");
-    return finish<void>(p, t, [] {});
+    TI const* pin = raw_ptr(in);
+    TO* pout = raw_ptr(out);
+    return run_elementwise<void>(
+        p, in, n,
+        [&](auto const& t, uint64_t off, uint64_t cnt) {
+            const int64_t o = static_cast<int64_t>(off);
+            check(hpxhip_transform_strided(dt<TI>, dt<C>, dt<TO>, Tr::kind, s, pin + o * st[In0], st[In0],
+                                           pout + o * st[Out], st[Out], cnt, t.stream()),
+                  "for_loop_n");
+        },
+        [] {});
 }
 template <typename P, typename Vars, std::size_t N, std::size_t Out, typename F, std::size_t In0, std::size_t In1>
 result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n,
@@ -618,13 +750,58 @@ result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, ui
     using TO = value_t<decltype(out)>;
     using Tr = tr::binary_t<F>;
     using C = tr::compute_t<Tr, F, TI>;
-    auto const& t = target_of(p, in0);
     C s[2] = {};
     Tr::scalars(b.f, s);
-    check(hpxhip_transform_binary_strided(dt<TI>, dt<C>, dt<TO>, Tr::kind, s, in0.device_ptr(), st[In0],
-                                          in1.device_ptr(), st[In1], out.device_ptr(), st[Out], n, t.stream()),
-          "for_loop_n");
-    return finish<void>(p, t, [] {});
+    TI const* p0 = raw_ptr(in0);
+    TI const* p1 = raw_ptr(in1);
+    TO* pout = raw_ptr(out);
+    return run_elementwise<void>(
+        p, in0, n,
+        [&](auto const& t, uint64_t off, uint64_t cnt) {
+            const int64_t o = static_cast<int64_t>(off);
+            check(hpxhip_transform_binary_strided(dt<TI>, dt<C>, dt<TO>, Tr::kind, s, p0 + o * st[In0], st[In0],
+                                                  p1 + o * st[In1], st[In1], pout + o * st[Out], st[Out], cnt,
+                                                  t.stream()),
+                  "for_loop_n");
+        },
+        [] {});
+}
+
+template <typename T>
+struct is_reduction : std::false_type {};
+template <typename T, typename Op>
+struct is_reduction<reduction_helper<T, Op>> : std::true_type {};
+
+// Any other body: body(first + i*stride, induction_k + i*stride_k, ...) on a
+// kernel instantiated for it (hipcc only).  Loop variables reach the body as
+// raw device pointers, as in for_loop_compute.cu:40-48 (`int* A, int* B, int* C`).
+template <typename P, typename Vars, std::size_t N, typename B, std::size_t... I>
+result_t<P, void> for_loop_generic(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n, B const& body,
+                                   std::index_sequence<I...>) {
+    static_assert(!(is_reduction<std::decay_t<std::tuple_element_t<I, Vars>>>::value || ...),
+                  "for_loop: reductions need a functional::loop_accumulate body");
+    auto ptrs = std::make_tuple(raw_ptr(std::get<I>(v))...);
+    return run_elementwise<void>(
+        p, std::get<0>(v), n,
+        [&](auto const& t, uint64_t off, uint64_t cnt) {
+            const int64_t o = static_cast<int64_t>(off);
+            device_loop(t, body, cnt,
+                        strided_ptr<std::remove_pointer_t<std::decay_t<decltype(std::get<I>(ptrs))>>>{
+                            std::get<I>(ptrs) + o * st[I], st[I]}...);
+        },
+        [] {});
+}
+template <typename Body>
+struct is_builtin_body : std::false_type {};
+template <std::size_t Out, typename F, std::size_t... In>
+struct is_builtin_body<compute::hip::functional::loop_assign<Out, F, In...>> : std::true_type {};
+template <std::size_t Red, typename F, std::size_t... In>
+struct is_builtin_body<compute::hip::functional::loop_accumulate<Red, F, In...>> : std::true_type {};
+
+template <typename P, typename Vars, std::size_t N, typename B,
+          typename = std::enable_if_t<!is_builtin_body<std::decay_t<B>>::value>>
+result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n, B const& body) {
+    return for_loop_generic(std::forward<P>(p), v, st, n, body, std::make_index_sequence<N>{});
 }
 template <typename P, typename It, typename Tuple, std::size_t... I>
 auto for_loop_dispatch(P&& p, It first, int64_t first_stride, uint64_t n, Tuple&& args, std::index_sequence<I...>) {
@@ -640,7 +817,8 @@ auto for_loop_dispatch(P&& p, It first, int64_t first_stride, uint64_t n, Tuple&
 template <typename P, typename It, typename Size, typename... Args>
 detail::result_t<P, void> for_loop_n(P&& p, It first, Size count, Args&&... args) {
     static_assert(sizeof...(Args) >= 1, "for_loop_n: missing loop body");
-    static_assert(detail::is_dev<It>, "for_loop_n: the loop variable must be a device iterator");
+    static_assert(detail::is_dev<It> || std::is_pointer<It>::value,
+                  "for_loop_n: the loop variable must be a device iterator or a device pointer");
     uint64_t n = count > 0 ? static_cast<uint64_t>(count) : 0;
     return detail::for_loop_dispatch(std::forward<P>(p), first, 1, n, std::forward_as_tuple(args...),
                                      std::make_index_sequence<sizeof...(Args) - 1>{});
@@ -656,7 +834,8 @@ detail::result_t<P, void> for_loop(P&& p, It first, It last, Args&&... args) {
 template <typename P, typename It, typename Size, typename S, typename... Args>
 detail::result_t<P, void> for_loop_n_strided(P&& p, It first, Size count, S stride, Args&&... args) {
     static_assert(sizeof...(Args) >= 1, "for_loop_n_strided: missing loop body");
-    static_assert(detail::is_dev<It>, "for_loop_n_strided: the loop variable must be a device iterator");
+    static_assert(detail::is_dev<It> || std::is_pointer<It>::value,
+                  "for_loop_n_strided: the loop variable must be a device iterator or a device pointer");
     if (stride == 0) throw hpx::exception(HPXHIP_ERROR_INVALID_ARGUMENT, "for_loop_n_strided: zero stride");
     uint64_t n = count > 0 ? static_cast<uint64_t>(count) : 0;
     return detail::for_loop_dispatch(std::forward<P>(p), first, static_cast<int64_t>(stride), n,

@@ -77,6 +77,45 @@ struct is_async_execution_policy : std::false_type {};
 template <typename C, typename E>
 struct is_async_execution_policy<policy<C, true, E>> : std::true_type {};
 
+// ------------------------------------------------------- executor concept
+// Traits (hpx/traits/is_executor.hpp, executor_traits.hpp); an executor
+// opts in by specialisation, as default_executor.hpp:233-260 does.
+template <typename Executor, typename Enable = void>
+struct executor_execution_category {
+    using type = parallel_execution_tag;
+};
+template <typename T> struct is_one_way_executor : std::false_type {};
+template <typename T> struct is_two_way_executor : std::false_type {};
+template <typename T> struct is_bulk_one_way_executor : std::false_type {};
+template <typename T> struct is_bulk_two_way_executor : std::false_type {};
+template <typename T>
+struct is_executor_any
+  : std::integral_constant<bool, is_one_way_executor<T>::value || is_two_way_executor<T>::value ||
+                                     is_bulk_one_way_executor<T>::value || is_bulk_two_way_executor<T>::value> {};
+
+// Customisation points (executors/execution.hpp:650-795): forward to the
+// executor's members.
+template <typename Executor, typename F, typename... Ts>
+void post(Executor&& exec, F&& f, Ts&&... ts) {
+    exec.post(std::forward<F>(f), std::forward<Ts>(ts)...);
+}
+template <typename Executor, typename F, typename... Ts>
+auto async_execute(Executor&& exec, F&& f, Ts&&... ts) {
+    return exec.async_execute(std::forward<F>(f), std::forward<Ts>(ts)...);
+}
+template <typename Executor, typename F, typename... Ts>
+void sync_execute(Executor&& exec, F&& f, Ts&&... ts) {
+    exec.sync_execute(std::forward<F>(f), std::forward<Ts>(ts)...);
+}
+template <typename Executor, typename F, typename Shape, typename... Ts>
+auto bulk_async_execute(Executor&& exec, F&& f, Shape const& shape, Ts&&... ts) {
+    return exec.bulk_async_execute(std::forward<F>(f), shape, std::forward<Ts>(ts)...);
+}
+template <typename Executor, typename F, typename Shape, typename... Ts>
+void bulk_sync_execute(Executor&& exec, F&& f, Shape const& shape, Ts&&... ts) {
+    exec.bulk_sync_execute(std::forward<F>(f), shape, std::forward<Ts>(ts)...);
+}
+
 // executor parameters (accepted, ignored)
 struct static_chunk_size {
     std::size_t chunk = 0;

@@ -12,8 +12,11 @@ inline std::atomic<int>& error_count() {
     static std::atomic<int> n{0};
     return n;
 }
-template <typename A, typename B>
-bool check_rel(bool ok, A const& a, B const& b, char const* expr, char const* file, int line) {
+// Each operand is evaluated exactly once (an operand may be a call with side
+// effects, e.g. HPX_TEST_EQ(hpx::init(argc, argv), 0)).
+template <typename A, typename B, typename Rel>
+bool check_rel(A const& a, B const& b, Rel rel, char const* expr, char const* file, int line) {
+    bool ok = rel(a, b);
     if (!ok) {
         ++error_count();
         std::cerr << file << "(" << line << "): test '" << expr << "' failed (" << a << " vs " << b << ")\n";
@@ -37,8 +40,12 @@ inline int report_errors() {
     ((expr) ? true                                                                              \
             : (++::hpx::util::detail::error_count(),                                            \
                (std::cerr << __FILE__ << "(" << __LINE__ << "): " << (msg) << "\n"), false))
-#define HPX_TEST_EQ(a, b) ::hpx::util::detail::check_rel((a) == (b), (a), (b), #a " == " #b, __FILE__, __LINE__)
-#define HPX_TEST_NEQ(a, b) ::hpx::util::detail::check_rel((a) != (b), (a), (b), #a " != " #b, __FILE__, __LINE__)
-#define HPX_TEST_LT(a, b) ::hpx::util::detail::check_rel((a) < (b), (a), (b), #a " < " #b, __FILE__, __LINE__)
-#define HPX_TEST_LTE(a, b) ::hpx::util::detail::check_rel((a) <= (b), (a), (b), #a " <= " #b, __FILE__, __LINE__)
+#define HPX_TEST_REL_(a, b, OP)                                                                   \
+    ::hpx::util::detail::check_rel(                                                               \
+        (a), (b), [](auto const& x_, auto const& y_) { return bool(x_ OP y_); }, #a " " #OP " " #b, \
+        __FILE__, __LINE__)
+#define HPX_TEST_EQ(a, b) HPX_TEST_REL_(a, b, ==)
+#define HPX_TEST_NEQ(a, b) HPX_TEST_REL_(a, b, !=)
+#define HPX_TEST_LT(a, b) HPX_TEST_REL_(a, b, <)
+#define HPX_TEST_LTE(a, b) HPX_TEST_REL_(a, b, <=)
 #define HPX_TEST_EQ_MSG(a, b, msg) HPX_TEST_MSG((a) == (b), msg)

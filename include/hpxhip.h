@@ -191,6 +191,7 @@ int hpxhip_free(void* ptr);
 int hpxhip_malloc_host(void** ptr, size_t bytes); /* pinned */
 int hpxhip_free_host(void* ptr);
 int hpxhip_mem_info(int device, size_t* free_bytes, size_t* total_bytes);
+
 int hpxhip_memcpy_async(void* dst, const void* src, size_t bytes, int kind, hpxhip_stream stream);
 int hpxhip_memcpy_peer_async(void* dst, int dst_device, const void* src, int src_device,
                              size_t bytes, hpxhip_stream stream);

@@ -113,11 +113,15 @@ void test_futures(executor_type& exec) {
     auto twice = s.then([](hpx::future<double>& x) { return 2.0 * x.get(); });
     HPX_TEST_EQ(twice.get(), 14.0 * double(n));
 
-    // target future: ready once all queued work is done
-    hpx::parallel::for_each(pol, c.begin(), c.end(), fn::multiply_step<double>{0.5});
-    auto tgt_done = dexec.target().get_future();
+    // target future: ready once all work queued on that target's stream is
+    // done.  The policy holds its own copy of the executor (and so of the
+    // target, with its own stream, cuda_target.cpp:203-211): the kernel runs
+    // on pol's stream, so that is the target whose future orders the read.
+    auto fe = hpx::parallel::for_each(pol, c.begin(), c.end(), fn::multiply_step<double>{0.5});
+    auto tgt_done = pol.executor().target().get_future();
     tgt_done.get();
     HPX_TEST(tgt_done.is_ready());
+    fe.get();
     HPX_TEST_EQ(double(c[0]), 3.5);
 
     // when_all over futures of independent reductions

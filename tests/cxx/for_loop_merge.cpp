@@ -1,8 +1,10 @@
 // C++ port of tests/unit/computeapi/cuda/for_loop_compute.cu:28-118 on the
 // HIP backend (two targets, `for_loop_n(par.on(exec), A, N, induction(B),
 // induction(C), *C = *A + 3.0 * *B)`, checked element by element against the
-// host transform), plus hpx::parallel::merge (merge.hpp:476) against
-// std::merge, ascending and descending, sync and task policies.
+// host transform), strided inductions, for_loop reductions
+// (for_loop_reduction.cpp) and for_loop_strided (for_loop_strided.cpp), task
+// policies on inline temporaries, plus hpx::parallel::merge (merge.hpp:476)
+// against std::merge, ascending and descending, sync and task policies.
 #include <hpx/hpx.hpp>
 #include <hpx/hpx_init.hpp>
 #include <hpx/util/lightweight_test.hpp>
@@ -59,6 +61,155 @@ void test_for_loop(std::mt19937& gen, int N) {
     std::vector<int> h_D = to_host(d_D);
     for (int i = 0; i < N; ++i) HPX_TEST_EQ(h_D[i], h_A[i] + 5);
 
+    // strided induction (for_loop_induction.hpp:210-219): *C = *A + 3.0 * B[2i]
+    if (N >= 2) {
+        int M = N / 2;
+        dvec<int> d_E(M, allocA);
+        hpx::parallel::for_loop_n(ex::par.on(exec), d_A.begin(), M, hpx::parallel::induction(d_B.begin(), 2),
+                                  hpx::parallel::induction(d_E.begin()), body);
+        std::vector<int> h_E = to_host(d_E);
+        for (int i = 0; i < M; ++i) HPX_TEST_EQ(h_E[i], static_cast<int>(h_A[i] + 3.0 * h_B[2 * i]));
+    }
+}
+
+// for_loop_reduction.cpp:20-140 restated over device iterators: 10007 size_t
+// iotas from a random start, `r op= *it`, checked against std::accumulate.
+// Every task-form call passes its policy as an inline temporary
+// (`par(task).on(exec)`): the temporary's target copy, and with it its stream,
+// is gone before get() -- the result must not depend on it.
+void test_for_loop_reduction(std::mt19937& gen) {
+    using T = std::uint64_t;
+    std::vector<T> c(10007);
+    std::iota(c.begin(), c.end(), T(gen()));
+    hip::target t;
+    hip::allocator<T> alloc(t);
+    dvec<T> d(c.size(), alloc);
+    hpx::parallel::copy(ex::par, c.begin(), c.end(), d.begin());
+    hip::default_executor exec(t);
+    fn::loop_accumulate<1, fn::identity, 0> body{};
+
+    T sum = 0;
+    hpx::parallel::for_loop(ex::par.on(exec), d.begin(), d.end(), hpx::parallel::reduction_plus(sum), body);
+    HPX_TEST_EQ(sum, std::accumulate(c.begin(), c.end(), T(0)));
+
+    T prod = 1;
+    hpx::future<void> f = hpx::parallel::for_loop(ex::par(ex::task).on(exec), d.begin(), d.end(),
+                                                  hpx::parallel::reduction_multiplies(prod), body);
+    f.wait();  // the live-out is final once the future is ready (for_loop_reduction.hpp:60-66)
+    HPX_TEST_EQ(prod, std::accumulate(c.begin(), c.end(), T(1), std::multiplies<T>()));
+    f.get();
+
+    // many task-form reductions in flight on temporaries, read in reverse
+    std::vector<T> sums(64, 0);
+    std::vector<hpx::future<void>> fs;
+    for (std::size_t k = 0; k < sums.size(); ++k) {
+        sums[k] = k;
+        fs.push_back(hpx::parallel::for_loop_n(ex::par(ex::task).on(hip::default_executor(t)), d.begin(),
+                                               c.size() - k, hpx::parallel::reduction_plus(sums[k]), body));
+    }
+    for (std::size_t k = fs.size(); k-- > 0;) {
+        fs[k].get();
+        HPX_TEST_EQ(sums[k], std::accumulate(c.begin(), c.end() - k, T(k)));
+    }
+
+    std::shuffle(c.begin(), c.end(), gen);
+    hpx::parallel::copy(ex::par, c.begin(), c.end(), d.begin());
+    T mn = c[0], mx = c[0];
+    hpx::parallel::for_loop_n(ex::par.on(exec), d.begin(), c.size(), hpx::parallel::reduction_min(mn), body);
+    hpx::parallel::for_loop_n(ex::par.on(exec), d.begin(), c.size(), hpx::parallel::reduction_max(mx), body);
+    HPX_TEST_EQ(mn, *std::min_element(c.begin(), c.end()));
+    HPX_TEST_EQ(mx, *std::max_element(c.begin(), c.end()));
+
+    T x = 0;
+    hpx::parallel::for_loop_n(ex::par.on(exec), d.begin(), c.size(), hpx::parallel::reduction_bit_xor(x), body);
+    T xr = 0;
+    for (T v : c) xr ^= v;
+    HPX_TEST_EQ(x, xr);
+
+    // inner product: loop iterator and an induction feed a binary body
+    std::vector<T> e(c.size(), T(3));
+    dvec<T> de(e.size(), alloc);
+    hpx::parallel::copy(ex::par, e.begin(), e.end(), de.begin());
+    T ip = 5;
+    fn::loop_accumulate<2, fn::multiply, 0, 1> dot{};
+    hpx::parallel::for_loop_n(ex::par.on(exec), d.begin(), c.size(), hpx::parallel::induction(de.begin()),
+                              hpx::parallel::reduction_plus(ip), dot);
+    HPX_TEST_EQ(ip, std::inner_product(c.begin(), c.end(), e.begin(), T(5)));
+}
+
+// Task-form reduce / transform_reduce / copy_if with inline temporary
+// policies; the futures are read after the temporaries (and their streams)
+// are gone, and after unrelated work reused the pooled streams.
+void test_task_temporaries(std::mt19937& gen) {
+    using T = std::int64_t;
+    std::uniform_int_distribution<T> dis(-1000, 1000);
+    std::vector<T> h(100003);
+    for (auto& x : h) x = dis(gen);
+    hip::target t;
+    hip::allocator<T> alloc(t);
+    dvec<T> d(h.size(), alloc), out(h.size(), alloc);
+    hpx::parallel::copy(ex::par, h.begin(), h.end(), d.begin());
+
+    std::vector<hpx::future<T>> rs;
+    std::vector<hpx::future<hpx::parallel::util::tagged_pair<dvec<T>::iterator, dvec<T>::iterator>>> cs;
+    for (int k = 0; k < 16; ++k) {
+        rs.push_back(hpx::parallel::reduce(ex::par(ex::task).on(hip::default_executor(t)), d.begin(), d.end() - k,
+                                           T(k)));
+        rs.push_back(hpx::parallel::transform_reduce(ex::par(ex::task).on(hip::default_executor(t)), d.begin(),
+                                                     d.end(), T(0), std::plus<T>(), fn::square{}));
+    }
+    // copy_if into one output buffer: the temporaries are created one after
+    // another, each hands its stream back to the device pool as it dies and
+    // the next takes it again, so the four compactions are stream-ordered
+    for (int k = 0; k < 4; ++k)
+        cs.push_back(hpx::parallel::copy_if(ex::par(ex::task).on(hip::default_executor(t)), d.begin(), d.end(),
+                                            out.begin(), fn::greater_than<T>{T(100 * k)}));
+    T sq = 0;
+    for (T x : h) sq += x * x;
+    for (int k = 0; k < 16; ++k) {
+        HPX_TEST_EQ(rs[2 * k].get(), std::accumulate(h.begin(), h.end() - k, T(k)));
+        HPX_TEST_EQ(rs[2 * k + 1].get(), sq);
+    }
+    for (int k = 0; k < 4; ++k) {
+        auto r = cs[k].get();
+        auto expect = std::count_if(h.begin(), h.end(), [k](T x) { return x > T(100 * k); });
+        HPX_TEST_EQ(r.out() - out.begin(), static_cast<std::ptrdiff_t>(expect));
+    }
+    // the last copy_if's output is what the buffer holds
+    std::vector<T> ref;
+    std::copy_if(h.begin(), h.end(), std::back_inserter(ref), [](T x) { return x > T(300); });
+    std::vector<T> got = to_host(out);
+    got.resize(ref.size());
+    HPX_TEST(got == ref);
+}
+
+// for_loop_strided.cpp:29-74 restated: every stride-th element set to 42.
+void test_for_loop_strided(std::mt19937& gen) {
+    using T = std::uint64_t;
+    std::vector<T> c(10007);
+    std::iota(c.begin(), c.end(), T(1000));
+    hip::target t;
+    hip::allocator<T> alloc(t);
+    hip::default_executor exec(t);
+    for (int stride : {1, 2, 7, int(gen() % 100) + 1, 10007, 20000}) {
+        dvec<T> d(c.size(), alloc);
+        hpx::parallel::copy(ex::par, c.begin(), c.end(), d.begin());
+        fn::loop_assign<0, fn::affine<T>, 0> set42{{T(0), T(42)}};
+        hpx::parallel::for_loop_strided(ex::par.on(exec), d.begin(), d.end(), stride, set42);
+        std::vector<T> h = to_host(d);
+        for (std::size_t i = 0; i != h.size(); ++i) {
+            if (i % stride == 0) HPX_TEST_EQ(h[i], T(42));
+            else HPX_TEST_NEQ(h[i], T(42));
+        }
+        // same through a task policy on a temporary
+        hpx::parallel::copy(ex::par, c.begin(), c.end(), d.begin());
+        hpx::parallel::for_loop_strided(ex::par(ex::task).on(hip::default_executor(t)), d.begin(), d.end(), stride,
+                                        set42)
+            .get();
+        h = to_host(d);
+        for (std::size_t i = 0; i != h.size(); ++i)
+            if (i % stride == 0) HPX_TEST_EQ(h[i], T(42));
+    }
 }
 
 template <typename T, typename Comp>
@@ -89,6 +240,9 @@ void test_merge(std::mt19937& gen, std::size_t n1, std::size_t n2, Comp comp) {
 int hpx_main(int, char**) {
     std::mt19937 gen(42);
     for (int n : {100, 1, 4097, 1 << 20}) test_for_loop(gen, n);
+    test_for_loop_reduction(gen);
+    test_task_temporaries(gen);
+    test_for_loop_strided(gen);
     test_merge<int64_t>(gen, 10007, 5003, std::less<int64_t>());
     test_merge<uint32_t>(gen, 1 << 20, (1 << 19) + 3, std::greater<uint32_t>());
     test_merge<double>(gen, 4096, 0, std::less<double>());

@@ -67,6 +67,7 @@ void f(hpx::compute::vector<int>& a) {
     ("algorithms_known_answer", ["20260101"]),
     ("stream_hip", ["--vector_size", str(1 << 26), "--iterations", "10"]),
     ("for_loop_merge", []),
+    ("device_closures", ["4242"]),
 ])
 def test_cxx_program(prog, args):
     exe = os.path.join(BIN, prog)
