@@ -83,7 +83,11 @@ struct tile_state {
     // Called by ALL 64 lanes of one wave; returns the exclusive prefix of
     // `tile` (op-combination of every predecessor's elements) on every lane.
     // Requires tile > 0 and that tile 0 publishes an inclusive value.
-    template <typename Op>
+    // Each round reads 64*K predecessors (lane l reads slots pred-l-64k, k <
+    // K, all loads in flight together): with ~256 tiles in flight at once
+    // (one per CU) a 64-wide window can need several round trips before it
+    // meets an inclusive value, each costing a hand-off latency.
+    template <typename Op, int K = 1>
     __device__ __forceinline__ T exclusive_prefix(uint64_t tile, Op op) const {
         const T id = Op::template identity<T>();
         const int lane = lane_id();
@@ -91,13 +95,24 @@ struct tile_state {
         int64_t pred = static_cast<int64_t>(tile) - 1;
         uint32_t spins = 0;
         while (true) {
-            const int64_t j = pred - lane;
-            T v = id;
-            uint32_t f = TILE_INCLUSIVE;  // j < 0: behind tile 0, never reached
-            if (j >= 0) f = read(static_cast<uint64_t>(j), &v);
-            while (!__all(f != TILE_INVALID)) {
+            T v[K];
+            uint32_t f[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int64_t j = pred - lane - k * kWave;
+                v[k] = id;
+                f[k] = TILE_INCLUSIVE;  // j < 0: behind tile 0, never reached
+                if (j >= 0) f[k] = read(static_cast<uint64_t>(j), &v[k]);
+            }
+            while (true) {
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < K; ++k) ok = ok && f[k] != TILE_INVALID;
+                if (__all(ok)) break;
                 __builtin_amdgcn_s_sleep(1);
-                if (f == TILE_INVALID) f = read(static_cast<uint64_t>(j), &v);
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (f[k] == TILE_INVALID) f[k] = read(static_cast<uint64_t>(pred - lane - k * kWave), &v[k]);
                 if (++spins > kSpinLimit) {
                     if (lane == 0 && err)
                         __hip_atomic_store(err, HPXHIP_DEVERR_LOOKBACK_TIMEOUT, __ATOMIC_RELAXED,
@@ -105,13 +120,20 @@ struct tile_state {
                     return excl;
                 }
             }
-            const uint64_t inclusive_lanes = __ballot(f == TILE_INCLUSIVE);
-            const int first = inclusive_lanes ? __builtin_ctzll(inclusive_lanes) : kWave;
-            if (lane > first) v = id;
-            const T s = wave_reduce(v, op);
-            excl = op(s, excl);
-            if (first < kWave) break;
-            pred -= kWave;
+            // Predecessors in order of distance: slot (k, lane) is pred - lane - 64k.
+            bool found = false;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (found) break;  // wave-uniform
+                const uint64_t inclusive_lanes = __ballot(f[k] == TILE_INCLUSIVE);
+                const int first = inclusive_lanes ? __builtin_ctzll(inclusive_lanes) : kWave;
+                T w = lane > first ? id : v[k];
+                const T s = wave_reduce(w, op);
+                excl = op(s, excl);
+                found = first < kWave;
+            }
+            if (found) break;
+            pred -= K * kWave;
         }
         return excl;
     }

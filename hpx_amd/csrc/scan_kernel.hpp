@@ -42,7 +42,7 @@ constexpr uint64_t tile_elems() {
 // Wave 0 of a tile: scans the WAVES wave totals in s_wave_total with DPP,
 // publishes the tile (aggregate, look-back, inclusive) and leaves in
 // s_wave_total[w] the tile prefix (op) the exclusive prefix of wave w.
-template <typename T, typename Op, int WAVES, bool LOOKBACK>
+template <typename T, typename Op, int WAVES, bool LOOKBACK, int LBK = 1>
 __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& st, Op op, const T* prefix_dev, T init,
                                             T* s_wave_total) {
     const T id = Op::template identity<T>();
@@ -58,7 +58,7 @@ __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& 
     } else {
         if constexpr (LOOKBACK) {
             if (lane == 0) st.publish(tile, agg, TILE_AGGREGATE);
-            p = st.exclusive_prefix(tile, op);
+            p = st.template exclusive_prefix<Op, LBK>(tile, op);
             if (lane == 0) st.publish(tile, op(p, agg), TILE_INCLUSIVE);
         } else {
             p = id;  // ablation only: measures the pass without the tile hand-off
@@ -68,7 +68,7 @@ __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& 
 }
 
 template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED, int ROUNDS = kRounds,
-          int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false>
+          int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false, int LBK = 1>
 __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init,
                                                    const T* prefix_dev, uint32_t* counter, tile_state<T> st) {
     constexpr int V = 16 / sizeof(T);
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
         const T wt = wave_reduce(lt, op);
         if (lane == 0) s_wave_total[wave] = wt;
         __syncthreads();
-        if (wave == 0) tile_prefix<T, Op, WAVES, LOOKBACK>(tile, st, op, prefix_dev, init, s_wave_total);
+        if (wave == 0) tile_prefix<T, Op, WAVES, LOOKBACK, LBK>(tile, st, op, prefix_dev, init, s_wave_total);
     }
 
     // ---- per-round lane scan + wave scan; x becomes the wave-local result
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
     if constexpr (!EARLY) {
         if (lane == 0) s_wave_total[wave] = carry;
         __syncthreads();
-        if (wave == 0) tile_prefix<T, Op, WAVES, LOOKBACK>(tile, st, op, prefix_dev, init, s_wave_total);
+        if (wave == 0) tile_prefix<T, Op, WAVES, LOOKBACK, LBK>(tile, st, op, prefix_dev, init, s_wave_total);
     }
     __syncthreads();
     const T pre = s_wave_total[wave];
