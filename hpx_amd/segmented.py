@@ -48,6 +48,69 @@ def partition_bounds(n: int, parts: int, k: int):
     return b, min(n, b + part)
 
 
+def rank_partitions(k: int, p: int, r: int):
+    """[first, last) partition indices held by rank r when k partitions are
+    spread over p ranks: contiguous blocks of ceil(k/p), in rank order (the
+    reference's bulk_create hands locality l a contiguous run of
+    ceil(k/L) partition ids, default_distribution_policy.hpp:294-324, and
+    numbers partitions in locality order, partitioned_vector_impl.hpp:331-
+    372).  Where the reference's count rule degenerates (k < L gives no
+    partition at all, and some k > L give the last locality a negative
+    count) the runs are clipped at k instead: later ranks may hold none."""
+    c = -(-k // p) if p else 0
+    a = min(k, r * c)
+    return a, min(k, a + c)
+
+
+class container_distribution_policy:
+    """hpx::container_distribution_policy (container_distribution_policy.hpp:
+    31-142); the module-level instance ``container_layout`` = one partition
+    per rank, ``container_layout(k)`` = k partitions over the ranks."""
+
+    def __init__(self, num_partitions: int | None = None):
+        self.num_partitions = None if num_partitions is None else int(num_partitions)
+        if self.num_partitions is not None and self.num_partitions < 1:
+            raise ValueError("container_layout: at least one partition")
+
+    def __call__(self, num_partitions: int):
+        return container_distribution_policy(num_partitions)
+
+    def partitions(self, ranks: int) -> int:
+        return ranks if self.num_partitions is None else self.num_partitions
+
+
+container_layout = container_distribution_policy()
+
+
+class layout_map:
+    """A partitioned_vector's resolved layout: n elements in k partitions of
+    ceil(n/k) (partitioned_vector_impl.hpp:325), partitions in contiguous
+    runs per rank, so every rank's elements are one contiguous range."""
+
+    def __init__(self, n: int, k: int, p: int):
+        self.n, self.k, self.p = int(n), int(k), int(p)
+
+    def segment_bounds(self, j: int):
+        return partition_bounds(self.n, self.k, j)
+
+    def rank_segments(self, r: int):
+        return rank_partitions(self.k, self.p, r)
+
+    def rank_bounds(self, r: int):
+        j0, j1 = self.rank_segments(r)
+        if j0 >= j1:
+            pos = self.segment_bounds(j0)[0] if j0 < self.k else self.n
+            return pos, pos
+        return self.segment_bounds(j0)[0], self.segment_bounds(j1 - 1)[1]
+
+    def max_segments(self) -> int:
+        return max(b - a for a, b in (self.rank_segments(r) for r in range(self.p)))
+
+    def same_ranges(self, other) -> bool:
+        return self.n == other.n and self.p == other.p and all(
+            self.rank_bounds(r) == other.rank_bounds(r) for r in range(self.p))
+
+
 # ----------------------------------------------------------------- comms
 HALO_MAX = L.STENCIL_MAX_FUSED  # widest 1d_stencil halo (points per side)
 
@@ -66,9 +129,16 @@ class LocalComm:
 
     def slots(self, nbytes: int):
         """(send_ptr, recv_ptr) device buffers for one all-gather."""
-        if self._buf is None:
-            self._buf = vector(64, dtype=np.uint64, tgt=self.tgt)
+        words = max(64, -(-int(nbytes) // 8))
+        if self._buf is None or self._buf.size() < words:
+            self._buf = vector(words, dtype=np.uint64, tgt=self.tgt)
         return self._buf.data(), self._buf.data()  # recv[0] == send
+
+    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream, recv_off=0):
+        n = int(send_counts[0])
+        if n:
+            L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_buf.data() + recv_off * itemsize),
+                   ctypes.c_void_p(send_buf.data() + send_off * itemsize), n * itemsize, L.D2D, stream)
 
     def allgather(self, nbytes: int, stream):
         return None
@@ -124,12 +194,16 @@ class TorchComm:
                                               device=self.device)
 
     def slots(self, nbytes: int):
+        words = max(1, -(-int(nbytes) // 8))
+        if self._send.numel() < words:
+            self._send = self.torch.zeros(words, dtype=self.torch.int64, device=self.device)
+            self._recv = self.torch.zeros(words * self.size, dtype=self.torch.int64, device=self.device)
         return self._send.data_ptr(), self._recv.data_ptr()
 
     def allgather(self, nbytes: int, stream):
         """Packed all-gather: recv bytes [r*nbytes, (r+1)*nbytes) <- rank r's
-        send[0:nbytes] (nbytes a multiple of 8, at most 64), so the segment
-        values sit contiguously for hpxhip_fold."""
+        send[0:nbytes] (nbytes a multiple of 8, sized by slots()), so the
+        segment values sit contiguously for hpxhip_fold."""
         words = max(1, nbytes // 8)
         with self.torch.cuda.stream(self._stream(stream)):
             self.dist.all_gather_into_tensor(self._recv[:self.size * words], self._send[:words])
@@ -154,14 +228,14 @@ class TorchComm:
                                         "version": 2, "strides": None}
         return self.torch.as_tensor(_cai(), device=self.device)
 
-    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream):
+    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream, recv_off=0):
         """RCCL all-to-all with uneven splits: send_counts[j] elements from
         send_buf[send_off:] go to rank j (in rank order); recv_counts[i]
-        elements from rank i land in recv_buf in rank order."""
+        elements from rank i land in recv_buf[recv_off:] in rank order."""
         sb = [int(c) * itemsize for c in send_counts]
         rb = [int(c) * itemsize for c in recv_counts]
         src = self._bytes_view(send_buf.data() + send_off * itemsize, max(1, sum(sb)))[:sum(sb)]
-        dst = self._bytes_view(recv_buf.data(), max(1, sum(rb)))[:sum(rb)]
+        dst = self._bytes_view(recv_buf.data() + recv_off * itemsize, max(1, sum(rb)))[:sum(rb)]
         with self.torch.cuda.stream(self._stream(stream)):
             self.dist.all_to_all_single(dst, src, rb, sb)
 
@@ -213,6 +287,19 @@ class HipEngine:
         L.call("hpxhip_scan", dt, op.kind, 1 if inclusive else 0, conv.kind, L.scalars_buf(dt, conv.scalars),
                L.scalar_buf(dt, 0), ctypes.c_void_p(prefix_ptr), ctypes.c_void_p(src.data() + lo * src.value_size),
                ctypes.c_void_p(dst.data() + dlo * dst.value_size), hi - lo, self.stream, None, 0)
+
+    def transform(self, pol, pv, lo, hi, dst, dlo, f):
+        """dst[dlo + i] = f(pv.local[lo + i]) on the partition's executor."""
+        from . import algorithms as A
+        A.transform((pol or _par()).on(_exec(pv)), pv.local.begin() + lo, pv.local.begin() + hi, dst.begin() + dlo, f)
+
+    def word(self, ptr, i):
+        """The i-th 8-byte slot of a device slot array."""
+        return ptr + 8 * int(i)
+
+    def put(self, ptr, dt, value):
+        """Store one dt value into a device slot (stream-ordered)."""
+        L.call("hpxhip_fill", dt, L.scalar_buf(dt, value), ctypes.c_void_p(ptr), 1, self.stream)
 
     def read(self, ptr, dt):
         out = np.empty(1, np_dtype(dt))
@@ -356,7 +443,7 @@ def _from_ordered(u, dt, descending):
 def _identity(kind, dt):
     isint = np_dtype(dt).kind in "iu"
     info = np.iinfo(np_dtype(dt)) if isint else None
-    return {L.PLUS: 0, L.MULTIPLIES: 1,
+    return {L.PLUS: (0 if isint else -0.0), L.MULTIPLIES: 1,
             L.MIN: (info.max if isint else float("inf")), L.MAX: (info.min if isint else float("-inf")),
             L.BIT_AND: (-1 if np_dtype(dt).kind == "i" else (info.max if isint else 0)), L.BIT_OR: 0,
             L.BIT_XOR: 0}[kind]
@@ -364,17 +451,28 @@ def _identity(kind, dt):
 
 # -------------------------------------------------------- partitioned_vector
 class partitioned_vector:
-    """hpx::partitioned_vector<T> with one partition per rank (container_layout
-    over the ranks, partitioned_vector_impl.hpp:317-395)."""
+    """hpx::partitioned_vector<T> over the ranks (partitioned_vector_decl.hpp:
+    146-405): ``layout`` = container_layout (one partition per rank, the
+    default) or container_layout(k) (k partitions, each rank holding a
+    contiguous run of them, rank_partitions).  A rank stores all its
+    partitions in ONE device vector (its elements are contiguous); the
+    segmented algorithms still work partition by partition where the
+    reference's results depend on it (segment-order folds and carries)."""
 
-    def __init__(self, n: int, dtype=np.float64, value=None, comm=None, tgt: target | None = None):
+    def __init__(self, n: int, dtype=np.float64, value=None, comm=None, tgt: target | None = None, layout=None):
         self.tgt = tgt or (comm.tgt if comm is not None and hasattr(comm, "tgt") else target(0))
         self.comm = comm or LocalComm(self.tgt)
         self.n = int(n)
         self.dtype = dtype_code(dtype)
-        self.rank, self.parts = self.comm.rank, self.comm.size
-        self.lo, self.hi = partition_bounds(self.n, self.parts, self.rank)
+        self._set_layout(layout)
         self.local = vector(self.hi - self.lo, dtype=self.dtype, value=value, tgt=self.tgt)
+
+    def _set_layout(self, layout=None):
+        layout = layout if layout is not None else container_layout
+        self.rank = self.comm.rank
+        self.layout = layout_map(self.n, layout.partitions(self.comm.size), self.comm.size)
+        self.parts = self.layout.k
+        self.lo, self.hi = self.layout.rank_bounds(self.rank)
 
     def size(self) -> int:
         return self.n
@@ -386,7 +484,11 @@ class partitioned_vector:
         return self.parts
 
     def segment_bounds(self, k: int):
-        return partition_bounds(self.n, self.parts, k)
+        return self.layout.segment_bounds(k)
+
+    def my_segments(self):
+        """[first, last) partition indices this rank holds."""
+        return self.layout.rank_segments(self.rank)
 
     def begin(self):
         return segmented_iterator(self, 0)
@@ -395,7 +497,7 @@ class partitioned_vector:
         return segmented_iterator(self, self.n)
 
     def local_range(self, first: int, last: int):
-        """Intersection of global [first, last) with this rank's partition,
+        """Intersection of global [first, last) with this rank's elements,
         as local indices."""
         a, b = max(first, self.lo), min(last, self.hi)
         return (a - self.lo, b - self.lo) if a < b else (0, 0)
@@ -469,29 +571,101 @@ class segmented:
                    ctypes.c_void_p(pv.local.data() + lo * pv.local.value_size), hi - lo, pv.tgt.stream)
         return last
 
+    # --- where a rank's results go in the destination partitioned_vector
+    def _dest_plan(self, pv, a, b, pd, d0):
+        """Output of input index i (in [a, b)) is pd index d0 + (i - a).
+        Returns (direct, ia, ib, send, recv, recv_at): direct when every
+        rank's outputs fall in its own part of pd (then they are written in
+        place at pd-local index ia - a + d0 - pd.lo); otherwise the counts of
+        an all-to-all that moves each rank's results to their owners."""
+        if pd.n < d0 + (b - a):
+            raise ValueError("segmented algorithm: destination range past the end of the partitioned_vector")
+        p = pv.comm.size
+        def in_range(r):
+            lo, hi = pv.layout.rank_bounds(r)
+            return max(lo, a), max(max(lo, a), min(hi, b))
+        out_ranges = [(x - a + d0, y - a + d0) for x, y in (in_range(r) for r in range(p))]
+        direct = all(y <= x or (pd.layout.rank_bounds(r)[0] <= x and y <= pd.layout.rank_bounds(r)[1])
+                     for r, (x, y) in enumerate(out_ranges))
+        ia, ib = in_range(pv.rank)
+        if direct:
+            return True, ia, ib, None, None, ia - a + d0 - pd.lo
+        oa, ob = out_ranges[pv.rank]
+        def overlap(x, y, r):
+            lo, hi = pd.layout.rank_bounds(r)
+            return max(0, min(y, hi) - max(x, lo))
+        send = [overlap(oa, ob, q) for q in range(p)]
+        recv = [overlap(x, y, pd.rank) for (x, y) in out_ranges]
+        firsts = [max(x, pd.lo) for (x, y) in out_ranges if overlap(x, y, pd.rank)]
+        recv_at = (min(firsts) - pd.lo) if firsts else 0
+        return False, ia, ib, send, recv, recv_at
+
+    def _finish_dest(self, eng, comm, plan, tmp, pd):
+        """Move non-direct results (tmp, this rank's outputs in order) to
+        their owners: one all-to-all with uneven splits (RCCL on the GPU)."""
+        _, _, _, send, recv, recv_at = plan
+        comm.alltoallv(tmp, 0, send, pd.local, recv, np_dtype(pd.dtype).itemsize, eng.stream, recv_off=recv_at)
+        eng.release(tmp)
+
     def transform(self, pol, first, last, dest, f):
         pv, a, b = _range(first, last)
-        pd, d0, _ = _range(dest, dest + (b - a)) if isinstance(dest, segmented_iterator) else (dest, 0, 0)
-        if pd.n != pv.n or d0 != a:
-            raise ValueError("segmented transform needs identically partitioned source and destination ranges")
-        lo, hi = pv.local_range(a, b)
-        from . import algorithms as A
-        if hi > lo:
-            A.transform(pol.on(_exec(pv)), pv.local.begin() + lo, pv.local.begin() + hi, pd.local.begin() + lo, f)
+        pd, d0, _ = _range(dest, dest + (b - a))
+        eng, comm = self.engine(pv), pv.comm
+        plan = self._dest_plan(pv, a, b, pd, d0)
+        direct, ia, ib, _, _, at = plan
+        lo, hi = ia - pv.lo, ib - pv.lo
+        if direct:
+            if hi > lo:
+                eng.transform(pol, pv, lo, hi, pd.local, at, f)
+        else:
+            tmp = eng.buffer(pd.local, hi - lo)
+            if hi > lo:
+                eng.transform(pol, pv, lo, hi, tmp, 0, f)
+            self._finish_dest(eng, comm, plan, tmp, pd)
         return dest + (b - a)
 
     def transform_binary(self, pol, first1, last1, first2, dest, f):
         pv, a, b = _range(first1, last1)
         p2, a2, _ = _range(first2, first2 + (b - a))
         pd, d0, _ = _range(dest, dest + (b - a))
-        if not (p2.n == pv.n == pd.n and a2 == a == d0):
-            raise ValueError("segmented transform needs identically partitioned ranges")
-        lo, hi = pv.local_range(a, b)
+        if not (p2.layout.same_ranges(pv.layout) and a2 == a):
+            raise ValueError("segmented binary transform: both inputs must be laid out alike")
+        eng, comm = self.engine(pv), pv.comm
+        plan = self._dest_plan(pv, a, b, pd, d0)
+        direct, ia, ib, _, _, at = plan
         from . import algorithms as A
+        lo, hi = ia - pv.lo, ib - pv.lo
+        out = pd.local.begin() + at if direct else None
+        tmp = None if direct else eng.buffer(pd.local, hi - lo)
         if hi > lo:
             A.transform(pol.on(_exec(pv)), pv.local.begin() + lo, pv.local.begin() + hi, p2.local.begin() + lo,
-                        pd.local.begin() + lo, f)
+                        out if direct else tmp.begin(), f)
+        if not direct:
+            self._finish_dest(eng, comm, plan, tmp, pd)
         return dest + (b - a)
+
+    # --- per-segment totals of [a, b), all-gathered in segment order
+    def _segment_totals(self, pv, a, b, op, conv, adt, eng, comm):
+        """S_j = the op-combination of conv(x) over segment j of [a, b)
+        (detail/reduce.hpp:43-62: no init), for this rank's partitions, into
+        consecutive 8-byte send slots padded with op's identity to the
+        largest per-rank partition count; one all-gather.  Returns (recv,
+        slots per rank): segment j of rank r sits at r*slots + (j - first)."""
+        j0, j1 = pv.my_segments()
+        cmax = max(1, pv.layout.max_segments())
+        send, recv = comm.slots(8 * cmax)
+        ident = _identity(op.kind, adt)
+        for i in range(cmax):
+            slot = eng.word(send, i)
+            if j0 + i < j1:
+                s0, s1 = pv.segment_bounds(j0 + i)
+                lo, hi = pv.local_range(max(s0, a), min(s1, b))
+                if hi > lo:
+                    eng.reduce_into(pv.local, lo, hi, op, conv, adt, slot)
+                    continue
+            eng.put(slot, adt, ident)
+        comm.allgather(8 * cmax, eng.stream)
+        return recv, cmax
 
     # --- reduce (segmented_algorithms/reduce.hpp:112-209)
     def transform_reduce(self, pol, first, last, init, red_op, conv_op):
@@ -501,12 +675,9 @@ class segmented:
         eng, comm = self.engine(pv), pv.comm
         from .algorithms import _acc_dtype, _slots_for
         adt = _acc_dtype(pv.dtype, init)
-        send, recv = comm.slots(8)
-        lo, hi = pv.local_range(a, b)
-        eng.reduce_into(pv.local, lo, hi, red_op, conv_op, adt, send)  # S_k (identity if empty)
-        comm.allgather(8, eng.stream)                                    # one RCCL all-gather of 8 B
+        recv, cmax = self._segment_totals(pv, a, b, red_op, conv_op, adt, eng, comm)  # S_k, one all-gather
         dev, _ = _slots_for(pv.tgt).next() if isinstance(eng, HipEngine) else (eng.scratch(), None)
-        eng.fold(adt, red_op, init, recv, comm.size, dev)                # init (op) S_0 (op) ... in order
+        eng.fold(adt, red_op, init, recv, comm.size * cmax, dev)         # init (op) S_0 (op) ... in order
         if getattr(pol, "is_task", False):
             # par(task): future<T> resolved by the stream, no host round trip
             # inside the pipeline (segmented_algorithms/reduce.hpp:112-209
@@ -529,22 +700,39 @@ class segmented:
         conv = F.require(conv, F.Unary, "segmented scan")
         pv, a, b = _range(first, last)
         pd, d0, _ = _range(dest, dest + (b - a))
-        if pd.n != pv.n or d0 != a:
-            raise ValueError("segmented scan needs identically partitioned input and output ranges")
+        if pd.dtype != pv.dtype:
+            raise TypeError("segmented scan: input and output element types must match")
         eng, comm = self.engine(pv), pv.comm
-        lo, hi = pv.local_range(a, b)
-        send, recv = comm.slots(8)
+        plan = self._dest_plan(pv, a, b, pd, d0)
+        direct, ia, ib, _, _, at = plan
         from .algorithms import _slots_for
-        if comm.size > 1:
-            eng.reduce_into(pv.local, lo, hi, op, conv, pv.dtype, send)       # step 1: segment totals
-            comm.allgather(8, eng.stream)
-            carry = _slots_for(pv.tgt).next()[0] if isinstance(eng, HipEngine) else eng.scratch()
-            eng.fold(pv.dtype, op, init, recv, comm.rank, carry)              # carries in segment order
+        def carry_slot():
+            return _slots_for(pv.tgt).next()[0] if isinstance(eng, HipEngine) else eng.scratch()
+        lo0 = ia - pv.lo                       # my first input element (local index)
+        out, out0 = (pd.local, at) if direct else (eng.buffer(pd.local, ib - ia), 0)
+        if pv.parts == 1:
+            # one segment on one rank: the carry is init itself
+            carry = carry_slot()
+            send, recv = comm.slots(8)
+            eng.fold(pv.dtype, op, init, recv, 0, carry)
+            if ib > ia:
+                eng.scan(pv.local, lo0, ib - pv.lo, out, out0, op, conv, inclusive, carry)
         else:
-            carry = _slots_for(pv.tgt).next()[0] if isinstance(eng, HipEngine) else eng.scratch()
-            eng.fold(pv.dtype, op, init, recv, 0, carry)                      # = init
-        if hi > lo:
-            eng.scan(pv.local, lo, hi, pd.local, lo, op, conv, inclusive, carry)  # step 2 with init = carry
+            # step 1: segment totals in segment order; carry_j = init (op)
+            # S_0 (op) ... (op) S_{j-1} (detail/scan.hpp:667-677), folded on
+            # the device; step 2: each segment scanned with its carry.
+            recv, cmax = self._segment_totals(pv, a, b, op, conv, pv.dtype, eng, comm)
+            j0, j1 = pv.my_segments()
+            for i, j in enumerate(range(j0, j1)):
+                s0, s1 = pv.segment_bounds(j)
+                lo, hi = pv.local_range(max(s0, a), min(s1, b))
+                if hi <= lo:
+                    continue
+                carry = carry_slot()
+                eng.fold(pv.dtype, op, init, recv, comm.rank * cmax + i, carry)
+                eng.scan(pv.local, lo, hi, out, out0 + (lo - lo0), op, conv, inclusive, carry)
+        if not direct:
+            self._finish_dest(eng, comm, plan, out, pd)
         return dest + (b - a)
 
     def inclusive_scan(self, pol, first, last, dest, op=F.plus, init=0):
@@ -589,7 +777,7 @@ class segmented:
             return segmented_iterator(pv, pv.n)
         bits = 8 * np_dtype(dt).itemsize
         ut = np.uint64 if bits == 64 else np.uint32
-        targets = np.array([partition_bounds(pv.n, p, j)[0] for j in range(1, p)], np.int64)
+        targets = np.array([pv.layout.rank_bounds(j)[0] for j in range(1, p)], np.int64)
         prefix = np.zeros(p - 1, ut)
         digits = np.arange(256, dtype=ut)
         for rnd in range(bits // 8):
@@ -660,6 +848,11 @@ def _read_words(eng, ptr, count, dt):
            eng.stream)
     L.call("hpxhip_stream_synchronize", eng.stream)
     return out
+
+
+def _par():
+    from .execution import par
+    return par
 
 
 def _exec(pv):

@@ -567,15 +567,24 @@ int oracle_segmented_scan(int dtype, int op_kind, int inclusive, const void* ini
         T* o = static_cast<T*>(out);
         std::vector<T> x(a, a + n);
         const uint64_t part = (n + parts - 1) / parts;
-        for (int p = 0; p < parts; ++p) {  // detail/scan.hpp:646-677
+        for (int p = 0; p < parts; ++p) {
             const uint64_t b = std::min<uint64_t>(n, p * part), e = std::min<uint64_t>(n, b + part);
+            if (b == e) continue;  // empty segments are skipped (detail/scan.hpp:602-624)
+            // step 1: the segment total, seeded by its first element
+            // (sequential_segmented_scan_T, detail/scan.hpp:46-59)
+            T total = x[b];
+            for (uint64_t i = b + 1; i < e; ++i) total = op(total, x[i]);
+            // step 2: the segment scanned from its carry (detail/scan.hpp:646-665)
             T acc = carry;
             for (uint64_t i = b; i < e; ++i) {
                 const T nxt = op(acc, x[i]);
                 o[i] = inclusive ? nxt : acc;
                 acc = nxt;
             }
-            carry = acc;
+            // step 3: next carry = carry (op) total (detail/scan.hpp:667-677;
+            // the sequential form, :409-429, applies op(total, carry), the
+            // same value for the commutative operators built here)
+            carry = op(carry, total);
         }
         return 0;
     });

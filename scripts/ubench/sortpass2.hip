@@ -82,11 +82,12 @@ int main() {
     }, n)
     for (int rep = 0; rep < 2; ++rep) {
         PASS(512, 16, 4);
-        PASS(1024, 16, 4);
-        PASS(1024, 16, 8);
-        PASS(512, 24, 4);
-        PASS(768, 16, 4);
-        PASS(1024, 16, 0);
+        PASS(256, 16, 4);
+        PASS(256, 24, 4);
+        PASS(256, 32, 4);
+        PASS(256, 8, 4);
+        PASS(512, 8, 4);
+        PASS(256, 16, 8);
     }
     uint32_t herr;
     CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));

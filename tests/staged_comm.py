@@ -41,6 +41,11 @@ class HostStagedComm:
 
     # reduce / scan / copy_if exchange
     def slots(self, nbytes):
+        import hpx_amd as hpx
+        words = max(1, -(-int(nbytes) // 8))
+        if self._send.size() < words:
+            self._send = hpx.vector(words, dtype=np.int64, tgt=self.tgt)
+            self._recv = hpx.vector(words * self.size, dtype=np.int64, tgt=self.tgt)
         return self._send.data(), self._recv.data()
 
     def allgather(self, nbytes, stream):
@@ -51,7 +56,7 @@ class HostStagedComm:
     def allgather_host(self, words):
         return np.stack(self._allgather_bytes(np.ascontiguousarray(words, np.int64).view(np.uint8))).view(np.int64)
 
-    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream):
+    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream, recv_off=0):
         import torch
         self.tgt.synchronize()
         n = int(sum(send_counts))
@@ -61,7 +66,7 @@ class HostStagedComm:
         self.dist.all_to_all_single(dst, src, [int(c) * itemsize for c in recv_counts],
                                     [int(c) * itemsize for c in send_counts])
         if dst.numel():
-            self._h2d(recv_buf.data(), dst.numpy())
+            self._h2d(recv_buf.data() + recv_off * itemsize, dst.numpy())
 
     def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream, count=1):
         from hpx_amd import _lib as L

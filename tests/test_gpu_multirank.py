@@ -45,6 +45,15 @@ def _worker(rank, size, port, q):
         alg.inclusive_scan(pol, x.begin(), x.end(), y.begin(), F.plus, 3)
         tgt.synchronize()
         res["scan"] = (y.lo, y.local.to_host())
+        # container_layout(5) over the two ranks, scan into a container_layout output
+        CL = S.container_layout
+        x5 = S.partitioned_vector(n, np.int64, comm=comm, tgt=tgt, layout=CL(5))
+        alg.generate(pol, x5.begin(), x5.end(), "range", 0x5EED, -1000, 1000)
+        res["reduce5"] = alg.reduce(pol, x5.begin(), x5.end(), 3, F.plus)
+        y2 = S.partitioned_vector(n, np.int64, comm=comm, tgt=tgt, layout=CL)
+        alg.inclusive_scan(pol, x5.begin(), x5.end(), y2.begin(), F.plus, 3)
+        tgt.synchronize()
+        res["scan5"] = (y2.lo, y2.local.to_host())
         for nx, nt in ((1 << 20, 6), (1001, 9)):
             init = np.random.default_rng(nx).standard_normal(nx)
             hs = S.heat_solver(nx, comm, tgt, init=init)
@@ -92,6 +101,9 @@ def test_two_ranks_on_gpu_segmented_sort_reduce_scan_stencil(gpu_target):
     assert all(results[r]["reduce"] == 3 + int(x.sum()) for r in range(size))
     got = np.concatenate([results[r]["scan"][1] for r in range(size)])
     np.testing.assert_array_equal(got, O.segmented_scan(x, 3, size, True))
+    assert all(results[r]["reduce5"] == 3 + int(x.sum()) for r in range(size))
+    got = np.concatenate([results[r]["scan5"][1] for r in range(size)])
+    np.testing.assert_array_equal(got, O.segmented_scan(x, 3, 5, True))
     for nx, nt in ((1 << 20, 6), (1001, 9)):
         init = np.random.default_rng(nx).standard_normal(nx)
         got = np.concatenate([results[r][("heat", nx)][1] for r in range(size)])

@@ -28,14 +28,25 @@ class GlooComm:
         self.rank, self.size = dist.get_rank(), dist.get_world_size()
 
     def slots(self, nbytes):
-        self._send = np.zeros(1, np.int64)
-        self._recv = np.zeros(self.size, np.int64)
+        w = max(1, nbytes // 8)
+        self._send = np.zeros(w, np.int64)
+        self._recv = np.zeros(self.size * w, np.int64)
         return self._send, self._recv
 
     def allgather(self, nbytes, stream):
-        out = [torch.zeros(1, dtype=torch.int64) for _ in range(self.size)]
-        dist.all_gather(out, torch.from_numpy(self._send.copy()))
-        self._recv[:] = [int(t.item()) for t in out]
+        w = max(1, nbytes // 8)
+        out = [torch.zeros(w, dtype=torch.int64) for _ in range(self.size)]
+        dist.all_gather(out, torch.from_numpy(self._send[:w].copy()))
+        self._recv[:self.size * w] = np.concatenate([t.numpy() for t in out])
+
+    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream, recv_off=0):
+        n = int(sum(send_counts))
+        src = torch.from_numpy(send_buf[send_off:send_off + n].view(np.uint8).copy())
+        dst = torch.zeros(int(sum(recv_counts)) * itemsize, dtype=torch.uint8)
+        dist.all_to_all_single(dst, src, [int(c) * itemsize for c in recv_counts],
+                               [int(c) * itemsize for c in send_counts])
+        m = int(sum(recv_counts))
+        recv_buf[recv_off:recv_off + m] = dst.numpy().view(recv_buf.dtype)
 
     def barrier(self):
         dist.barrier()
@@ -87,16 +98,89 @@ class NumpyEngine:
     def read_words(self, h, count, dt):
         return list(h[:count])
 
+    def word(self, arr, i):
+        return arr[i:]
+
+    def transform(self, pol, pv, lo, hi, dst, dlo, f):
+        dst[dlo:dlo + hi - lo] = [f(v) for v in pv.local[lo:hi]]
+
+    def put(self, slot, dt_code, value):
+        dt = {2: np.int64, 5: np.float64}[dt_code]
+        slot[0] = np.array([value], dt).view(np.int64)[0]
+
+    def buffer(self, like, n):
+        return np.zeros(max(1, n), like.dtype)
+
+    def release(self, buf):
+        pass
+
 
 class HostPV(S.partitioned_vector):
-    def __init__(self, glob, comm):
+    def __init__(self, glob, comm, layout=None):
         self.comm = comm
         self.tgt = None
         self.n = glob.size
         self.dtype = {np.dtype(np.int64): 2, np.dtype(np.float64): 5}[glob.dtype]
-        self.rank, self.parts = comm.rank, comm.size
-        self.lo, self.hi = S.partition_bounds(self.n, self.parts, self.rank)
+        self._set_layout(layout)
         self.local = glob[self.lo:self.hi].copy()
+
+
+def _gather(results, key, n, dtype=np.int64):
+    got = np.zeros(n, dtype)
+    for r in results:
+        lo, loc = results[r][key]
+        got[lo:lo + loc.size] = loc
+    return got
+
+
+def _layout_worker(rank, size, port, q):
+    """partitioned_vector_inclusive_scan.cpp:321-340 and
+    partitioned_vector_reduce.cpp:47-76 restated: container_layout,
+    container_layout(3), (1000), (10), and scans whose output has another
+    layout than the input."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        comm = GlooComm()
+        alg = S.segmented(NumpyEngine())
+        CL = S.container_layout
+        res = {}
+        n = 10007
+        ones = np.ones(n, np.int64)
+        x = O.generate(np.int64, "range", n, 0x5EED, -1000, 1000)
+        xf = O.generate(np.float64, "unit", n, 0x5EED)
+        for name, lay in (("default", CL), ("3", CL(3)), ("10", CL(10)), ("1000", CL(1000)), ("1", CL(1))):
+            pv = HostPV(ones, comm, lay)
+            res[("reduce_ones", name)] = alg.reduce(None, pv.begin(), pv.end(), 1, F.plus)
+            pf = HostPV(xf, comm, lay)
+            res[("reduce_f64", name)] = alg.reduce(None, pf.begin(), pf.end(), 0.5, F.plus)
+            pi = HostPV(x, comm, lay)
+            out = HostPV(np.zeros(n, np.int64), comm, lay)
+            alg.inclusive_scan(None, pi.begin(), pi.end(), out.begin(), F.plus, 3)
+            res[("incl", name)] = (out.lo, out.local.copy())
+            alg.exclusive_scan(None, pi.begin() + 17, pi.end() - 5, out.begin() + 17, 2)
+            res[("excl_sub", name)] = (out.lo, out.local.copy())
+            res[("parts", name)] = (pi.get_num_partitions(), pi.my_segments())
+            fo = HostPV(np.zeros(n, np.float64), comm, lay)
+            alg.inclusive_scan(None, pf.begin(), pf.end(), fo.begin(), F.plus, 0.25)
+            res[("incl_f64", name)] = (fo.lo, fo.local.copy())
+        # segmented output layouts (inclusive_scan_tests_segmented_out_with_policy)
+        for name, lin, lout in (("loc->3", CL, CL(3)), ("loc->10", CL, CL(10)), ("7->loc", CL(7), CL),
+                                ("3->1", CL(3), CL(1))):
+            pi = HostPV(x, comm, lin)
+            out = HostPV(np.zeros(n, np.int64), comm, lout)
+            alg.inclusive_scan(None, pi.begin(), pi.end(), out.begin(), F.plus, 0)
+            res[("mixed", name)] = (out.lo, out.local.copy())
+            out2 = HostPV(np.zeros(n, np.int64), comm, lout)
+            alg.transform(None, pi.begin(), pi.end(), out2.begin(), F.add_value(5))
+            res[("mixed_transform", name)] = (out2.lo, out2.local.copy())
+            # shifted destination: out[100 + i] = scan(x[0 .. i]) over x[0, n-100)
+            out3 = HostPV(np.zeros(n, np.int64), comm, lout)
+            alg.inclusive_scan(None, pi.begin(), pi.end() - 100, out3.begin() + 100, F.plus, 0)
+            res[("shifted", name)] = (out3.lo, out3.local.copy())
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
 
 
 def _worker(rank, size, port, q):
@@ -176,6 +260,58 @@ def test_segmented_algorithms_gloo(size):
     parts = sorted((results[r]["copy_if"][1], results[r]["copy_if"][2]) for r in range(size))
     assert all(results[r]["copy_if"][0] == sel.size for r in range(size))
     np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), sel)
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_partitioned_vector_layouts_gloo(size):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_layout_worker, args=(r, size, port, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=180) for _ in range(size))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 10007
+    x = O.generate(np.int64, "range", n, 0x5EED, -1000, 1000)
+    xf = O.generate(np.float64, "unit", n, 0x5EED)
+    for name, k in (("default", size), ("3", 3), ("10", 10), ("1000", 1000), ("1", 1)):
+        for r in range(size):
+            assert results[r][("reduce_ones", name)] == n + 1
+            # FP: the segment-order fold of the reference (init (+) S_0 (+) ... over k segments)
+            assert results[r][("reduce_f64", name)] == O.segmented_reduce(xf, 0.5, k)
+            nparts, (j0, j1) = results[r][("parts", name)]
+            assert nparts == k and (j0, j1) == S.rank_partitions(k, size, r)
+        np.testing.assert_array_equal(_gather(results, ("incl", name), n), O.segmented_scan(x, 3, k, True))
+        sub = _gather(results, ("excl_sub", name), n)
+        exp = np.concatenate([[2], 2 + np.cumsum(x[17:n - 5])[:-1]])
+        np.testing.assert_array_equal(sub[17:n - 5], exp)
+        np.testing.assert_array_equal(_gather(results, ("incl_f64", name), n, np.float64),
+                                      O.segmented_scan(xf, 0.25, k, True))
+    for name in ("loc->3", "loc->10", "7->loc", "3->1"):
+        np.testing.assert_array_equal(_gather(results, ("mixed", name), n), np.cumsum(x))
+        np.testing.assert_array_equal(_gather(results, ("mixed_transform", name), n), x + 5)
+        got = _gather(results, ("shifted", name), n)
+        np.testing.assert_array_equal(got[100:], np.cumsum(x[:n - 100]))
+
+
+def test_layout_maps():
+    # partitioned_vector_impl.hpp:325 partition sizes; contiguous partition runs per rank
+    for n, k, p in [(10007, 3, 2), (10007, 10, 3), (1000, 1000, 3), (10, 4, 3), (5, 8, 3), (0, 3, 2)]:
+        m = S.layout_map(n, k, p)
+        runs = [m.rank_segments(r) for r in range(p)]
+        assert runs[0][0] == 0 and runs[-1][1] == k and all(a1 == b0 for (_, a1), (b0, _) in zip(runs, runs[1:]))
+        bounds = [m.rank_bounds(r) for r in range(p)]
+        assert bounds[0][0] == 0 and bounds[-1][1] == n
+        assert all(a1 == b0 for (_, a1), (b0, _) in zip(bounds, bounds[1:]))
+        for r in range(p):
+            j0, j1 = runs[r]
+            if j1 > j0:
+                assert bounds[r] == (m.segment_bounds(j0)[0], m.segment_bounds(j1 - 1)[1])
+    with pytest.raises(ValueError):
+        S.container_layout(0)
 
 
 def test_partition_bounds_match_reference_layout():

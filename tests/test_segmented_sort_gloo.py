@@ -51,13 +51,13 @@ class GlooComm:
         dist.all_gather(out, w)
         return np.stack([o.numpy() for o in out])
 
-    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream):
+    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream, recv_off=0):
         n = int(sum(send_counts))
         src = torch.from_numpy(send_buf[send_off:send_off + n].view(np.uint8).copy())
         dst = torch.zeros(int(sum(recv_counts)) * itemsize, dtype=torch.uint8)
         dist.all_to_all_single(dst, src, [int(c) * itemsize for c in recv_counts],
                                [int(c) * itemsize for c in send_counts])
-        recv_buf[:int(sum(recv_counts))] = dst.numpy().view(recv_buf.dtype)
+        recv_buf[recv_off:recv_off + int(sum(recv_counts))] = dst.numpy().view(recv_buf.dtype)
 
     def barrier(self):
         dist.barrier()
@@ -88,13 +88,12 @@ class SortEngine:
 
 
 class HostPV(S.partitioned_vector):
-    def __init__(self, glob, comm):
+    def __init__(self, glob, comm, layout=None):
         self.comm = comm
         self.tgt = None
         self.n = glob.size
         self.dtype = CODES[glob.dtype]
-        self.rank, self.parts = comm.rank, comm.size
-        self.lo, self.hi = S.partition_bounds(self.n, self.parts, self.rank)
+        self._set_layout(layout)
         self.local = glob[self.lo:self.hi].copy()
 
 
