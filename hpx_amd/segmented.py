@@ -293,9 +293,9 @@ class HipEngine:
         from . import algorithms as A
         A.transform((pol or _par()).on(_exec(pv)), pv.local.begin() + lo, pv.local.begin() + hi, dst.begin() + dlo, f)
 
-    def word(self, ptr, i):
-        """The i-th 8-byte slot of a device slot array."""
-        return ptr + 8 * int(i)
+    def word(self, ptr, i, size=8):
+        """The i-th `size`-byte slot of a device slot array."""
+        return ptr + size * int(i)
 
     def put(self, ptr, dt, value):
         """Store one dt value into a device slot (stream-ordered)."""
@@ -648,15 +648,18 @@ class segmented:
     def _segment_totals(self, pv, a, b, op, conv, adt, eng, comm):
         """S_j = the op-combination of conv(x) over segment j of [a, b)
         (detail/reduce.hpp:43-62: no init), for this rank's partitions, into
-        consecutive 8-byte send slots padded with op's identity to the
-        largest per-rank partition count; one all-gather.  Returns (recv,
+        consecutive send slots of the value's size, padded with op's identity
+        to the largest per-rank partition count (rounded so a rank's block is
+        whole 8-byte words); one all-gather.  Returns (recv,
         slots per rank): segment j of rank r sits at r*slots + (j - first)."""
         j0, j1 = pv.my_segments()
+        size = np_dtype(adt).itemsize
         cmax = max(1, pv.layout.max_segments())
-        send, recv = comm.slots(8 * cmax)
+        cmax += (cmax * size) % 8 // size          # whole 8-byte words per rank block
+        send, recv = comm.slots(cmax * size)
         ident = _identity(op.kind, adt)
         for i in range(cmax):
-            slot = eng.word(send, i)
+            slot = eng.word(send, i, size)
             if j0 + i < j1:
                 s0, s1 = pv.segment_bounds(j0 + i)
                 lo, hi = pv.local_range(max(s0, a), min(s1, b))
@@ -664,7 +667,7 @@ class segmented:
                     eng.reduce_into(pv.local, lo, hi, op, conv, adt, slot)
                     continue
             eng.put(slot, adt, ident)
-        comm.allgather(8 * cmax, eng.stream)
+        comm.allgather(cmax * size, eng.stream)
         return recv, cmax
 
     # --- reduce (segmented_algorithms/reduce.hpp:112-209)

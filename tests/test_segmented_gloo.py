@@ -98,7 +98,7 @@ class NumpyEngine:
     def read_words(self, h, count, dt):
         return list(h[:count])
 
-    def word(self, arr, i):
+    def word(self, arr, i, size=8):
         return arr[i:]
 
     def transform(self, pol, pv, lo, hi, dst, dlo, f):
