@@ -45,7 +45,7 @@ $(ORACLE): oracle/oracle.cpp oracle/oracle.h
 	$(CXX) $(OFLAGS) -shared -o $@ oracle/oracle.cpp
 
 # ... and the hipcc-compiled ones (device closures, HPX_HOST_DEVICE lambdas)
-HIPT     := device_closures
+HIPT     := device_closures partitioned_vector
 HIPTBIN  := $(HIPT:%=tests/cxx/bin/%)
 HTFLAGS  := -O2 -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-parameter -Iinclude
 

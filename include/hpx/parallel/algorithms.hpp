@@ -35,6 +35,7 @@
 #include <hpx/compute/hip/functional.hpp>
 #include <hpx/parallel/detail/device_closures.hpp>
 #include <hpx/parallel/execution.hpp>
+#include <hpx/parallel/segmented_fwd.hpp>
 
 #include <algorithm>
 #include <array>
@@ -52,6 +53,8 @@ using hip::detail::check;
 
 template <typename It>
 constexpr bool is_dev = hip::is_device_iterator<typename std::decay<It>::type>::value;
+template <typename It>
+constexpr bool is_seg = hpx::is_segmented_iterator<typename std::decay<It>::type>::value;
 template <typename It>
 using value_t = typename std::iterator_traits<It>::value_type;
 template <typename T>
@@ -194,6 +197,9 @@ auto host_ptr(It it) {
 // compiled by hipcc (detail/device_closures.hpp), else it does not compile.
 template <typename P, typename It, typename F>
 detail::result_t<P, It> for_each(P&& p, It first, It last, F&& f) {
+    if constexpr (detail::is_seg<It>) {
+        return segmented_detail::for_each(std::forward<P>(p), first, last, std::forward<F>(f));
+    } else {
     static_assert(detail::is_dev<It>, "for_each: device iterators required");
     using T = detail::value_t<It>;
     uint64_t n = detail::distance(first, last);
@@ -211,6 +217,7 @@ detail::result_t<P, It> for_each(P&& p, It first, It last, F&& f) {
             }
         },
         [last] { return last; });
+    }
 }
 
 template <typename P, typename It, typename Size, typename F>
@@ -225,6 +232,9 @@ detail::result_t<P, It> for_each_n(P&& p, It first, Size count, F&& f) {
 // ------------------------------------------------------------------ fill
 template <typename P, typename It, typename T>
 detail::result_t<P, void> fill(P&& p, It first, It last, T value) {
+    if constexpr (detail::is_seg<It>) {
+        return segmented_detail::fill(std::forward<P>(p), first, last, value);
+    } else {
     static_assert(detail::is_dev<It>, "fill: device iterators required");
     using V = detail::value_t<It>;
     V v = static_cast<V>(value);
@@ -235,6 +245,7 @@ detail::result_t<P, void> fill(P&& p, It first, It last, T value) {
             detail::check(hpxhip_fill(detail::dt<V>, &v, base + off, cnt, t.stream()), "fill");
         },
         [] {});
+    }
 }
 
 template <typename P, typename It, typename Size, typename T>
@@ -257,6 +268,9 @@ detail::result_t<P, It> fill_n(P&& p, It first, Size count, T value) {
 template <typename P, typename In, typename Out>
 detail::result_t<P, util::tagged_pair<In, Out>> copy(P&& p, In first, In last, Out dest) {
     using R = util::tagged_pair<In, Out>;
+    if constexpr (detail::is_seg<In> || detail::is_seg<Out>) {
+        return segmented_detail::copy(std::forward<P>(p), first, last, dest);
+    } else {
     uint64_t n = detail::distance(first, last);
     if constexpr (detail::is_dev<In> && detail::is_dev<Out>) {
         using T = detail::value_t<In>;
@@ -289,6 +303,7 @@ detail::result_t<P, util::tagged_pair<In, Out>> copy(P&& p, In first, In last, O
                           "copy (H2D)");
         Out end = dest + static_cast<std::ptrdiff_t>(n);
         return detail::finish<R>(p, t, [last, end] { return R{last, end}; });
+    }
     }
 }
 
@@ -323,6 +338,9 @@ detail::result_t<P, util::tagged_pair<In, Out>> copy_if(P&& p, In first, In last
 // ------------------------------------------------------------- transform
 template <typename P, typename In, typename Out, typename F>
 detail::result_t<P, util::tagged_pair<In, Out>> transform(P&& p, In first, In last, Out dest, F&& f) {
+    if constexpr (detail::is_seg<In>) {
+        return segmented_detail::transform(std::forward<P>(p), first, last, dest, std::forward<F>(f));
+    } else {
     static_assert(detail::is_dev<In> && detail::is_dev<Out>, "transform: device iterators required");
     using TI = detail::value_t<In>;
     using TO = detail::value_t<Out>;
@@ -347,12 +365,16 @@ detail::result_t<P, util::tagged_pair<In, Out>> transform(P&& p, In first, In la
             }
         },
         [last, end] { return R{last, end}; });
+    }
 }
 
 namespace detail {
 template <typename P, typename In1, typename In2, typename Out, typename F>
 result_t<P, util::tagged_tuple<In1, In2, Out>> transform_binary(P&& p, In1 first1, uint64_t n, In2 first2, Out dest,
                                                                 F&& f) {
+    if constexpr (is_seg<In1>) {
+        return segmented_detail::transform_binary(std::forward<P>(p), first1, n, first2, dest, std::forward<F>(f));
+    } else {
     static_assert(is_dev<In1> && is_dev<In2> && is_dev<Out>, "transform: device iterators required");
     using T = value_t<In1>;
     using T2 = value_t<In2>;
@@ -382,11 +404,12 @@ result_t<P, util::tagged_tuple<In1, In2, Out>> transform_binary(P&& p, In1 first
             }
         },
         [e1, e2, eo] { return R{e1, e2, eo}; });
+    }
 }
 }  // namespace detail
 
 template <typename P, typename In1, typename In2, typename Out, typename F,
-          typename = typename std::enable_if<detail::is_dev<Out>>::type>
+          typename = typename std::enable_if<detail::is_dev<Out> || detail::is_seg<Out>>::type>
 detail::result_t<P, util::tagged_tuple<In1, In2, Out>> transform(P&& p, In1 first1, In1 last1, In2 first2, Out dest,
                                                                 F&& f) {
     return detail::transform_binary(std::forward<P>(p), first1, detail::distance(first1, last1), first2, dest,
@@ -404,6 +427,10 @@ detail::result_t<P, util::tagged_tuple<In1, In2, Out>> transform(P&& p, In1 firs
 namespace detail {
 template <typename T, typename P, typename It, typename Op, typename Conv>
 result_t<P, T> reduce_impl(P&& p, It first, It last, T init, Op&& op, Conv&& conv) {
+    if constexpr (is_seg<It>) {
+        return segmented_detail::reduce<T>(std::forward<P>(p), first, last, init, std::forward<Op>(op),
+                                           std::forward<Conv>(conv));
+    } else {
     static_assert(is_dev<It>, "reduce: device iterators required");
     using TI = value_t<It>;
     auto const& t = target_of(p, first);
@@ -415,6 +442,7 @@ result_t<P, T> reduce_impl(P&& p, It first, It last, T init, Op&& op, Conv&& con
           "transform_reduce");
     fetch_slot(t, slot, sizeof(T), "reduce result");
     return finish_slot<T>(p, t, std::move(slot), load_value<T>{});
+    }
 }
 }  // namespace detail
 
@@ -434,7 +462,7 @@ detail::result_t<P, detail::value_t<It>> reduce(P&& p, It first, It last) {
 }
 
 template <typename P, typename It, typename T, typename Red, typename Conv,
-          typename = typename std::enable_if<detail::is_dev<It> && detail::tr::is_unary<Conv>>::type>
+          typename = typename std::enable_if<(detail::is_dev<It> || detail::is_seg<It>) && detail::tr::is_unary<Conv>>::type>
 detail::result_t<P, T> transform_reduce(P&& p, It first, It last, T init, Red&& red, Conv&& conv) {
     return detail::reduce_impl<T>(std::forward<P>(p), first, last, init, std::forward<Red>(red),
                                   std::forward<Conv>(conv));
@@ -478,6 +506,10 @@ detail::result_t<P, T> transform_reduce(P&& p, It1 first1, It1 last1, It2 first2
 namespace detail {
 template <typename P, typename In, typename Out, typename Op, typename Conv, typename T>
 result_t<P, Out> scan_impl(P&& p, In first, In last, Out dest, Op&& op, Conv&& conv, T init, bool inclusive) {
+    if constexpr (is_seg<In>) {
+        return segmented_detail::scan(std::forward<P>(p), first, last, dest, std::forward<Op>(op),
+                                      std::forward<Conv>(conv), init, inclusive);
+    } else {
     static_assert(is_dev<In> && is_dev<Out>, "scan: device iterators required");
     using V = value_t<In>;
     static_assert(std::is_same<V, value_t<Out>>::value, "scan: input and output element types must match");
@@ -491,6 +523,7 @@ result_t<P, Out> scan_impl(P&& p, In first, In last, Out dest, Op&& op, Conv&& c
           inclusive ? "inclusive_scan" : "exclusive_scan");
     Out end = dest + static_cast<std::ptrdiff_t>(n);
     return finish<Out>(p, t, [end] { return end; });
+    }
 }
 using ident = hpx::compute::hip::functional::identity;
 }  // namespace detail
@@ -888,3 +921,6 @@ using parallel::v1::transform_exclusive_scan;
 using parallel::v1::transform_inclusive_scan;
 using parallel::v1::transform_reduce;
 }  // namespace hpx
+
+// the segmented algorithms' definitions (they call back into the above)
+#include <hpx/parallel/segmented_algorithms.hpp>

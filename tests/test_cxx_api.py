@@ -68,6 +68,7 @@ void f(hpx::compute::vector<int>& a) {
     ("stream_hip", ["--vector_size", str(1 << 26), "--iterations", "10"]),
     ("for_loop_merge", []),
     ("device_closures", ["4242"]),
+    ("partitioned_vector", []),
 ])
 def test_cxx_program(prog, args):
     exe = os.path.join(BIN, prog)
