@@ -88,6 +88,8 @@ def main(argv=None, comm_tgt=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--cpu-logn", type=int, default=27)
+    ap.add_argument("--stencil-logn", type=int, default=32, help="1d_stencil points (total over the ranks)")
+    ap.add_argument("--stencil-steps", type=int, default=100)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--triad-only", action="store_true", help=argparse.SUPPRESS)  # PMC child mode
     args = ap.parse_args(argv)
@@ -201,11 +203,12 @@ def main(argv=None, comm_tgt=None):
     for v in (a, b, c):
         v.local.free()
     if not args.no_extras and world == 1:
-        out["extras"] = extras(hpx, L, ex, F, tgt, pol, x, y, n_local, world)
-    x.local.free()
+        out["extras"] = extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args)
     y.local.free()
     if not args.no_extras and world > 1:
-        out["extras"] = dist_extras(S, F, comm, tgt, pol, n_local, world)
+        out["extras"] = dist_extras(S, F, comm, tgt, pol, x, n_local, world, args)
+    else:
+        x.local.free()
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_logn)
     if rank == 0 and world == 1 and not args.no_pmc:
@@ -235,41 +238,28 @@ def timed(L, tgt, fn, reps=3):
     return best
 
 
-def extras(hpx, L, ex, F, tgt, pol, x, y, n_local, world):
+def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
     from hpx_amd import parallel as P
     res = {}
-    # f64 reduce / scan on the same vectors reinterpreted (values don't matter for speed)
     xv, yv = x.local, y.local
     n = n_local
     ms = timed(L, tgt, lambda: P.copy_if(pol, xv.begin(), xv.end(), yv.begin(), F.not_less_than(0)))
     res["copy_if_int64"] = {"ms": round(ms, 4), "gbs_model_12B": round(12 * n / ms / 1e6, 1),
                             "pct_peak": pct(12 * n / ms / 1e6)}
+    res["segmented_reduce_int64"] = seg_reduce_row(S, F, comm, tgt, pol, x)
     # sort of 2^30 uint64 keys (8 GiB + 8 GiB workspace)
     keys = hpx.vector(n, dtype=np.uint64, tgt=tgt)
     regen = lambda: P.generate(pol, keys.begin(), keys.end(), "bits", 7)  # noqa: E731
     ms_gen = timed(L, tgt, regen, reps=2)
     ms_sort = timed(L, tgt, lambda: (regen(), P.sort(pol, keys.begin(), keys.end())), reps=2) - ms_gen
-    ok = P.reduce(pol, keys.begin(), keys.begin() + 1, 0, F.plus) <= P.reduce(pol, keys.begin() + 1, keys.begin() + 2, 0, F.plus)
     res["sort_uint64"] = {"ms": round(ms_sort, 3), "gkeys_per_s": round(n / ms_sort / 1e6, 3),
                           "gbs_model_136B": round(136 * n / ms_sort / 1e6, 1),
-                          "pct_peak": pct(136 * n / ms_sort / 1e6), "sorted_head_check": bool(ok)}
+                          "pct_peak": pct(136 * n / ms_sort / 1e6)}
+    res["sort_uint64"].update(sort_check(P, F, pol, tgt, keys, regen))
     keys.free()
-    # 1d_stencil heat: 2^32 points on one GPU (two 32 GiB buffers), 10 steps
-    from hpx_amd import stencil
-    nx = 1 << 32 if world == 1 else n
-    st = stencil.stepper(nx, tgt)
-    nt = 10
-    ms = timed(L, tgt, lambda: st.do_work(nt), reps=2)
-    # temporal blocking: up to 8 steps per pass over HBM; hbm_gbs counts the
-    # bytes the passes move, gbs_16B_per_step is the one-step-per-pass model
-    passes = stencil.fused_passes(nx, nt)
-    hbm = sum(stencil.pass_hbm_bytes(nx, s) for s in passes)
-    res["stencil_heat"] = {"points": nx, "steps": nt, "passes": passes, "ms": round(ms, 3),
-                           "gpoint_steps_per_s": round(nx * nt / ms / 1e6, 2),
-                           "hbm_gbs": round(hbm / ms / 1e6, 1), "pct_peak": pct(hbm / ms / 1e6),
-                           "gbs_16B_per_step_model": round(16 * nx * nt / ms / 1e6, 1)}
-    for v in st.U:
-        v.free()
+    # 1d_stencil heat: 2^32 points, 100 steps (BASELINE.md plan), through the
+    # partitioned solver -- the same row the N > 1 run reports
+    res["stencil_heat_dist"] = stencil_row(S, comm, tgt, 1 << args.stencil_logn, args.stencil_steps)
     # host <-> device transfer (hpx/compute/cuda/transfer.hpp:188-348): 1 GiB,
     # pinned (hpxhip_malloc_host) and pageable host buffers
     nb = 1 << 30
@@ -290,23 +280,99 @@ def extras(hpx, L, ex, F, tgt, pol, x, y, n_local, world):
     return res
 
 
-def dist_extras(S, F, comm, tgt, pol, n_local, world):
+def sort_check(P, F, pol, tgt, keys, regen):
+    """Full-size check of the 2^30 sort, on the device: the sorted keys are
+    a permutation of the generated ones (XOR and wrapping sum of all keys
+    unchanged) and no adjacent pair is out of order (is_sorted)."""
+    regen()
+    xor0 = P.reduce(pol, keys.begin(), keys.end(), 0, F.bit_xor)
+    sum0 = P.reduce(pol, keys.begin(), keys.end(), 0, F.plus)
+    P.sort(pol, keys.begin(), keys.end())
+    ok = bool(P.is_sorted(pol, keys.begin(), keys.end()))
+    same = (P.reduce(pol, keys.begin(), keys.end(), 0, F.bit_xor) == xor0 and
+            P.reduce(pol, keys.begin(), keys.end(), 0, F.plus) == sum0)
+    return {"is_sorted_full": ok, "checksums_match": bool(same)}
+
+
+def seg_reduce_row(S, F, comm, tgt, pol, x, reps=5):
+    """Segmented transform_reduce of the int64 partitioned_vector x
+    (segmented_algorithms/reduce.hpp:112-209): local kernel + one 8-B
+    all-gather + device fold per call; max-over-ranks wall time of `reps`
+    back-to-back calls between barriers."""
+    import time
+    n_local = len(x.local)
+    S.algorithms.reduce(pol, x.begin(), x.end(), 0, F.plus)
+    tgt.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = S.algorithms.reduce(pol, x.begin(), x.end(), 0, F.plus)
+    tgt.synchronize()
+    comm.barrier()
+    el = max_over_ranks(comm, (time.perf_counter() - t0) / reps)
+    per_rank = 8 * n_local / el / 1e9
+    return {"elements_per_rank": n_local, "ranks": comm.size, "ms": round(1e3 * el, 4),
+            "gbs_per_rank": round(per_rank, 1), "gbs_total": round(per_rank * comm.size, 1),
+            "pct_peak_per_rank": pct(per_rank), "value": int(r)}
+
+
+def stencil_row(S, comm, tgt, nx, nt):
+    """examples/1d_stencil heat over the ranks (strong scaling: nx points in
+    total), partitioned solver with temporal blocking and the halo ring;
+    max-over-ranks wall time of nt steps.  Check: the linear ramp U0[i] = i
+    is a steady state away from the periodic wrap, so after nt steps every
+    point at distance > nt from the wrap still equals its global index
+    (sampled windows, exact)."""
+    import time
+    from hpx_amd import _lib as L
+    hs = S.heat_solver(nx, comm, tgt)
+    hs.do_work(1)
+    hs.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    hs.do_work(nt)
+    hs.synchronize()
+    comm.barrier()
+    el = max_over_ranks(comm, time.perf_counter() - t0)
+    cur = hs.current
+    m = len(cur)
+    ok = True
+    for w0 in (0, m // 2, max(0, m - 4096)):
+        win = np.empty(min(4096, m - w0), np.float64)
+        L.call("hpxhip_memcpy_async", win.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(cur.data() + 8 * w0),
+               8 * win.size, L.D2H, tgt.stream)
+        tgt.synchronize()
+        g = hs.lo + w0 + np.arange(win.size)
+        far = (g > nt + 2) & (g < nx - nt - 3)  # nt + 1 steps ran (one warm-up)
+        ok = ok and bool(np.all(win[far] == g[far].astype(np.float64)))
+    ok = bool(max_over_ranks(comm, 0.0 if ok else 1.0) == 0.0)
+    for v in hs.U:
+        v.free()
+    return {"points": nx, "ranks": comm.size, "steps": nt, "ms": round(1e3 * el, 3),
+            "gpoint_steps_per_s": round(nx * nt / el / 1e9, 2), "gbs_model_16B": round(16 * nx * nt / el / 1e9, 1),
+            "ramp_check": ok, "halo_width": hs.W}
+
+
+def dist_extras(S, F, comm, tgt, pol, x, n_local, world, args):
     """Multi-GPU rows of SURVEY.md section 8(e) (all ranks, max-over-ranks
     wall time between barriers):
+      * segmented reduce of the step's int64 partitioned_vector (GB/s per
+        rank and in total);
       * segmented sort of 2^logn uint64 keys per GPU (weak scaling): local
         radix sort, exact global cut, one RCCL all-to-all, pairwise merges;
-        checked: every partition sorted on sampled windows, partitions
-        ordered across ranks (first/last keys all-gathered);
-      * 1d_stencil heat, 2^32 points over the ranks (strong scaling), halo
-        ring over RCCL send/recv overlapped with the interior update;
-        checked: ramp interior unchanged (steady state away from the wrap)."""
+        checked on the device: every partition sorted (is_sorted) and the
+        partitions ordered across ranks (first/last keys all-gathered);
+      * 1d_stencil heat, 2^32 points over the ranks, 100 steps (strong
+        scaling), halo ring over RCCL send/recv overlapped with the interior."""
     import time
-    res = {}
+    from hpx_amd import parallel as P
+    res = {"segmented_reduce_int64": seg_reduce_row(S, F, comm, tgt, pol, x)}
 
     def tmax(v):
         return max_over_ranks(comm, v)
 
     n = n_local * world
+    x.local.free()
     keys = S.partitioned_vector(n, np.uint64, comm=comm, tgt=tgt)
     best = None
     for rep in range(3):
@@ -321,40 +387,16 @@ def dist_extras(S, F, comm, tgt, pol, n_local, world):
         best = el if best is None else min(best, el)
     loc = keys.local
     m = len(loc)
-    ok = True
-    from hpx_amd import _lib as L
-    for w0 in (0, m // 2, max(0, m - (1 << 20))):
-        win = np.empty(min(1 << 20, m - w0), np.uint64)
-        if win.size:
-            L.call("hpxhip_memcpy_async", win.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(loc.data() + 8 * w0),
-                   8 * win.size, L.D2H, tgt.stream)
-            tgt.synchronize()
-            ok = ok and bool(np.all(win[1:] >= win[:-1]))
+    ok = bool(P.is_sorted(pol, loc.begin(), loc.end())) if m else True
     ends = np.array([loc[0], loc[m - 1]] if m else [0, 0], np.uint64).view(np.int64)
     g = comm.allgather_host(ends).view(np.uint64)
-    ok = ok and all(g[r, 1] <= g[r + 1, 0] for r in range(world - 1)) and all(g[r, 0] <= g[r, 1] for r in range(world))
+    ok = ok and all(g[r, 1] <= g[r + 1, 0] for r in range(world - 1))
+    ok = bool(tmax(0.0 if ok else 1.0) == 0.0)
     res["segmented_sort_uint64"] = {"keys_per_gpu": n_local, "keys_total": n, "ms": round(1e3 * best, 3),
-                                    "gkeys_per_s": round(n / best / 1e9, 3), "ordered_across_partitions": bool(ok)}
+                                    "gkeys_per_s": round(n / best / 1e9, 3), "gbs_model_136B_per_rank":
+                                    round(136 * n_local / best / 1e9, 1), "sorted_and_ordered": ok}
     loc.free()
-    nx = min(1 << 32, 4 * n)   # 2^32 points at the benchmark sizes
-    hs = S.heat_solver(nx, comm, tgt)
-    hs.do_work(1)
-    hs.synchronize()
-    comm.barrier()
-    nt = 10
-    t0 = time.perf_counter()
-    hs.do_work(nt)
-    hs.synchronize()
-    comm.barrier()
-    el = tmax(time.perf_counter() - t0)
-    cur = hs.current
-    mid = len(cur) // 2
-    ok = float(cur[mid]) == float(hs.lo + mid)  # ramp steady state in the interior
-    res["stencil_heat_dist"] = {"points": nx, "ranks": world, "steps": nt, "ms": round(1e3 * el, 3),
-                                "gpoint_steps_per_s": round(nx * nt / el / 1e9, 2),
-                                "gbs_model_16B": round(16 * nx * nt / el / 1e9, 1), "interior_check": bool(ok)}
-    for v in hs.U:
-        v.free()
+    res["stencil_heat_dist"] = stencil_row(S, comm, tgt, 1 << args.stencil_logn, args.stencil_steps)
     return res
 
 
@@ -415,7 +457,11 @@ def pmc_traffic(logn):
 
 def cpu_baseline(logn):
     """HPX-par restatement (oracle) of the same step on the host cores, on a
-    2^logn sample: triad + reduce + inclusive scan."""
+    2^logn sample: triad + reduce + inclusive scan; plus the extras' host
+    rows: copy_if on the same sample, sort of 2^(logn-2)
+    uint64 keys (sort.hpp:78-229 restated: parallel quicksort, std::sort
+    leaves) and the 1d_stencil heat solver (1d_stencil_4_parallel.cpp:87-156
+    restated) on 2^(logn-3) points x 20 steps."""
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1))
@@ -425,11 +471,27 @@ def cpu_baseline(logn):
     t_red, _ = O.par_reduce_i64(x, threads, reps=3)
     t_scan, _ = O.par_scan_i64(x, threads, reps=3)
     gbs = (24 + 8 + 16) * n / (t_triad + t_red + t_scan) / 1e9
+    t_cif, _ = O.par_copy_if_i64(x, threads, reps=2)
+    del x
+    ns = 1 << max(10, logn - 2)
+    keys = O.generate(np.uint64, "bits", ns, 7)
+    t_sort, _ = O.par_sort_u64(keys, threads)
+    del keys
+    nx, nt = 1 << max(10, logn - 3), 20
+    t_st, _ = O.par_stencil(np.arange(nx, dtype=np.float64), nt, threads)
     return {"value": round(gbs, 2), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"2^{logn} elements: triad f64 + reduce int64 + inclusive_scan int64, best of 3, "
                       f"HPX par chunking (4*cores chunks) on {threads} std::threads",
             "triad_gbs": round(24 * n / t_triad / 1e9, 2), "reduce_gbs": round(8 * n / t_red / 1e9, 2),
-            "scan_gbs": round(16 * n / t_scan / 1e9, 2)}
+            "scan_gbs": round(16 * n / t_scan / 1e9, 2),
+            "extras": {"copy_if_int64": {"elements": n, "ms": round(1e3 * t_cif, 2),
+                                         "gbs_model_12B": round(12 * n / t_cif / 1e9, 2)},
+                       "sort_uint64": {"keys": ns, "ms": round(1e3 * t_sort, 2),
+                                       "gkeys_per_s": round(ns / t_sort / 1e9, 4),
+                                       "gbs_model_136B": round(136 * ns / t_sort / 1e9, 2)},
+                       "stencil_heat": {"points": nx, "steps": nt, "ms": round(1e3 * t_st, 2),
+                                        "gpoint_steps_per_s": round(nx * nt / t_st / 1e9, 3),
+                                        "gbs_model_16B": round(16 * nx * nt / t_st / 1e9, 2)}}}
 
 
 if __name__ == "__main__":

@@ -131,6 +131,7 @@ SIGNATURES = {
     "hpxhip_sort": [_i, _vp, _u64, _i, _vp, _vp, _sz],
     "hpxhip_sort_by_key": [_i, _i, _vp, _vp, _u64, _i, _vp, _vp, _sz],
     "hpxhip_merge": [_i, _vp, _u64, _vp, _u64, _vp, _i, _vp, _vp, _sz],
+    "hpxhip_unsorted_pairs": [_i, _vp, _u64, _i, _vp, _vp],
     "hpxhip_sorted_bounds": [_i, _vp, _u64, _vp, _u64, _i, _i, _vp, _vp],
     "hpxhip_stencil_heat_step": [_vp, _vp, _u64, _vp, _vp, _d, _d, _d, _vp],
     "hpxhip_stencil_heat_run": [_vp, _vp, _u64, _u64, _d, _d, _d, _vp],

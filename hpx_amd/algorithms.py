@@ -356,13 +356,36 @@ def transform_exclusive_scan(pol, first, last, dest, init, op, conv):
 
 
 # --------------------------------------------------------------------- sort
-def sort(pol, first, last, comp=F.less):
-    """sort.hpp:364; comp = std::less (default) or std::greater."""
+def sort(pol, first, last=None, comp=F.less):
+    """sort.hpp:364; comp = std::less (default) or std::greater.  With a
+    container instead of an iterator pair -- sort(pol, rng[, comp]) -- the
+    range overload of container_algorithms/sort.hpp:102 (hpx::parallel::sort
+    over begin(rng), end(rng)); returns the range's end iterator."""
+    from .compute import vector as _vector
+    if isinstance(first, _vector):
+        rng = first
+        if last is not None:
+            comp = last
+        return sort(pol, rng.begin(), rng.end(), comp)
     comp = F.require(comp, F.Compare, "sort")
     n = _check_range(first, last)
     stream, tgt, is_task = _context(pol, first)
     L.call("hpxhip_sort", first.dtype, _vp(first.address), n, 1 if comp.descending else 0, stream, None, 0)
     return _finish(is_task, stream, tgt, lambda: last)
+
+
+def is_sorted(pol, first, last, comp=F.less):
+    """is_sorted.hpp:40-120: True iff no adjacent pair is ordered after one
+    another under comp (std::less / std::greater, the sort's key order),
+    counted on the device (hpxhip_unsorted_pairs); a future under par(task)."""
+    comp = F.require(comp, F.Compare, "is_sorted")
+    n = _check_range(first, last)
+    stream, tgt, is_task = _context(pol, first)
+    dev, host = _slots_for(tgt).next()
+    L.call("hpxhip_unsorted_pairs", first.dtype, _vp(first.address), n, 1 if comp.descending else 0, _vp(dev),
+           stream)
+    L.call("hpxhip_memcpy_async", _vp(host), _vp(dev), 8, L.D2H, stream)
+    return _finish(is_task, stream, tgt, lambda: _read_host(host, L.U64) == 0)
 
 
 def sort_by_key(pol, key_first, key_last, value_first, comp=F.less):

@@ -224,6 +224,36 @@ namespace hpxhip {
 size_t merge_scratch_bytes(uint64_t n) { return ((n + kTile - 1) / kTile + 1) * 8; }
 }  // namespace hpxhip
 
+// Adjacent pairs (i, i+1) with key[i] ordered after key[i+1]; thread t
+// handles the pairs starting in its 16-byte vector (the neighbour of the
+// vector's last element is the next vector's first, re-read through the cache).
+template <typename U, typename X>
+__global__ __launch_bounds__(256) void k_unsorted_pairs(const U* __restrict__ keys, uint64_t n, X xf,
+                                                        unsigned long long* __restrict__ count) {
+    constexpr int V = 16 / sizeof(U);
+    using VT = vec<U, V>;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    uint64_t c = 0;
+    const bool aligned = (reinterpret_cast<uintptr_t>(keys) % 16) == 0;
+    if (aligned) {
+        const uint64_t nvec = n / V;
+        const VT* vk = reinterpret_cast<const VT*>(keys);
+        for (uint64_t v = tid; v < nvec; v += stride) {
+            const VT x = ld_stream(&vk[v]);
+#pragma unroll
+            for (int e = 0; e + 1 < V; ++e) c += xf(x.v[e]) > xf(x.v[e + 1]);
+            const uint64_t nx = (v + 1) * V;
+            if (nx < n) c += xf(x.v[V - 1]) > xf(keys[nx]);
+        }
+        for (uint64_t i = nvec * V + tid; i + 1 < n; i += stride) c += xf(keys[i]) > xf(keys[i + 1]);
+    } else {
+        for (uint64_t i = tid; i + 1 < n; i += stride) c += xf(keys[i]) > xf(keys[i + 1]);
+    }
+    const uint64_t w = wave_reduce(c, op_plus{});
+    if (lane_id() == 0 && w) atomicAdd(count, static_cast<unsigned long long>(w));
+}
+
 extern "C" {
 
 int hpxhip_merge(int dtype, const void* in1, uint64_t n1, const void* in2, uint64_t n2, void* out, int descending,
@@ -259,6 +289,35 @@ int hpxhip_sorted_bounds(int dtype, const void* sorted, uint64_t n, const void* 
             hipLaunchKernelGGL((k_bounds<U, ordered_bits<T, false>>), grid, dim3(256), 0, s,
                                static_cast<const U*>(sorted), n, static_cast<const U*>(values_dev), m, upper,
                                ordered_bits<T, false>{}, out_dev);
+        HPXHIP_CHECK_LAUNCH();
+        return 0;
+    });
+}
+
+// is_sorted.hpp:40-120 (hpx::parallel::is_sorted / is_sorted_until): the
+// number of adjacent pairs out of order under the sort's key order, counted
+// on the device (grid-stride, 16-B loads, wave reduction, one 64-bit atomic
+// add per wave); 0 <=> sorted.  *count_dev is overwritten.
+int hpxhip_unsorted_pairs(int dtype, const void* keys, uint64_t n, int descending, uint64_t* count_dev,
+                          hpxhip_stream stream) {
+    if (!count_dev || (n && !keys)) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    HPXHIP_CHECK(hipMemsetAsync(count_dev, 0, sizeof(uint64_t), s));
+    if (n < 2) return 0;
+    return with_dtype(dtype, [&](auto t) -> int {
+        using T = typename decltype(t)::type;
+        using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
+        const unsigned grid = static_cast<unsigned>(std::min<uint64_t>((n + 1023) / 1024, 8192));
+        if (descending)
+            hipLaunchKernelGGL((k_unsorted_pairs<U, ordered_bits<T, true>>), dim3(grid), dim3(256), 0, s,
+                               static_cast<const U*>(keys), n, ordered_bits<T, true>{},
+                               reinterpret_cast<unsigned long long*>(count_dev));
+        else
+            hipLaunchKernelGGL((k_unsorted_pairs<U, ordered_bits<T, false>>), dim3(grid), dim3(256), 0, s,
+                               static_cast<const U*>(keys), n, ordered_bits<T, false>{},
+                               reinterpret_cast<unsigned long long*>(count_dev));
         HPXHIP_CHECK_LAUNCH();
         return 0;
     });

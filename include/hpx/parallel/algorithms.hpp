@@ -594,6 +594,35 @@ detail::result_t<P, It> sort(P&& p, It first, It last, Comp&& = Comp()) {
     return detail::finish<It>(p, t, [last] { return last; });
 }
 
+// container_algorithms/sort.hpp:102: sort(policy, rng[, comp]) over
+// begin(rng), end(rng) (projections: the identity only -- the radix sort
+// orders by the keys' own bits).
+template <typename P, typename Rng, typename Comp = std::less<>,
+          typename = std::enable_if_t<detail::is_dev<decltype(std::declval<Rng&>().begin())>>>
+auto sort(P&& p, Rng&& rng, Comp&& comp = Comp()) {
+    return sort(std::forward<P>(p), rng.begin(), rng.end(), std::forward<Comp>(comp));
+}
+
+// is_sorted.hpp:40-120: no adjacent pair ordered after one another under
+// comp (std::less / std::greater), counted on the device.
+template <typename P, typename It, typename Comp = std::less<>>
+detail::result_t<P, bool> is_sorted(P&& p, It first, It last, Comp&& = Comp()) {
+    static_assert(detail::is_dev<It>, "is_sorted: device iterators required");
+    using T = detail::value_t<It>;
+    auto const& t = detail::target_of(p, first);
+    auto slot = t.make_result_slot();
+    detail::check(hpxhip_unsorted_pairs(detail::dt<T>, first.device_ptr(), detail::distance(first, last),
+                                        detail::tr::compare_t<Comp>::descending ? 1 : 0,
+                                        static_cast<uint64_t*>(slot.device()), t.stream()),
+                  "is_sorted");
+    detail::fetch_slot(t, slot, 8, "is_sorted count");
+    return detail::finish_slot<bool>(p, t, std::move(slot), [](unsigned char const* b) {
+        uint64_t c;
+        std::memcpy(&c, b, 8);
+        return c == 0;
+    });
+}
+
 template <typename P, typename KeyIt, typename ValIt, typename Comp = std::less<>>
 detail::result_t<P, util::tagged_pair<KeyIt, ValIt>> sort_by_key(P&& p, KeyIt key_first, KeyIt key_last,
                                                                  ValIt value_first, Comp&& = Comp()) {
@@ -914,6 +943,7 @@ using parallel::v1::reduction_plus;
 using parallel::v1::merge;
 using parallel::v1::inclusive_scan;
 using parallel::v1::reduce;
+using parallel::v1::is_sorted;
 using parallel::v1::sort;
 using parallel::v1::sort_by_key;
 using parallel::v1::transform;

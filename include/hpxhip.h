@@ -318,6 +318,13 @@ int hpxhip_merge(int dtype, const void* in1, uint64_t n1, const void* in2, uint6
 int hpxhip_sorted_bounds(int dtype, const void* sorted, uint64_t n, const void* values_dev, uint64_t m,
                          int upper, int descending, uint64_t* out_dev, hpxhip_stream stream);
 
+/* is_sorted.hpp:40-120: *count_dev (uint64, device; overwritten) = the
+   number of adjacent pairs (keys[i], keys[i+1]) ordered after one another
+   under the sort's key order (0 <=> sorted); full-size sort verification
+   without a host copy. */
+int hpxhip_unsorted_pairs(int dtype, const void* keys, uint64_t n, int descending, uint64_t* count_dev,
+                          hpxhip_stream stream);
+
 /* ---------------------------------------------------------- 1d_stencil */
 /* One heat step of examples/1d_stencil: next[i] = heat(cur[i-1], cur[i], cur[i+1])
    with heat(l,m,r) = m + (k*dt/(dx*dx)) * (l - 2*m + r)  (1d_stencil_1.cpp:43-46).

@@ -668,6 +668,29 @@ double oracle_par_copy_if_i64(const int64_t* in, int64_t* out, uint64_t n, uint6
     return now() - t0;
 }
 
+// examples/1d_stencil/1d_stencil_4_parallel.cpp:87-156 restated on
+// std::threads: per step, the points are split into HPX par chunks, each
+// computed from the current buffer (periodic neighbours, idx() :35-38), then
+// the buffers swap (the next step depends on all chunks: a join per step).
+// Same arithmetic as oracle_stencil_heat, so the result is identical.
+double oracle_par_stencil(double* u0, double* u1, uint64_t n, uint64_t nt, double k, double dt, double dx,
+                          int threads) {
+    const double t0 = now();
+    double* cur = u0;
+    double* nxt = u1;
+    for (uint64_t t = 0; t < nt && n >= 2; ++t) {
+        run_par(n, threads, [&](size_t, uint64_t beg, uint64_t len) {
+            for (uint64_t i = beg; i < beg + len; ++i) {
+                const double l = cur[i == 0 ? n - 1 : i - 1];
+                const double r = cur[i + 1 == n ? 0 : i + 1];
+                nxt[i] = heat(l, cur[i], r, k, dt, dx);
+            }
+        });
+        std::swap(cur, nxt);
+    }
+    return now() - t0;
+}
+
 // HPX sort.hpp:78-229 restated: median-of-3 pivot, partition, recurse in
 // parallel above the chunk limit, std::sort leaves.
 static void par_sort_rec(uint64_t* first, uint64_t* last, uint64_t limit, int depth) {

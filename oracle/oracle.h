@@ -107,6 +107,8 @@ double oracle_par_reduce_i64(const int64_t* in, uint64_t n, int64_t init, int64_
 double oracle_par_scan_i64(const int64_t* in, int64_t* out, uint64_t n, int threads);
 /* parallel sort uint64 (HPX sort.hpp quicksort restatement, std::sort leaves); seconds */
 double oracle_par_sort_u64(uint64_t* keys, uint64_t n, int threads);
+double oracle_par_stencil(double* u0, double* u1, uint64_t n, uint64_t nt, double k, double dt, double dx,
+                          int threads);
 /* copy_if int64 x >= 0 (3-phase), returns seconds, count in *count */
 double oracle_par_copy_if_i64(const int64_t* in, int64_t* out, uint64_t n, uint64_t* count,
                               int threads);

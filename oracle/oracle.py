@@ -282,6 +282,19 @@ def par_sort_u64(a: np.ndarray, threads):
     return t, k
 
 
+def par_stencil(u, nt, threads, k=0.5, dt=1.0, dx=1.0):
+    """HPX-par restatement of the 1d_stencil heat solver (1d_stencil_4_parallel.cpp:87-156)
+    on `threads` host threads; returns (seconds, final state)."""
+    lib = load()
+    u0 = np.array(u, np.float64, copy=True)
+    u1 = np.empty_like(u0)
+    lib.oracle_par_stencil.restype = ctypes.c_double
+    lib.oracle_par_stencil.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                       ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int]
+    t = lib.oracle_par_stencil(_p(u0), _p(u1), u0.size, int(nt), k, dt, dx, threads)
+    return t, (u0 if nt % 2 == 0 else u1)
+
+
 def par_copy_if_i64(a: np.ndarray, threads, reps=3):
     lib = load()
     out = np.empty_like(a)

@@ -28,7 +28,7 @@ def _worker(rank, size, port, q):
         out = io.StringIO()
         with contextlib.redirect_stdout(out):
             bench.main(["--gpus", str(size), "--steps", "2", "--warmup", "1", "--logn", "22", "--no-cpu",
-                        "--no-pmc"], comm_tgt=(comm, tgt))
+                        "--no-pmc", "--stencil-logn", "22", "--stencil-steps", "40"], comm_tgt=(comm, tgt))
         q.put((rank, out.getvalue()))
     except Exception as e:
         q.put((rank, e))
@@ -62,5 +62,7 @@ def test_bench_two_ranks_one_json_line(gpu_target):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["global_elements"] == 2 * (1 << 22)
     x = d["extras"]
-    assert x["segmented_sort_uint64"]["ordered_across_partitions"] is True
-    assert x["stencil_heat_dist"]["interior_check"] is True
+    assert x["segmented_sort_uint64"]["sorted_and_ordered"] is True
+    assert x["stencil_heat_dist"]["ramp_check"] is True and x["stencil_heat_dist"]["points"] == 1 << 22
+    r = x["segmented_reduce_int64"]
+    assert r["ranks"] == 2 and r["gbs_per_rank"] > 0

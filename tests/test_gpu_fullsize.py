@@ -1,0 +1,159 @@
+"""Full-size checks at the benchmark's scales (BASELINE.json configs[1] and
+[2]: 2^30 int64/double reduce and scan, 2^30 uint64 sort), through
+size-independent properties and closed forms, plus the range overload of
+sort (container_algorithms/sort.hpp:102, sort_range_tests.hpp) and
+is_sorted (is_sorted.hpp).
+
+* double reduce/scan at 2^30: x_i = 0.5 * k_i with integers k_i in [0, 1023]
+  -> every partial sum is a multiple of 0.5 below 2^53, so every summation
+  order gives the same double: the GPU results equal 0.5 * the int64 results
+  bit for bit (the reference's all-1.0 benchmark, inclusive_scan_tests.hpp:26-60,
+  generalised);
+* mixed-sign double scan: |gpu - exact prefix| <= (2 ntiles + 64) u sum_{j<=i}|x_j|
+  (exact prefix in 80-bit long double on the host), a bound that stays
+  meaningful under cancellation;
+* sort of 2^30 uint64: a permutation of the input (XOR and wrapping sum of the
+  keys unchanged) with no adjacent pair out of order (device-side is_sorted)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import hpx_amd as hpx
+from hpx_amd import _lib as L
+from hpx_amd import execution as ex, functional as F
+from hpx_amd import parallel as P
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pol(gpu_target):
+    return ex.par.on(hpx.default_executor(gpu_target))
+
+
+def window(v, lo, n, dt):
+    out = np.empty(n, dt)
+    L.call("hpxhip_memcpy_async", out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(v.data() + lo * out.itemsize),
+           out.nbytes, L.D2H, v.target().stream)
+    v.target().synchronize()
+    return out
+
+
+def test_double_reduce_scan_2p30_exact(pol, gpu_target):
+    n = 1 << 30
+    k = hpx.vector(n, dtype=np.int64, tgt=gpu_target)
+    P.generate(pol, k.begin(), k.end(), "range", 0x5EED, 0, 1023)
+    x = hpx.vector(n, dtype=np.float64, tgt=gpu_target)
+    L.call("hpxhip_transform", L.I64, L.F64, L.F64, L.U_SCALE, L.scalars_buf(L.F64, [0.5]), ctypes.c_void_p(k.data()),
+           ctypes.c_void_p(x.data()), n, gpu_target.stream)
+    ki = P.reduce(pol, k.begin(), k.end(), 0, F.plus)
+    xs = P.reduce(pol, x.begin(), x.end(), 0.0, F.plus)
+    assert xs == 0.5 * ki and ki > 0
+    y = hpx.vector(n, dtype=np.float64, tgt=gpu_target)
+    P.inclusive_scan(pol, x.begin(), x.end(), y.begin(), F.plus, 0.0)
+    ky = hpx.vector(n, dtype=np.int64, tgt=gpu_target)
+    P.inclusive_scan(pol, k.begin(), k.end(), ky.begin(), F.plus, 0)
+    for lo in (0, (1 << 20) - 3, n // 2 + 4097, n - 4096):
+        np.testing.assert_array_equal(window(y, lo, 4096, np.float64), 0.5 * window(ky, lo, 4096, np.int64))
+    assert window(y, n - 1, 1, np.float64)[0] == xs
+    # exclusive: y_ex[i] = y_in[i] - x[i] exactly (all values are multiples of 0.5)
+    P.exclusive_scan(pol, x.begin(), x.end(), y.begin(), 0.0)
+    w = window(y, n - 4096, 4096, np.float64)
+    kk = window(ky, n - 4096, 4096, np.int64) - window(k, n - 4096, 4096, np.int64)
+    np.testing.assert_array_equal(w, 0.5 * kk)
+    for v in (k, x, y, ky):
+        v.free()
+
+
+def test_int64_scan_2p30_properties(pol, gpu_target):
+    n = 1 << 30
+    x = hpx.vector(n, dtype=np.int64, tgt=gpu_target)
+    P.generate(pol, x.begin(), x.end(), "range", 7, -(1 << 40), 1 << 40)
+    y = hpx.vector(n, dtype=np.int64, tgt=gpu_target)
+    P.inclusive_scan(pol, x.begin(), x.end(), y.begin(), F.plus, 11)
+    r = P.reduce(pol, x.begin(), x.end(), 11, F.plus)
+    assert window(y, n - 1, 1, np.int64)[0] == r
+    # sampled windows against the host restatement of the generator + a scan
+    for lo in (0, n // 3, n - 8192):
+        xs = O.generate(np.int64, "range", 8192, 7, -(1 << 40), 1 << 40, offset=lo)
+        base = 11 if lo == 0 else int(window(y, lo - 1, 1, np.int64)[0])
+        np.testing.assert_array_equal(window(y, lo, 8192, np.int64), O.scan(xs, base, True))
+    x.free()
+    y.free()
+
+
+def test_mixed_sign_double_scan_bound(pol, gpu_target):
+    n = (1 << 24) + 3
+    x = O.generate(np.float64, "unit", n, 0x5EED) - 0.5
+    dx = hpx.vector.from_host(x, gpu_target)
+    dy = hpx.vector(n, dtype=np.float64, tgt=gpu_target)
+    P.inclusive_scan(pol, dx.begin(), dx.end(), dy.begin(), F.plus, 0.0)
+    got = dy.to_host()
+    exact = np.cumsum(x.astype(np.longdouble))
+    u = 2.0 ** -53
+    ntiles = n // 12288 + 2
+    bound = (2 * ntiles + 64) * u * np.cumsum(np.abs(x))
+    err = np.abs(got.astype(np.longdouble) - exact).astype(np.float64)
+    assert np.all(err <= bound), float(np.max(err / bound))
+    # the bound is not vacuous: the prefixes cancel to a few units while sum|x| grows to n/4
+    assert float(np.max(np.abs(got[-1000:]))) < 0.01 * float(np.sum(np.abs(x)))
+
+
+@pytest.mark.parametrize("desc", [False, True])
+def test_sort_2p30_permutation_and_order(pol, gpu_target, desc):
+    n = 1 << 30
+    keys = hpx.vector(n, dtype=np.uint64, tgt=gpu_target)
+    P.generate(pol, keys.begin(), keys.end(), "bits", 7)
+    xor0 = P.reduce(pol, keys.begin(), keys.end(), 0, F.bit_xor)
+    sum0 = P.reduce(pol, keys.begin(), keys.end(), 0, F.plus)
+    comp = F.greater if desc else F.less
+    assert not P.is_sorted(pol, keys.begin(), keys.end(), comp)
+    P.sort(pol, keys.begin(), keys.end(), comp)
+    assert P.is_sorted(pol, keys.begin(), keys.end(), comp)
+    assert not P.is_sorted(pol, keys.begin(), keys.end(), F.less if desc else F.greater)
+    assert P.reduce(pol, keys.begin(), keys.end(), 0, F.bit_xor) == xor0
+    assert P.reduce(pol, keys.begin(), keys.end(), 0, F.plus) == sum0
+    keys.free()
+
+
+# ---------------------------------------------------- sort_range_tests.hpp
+@pytest.mark.parametrize("dt", [np.int64, np.uint32, np.float64, np.int32])
+def test_sort_range_overload(pol, gpu_target, dt):
+    # test_sort1/2: HPX_SORT_TEST_SIZE (5,000,000) random values, default and
+    # std::greater comparisons, sync and task policies; verify_ = sortedness
+    n = 5000000
+    rng = np.random.default_rng(int(np.dtype(dt).itemsize))
+    if np.dtype(dt).kind == "f":
+        h = rng.uniform(-1e300, 1e300, n).astype(dt)
+    else:
+        info = np.iinfo(dt)
+        h = rng.integers(info.min, info.max, n, dtype=dt, endpoint=True)
+    v = hpx.vector.from_host(h, gpu_target)
+    end = P.sort(pol, v)
+    assert end == v.end()
+    np.testing.assert_array_equal(v.to_host(), O.sort(h))
+    assert P.is_sorted(pol, v.begin(), v.end())
+    v2 = hpx.vector.from_host(h, gpu_target)
+    tpol = ex.par(ex.task).on(hpx.default_executor(gpu_target))
+    P.sort(tpol, v2, F.greater).get()
+    np.testing.assert_array_equal(v2.to_host(), O.sort(h, True))
+    assert P.is_sorted(tpol, v2.begin(), v2.end(), F.greater).get()
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 64, 65, 1000, 4097])
+def test_is_sorted_small(pol, gpu_target, n):
+    for dt in (np.int32, np.int64, np.float32):
+        h = np.sort(np.random.default_rng(n).integers(-100, 100, n).astype(dt))
+        v = hpx.vector.from_host(h, gpu_target)
+        assert P.is_sorted(pol, v.begin(), v.end())
+        if n >= 2:
+            h2 = h.copy()
+            h2[0] = h2.max() + 1  # one pair out of order
+            v2 = hpx.vector.from_host(h2, gpu_target)
+            assert not P.is_sorted(pol, v2.begin(), v2.end())
+            assert P.is_sorted(pol, v2.begin(), v2.end(), F.greater) == (n == 2)
+        # unaligned start
+        if n >= 3:
+            assert P.is_sorted(pol, v.begin() + 1, v.end())
