@@ -146,6 +146,14 @@ struct ordered_bits {
         else u = raw;
         return DESC ? ~u : u;
     }
+    // ordered bits -> storage bits
+    __device__ __forceinline__ U inverse(U o) const {
+        constexpr U sign = U(1) << (sizeof(U) * 8 - 1);
+        const U u = DESC ? ~o : o;
+        if constexpr (std::is_floating_point_v<T>) return (u & sign) ? (u ^ sign) : ~u;
+        else if constexpr (std::is_signed_v<T>) return u ^ sign;
+        else return u;
+    }
 };
 
 // ---------------------------------------------------------------------------

@@ -19,6 +19,29 @@ __device__ __forceinline__ G enc_agg(uint64_t c) { return static_cast<G>((c + 1)
 template <typename G>
 __device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 1) | 1u); }
 
+// Wave match of 8-bit digits: the lanes among `active` whose digit equals
+// this lane's.  Per bit one ballot (v_cmp on the lane's bit as 0/-1) folded
+// into both halves of the peer mask with one v_bitop3 each (acc & ~(m ^ x),
+// truth table 0x90): 4 VALU per bit where the select/xor/and form took 9
+// (scripts/ubench/bucket.hip; the ranking is the VALU-bound part of a pass).
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
+    uint32_t lo = static_cast<uint32_t>(active), hi = static_cast<uint32_t>(active >> 32);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(d), b, 1));
+        uint64_t m;
+        asm("v_cmp_ne_u32_e64 %0, 0, %1" : "=s"(m) : "v"(x));
+        lo = __builtin_amdgcn_bitop3_b32(lo, static_cast<uint32_t>(m), x, 0x90);
+        hi = __builtin_amdgcn_bitop3_b32(hi, static_cast<uint32_t>(m >> 32), x, 0x90);
+    }
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+// number of set bits of `peers` below this lane
+__device__ __forceinline__ uint32_t peers_below(uint64_t peers) {
+    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(peers >> 32),
+                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(peers), 0u));
+}
+
 // ---------------------------------------------------------------- histogram
 // One read of the keys -> all passes' 256-bin histograms.  Each bin has
 // COPIES lane-private LDS counters (lane % COPIES), interleaved so that bin
@@ -139,21 +162,14 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     }
 
     // ---- wave-level match ranking (stable: round-major, then lane order)
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t rank[ITEMS];
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = wbase + r * kWave + lane;
         const bool valid = full || i < n;
         const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
-        const uint32_t below = static_cast<uint32_t>(__builtin_popcountll(peers & lt_mask));
+        const uint64_t peers = match_digit(d, __ballot(valid));
+        const uint32_t below = peers_below(peers);
         const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(peers));
         const uint32_t old = s_whist[wave][d];
         rank[r] = old + below;
@@ -259,6 +275,195 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             if constexpr (HAS_VAL) vout[dst] = s_vals[i];
         }
     }
+}
+
+// ------------------------------------------------------- hybrid (MSD) tail
+// After two onesweep passes on the two most significant non-constant digits
+// (p2, then p1) the keys are ordered by the 16-bit prefix (digit p1, digit
+// p2); every prefix value is a contiguous bucket.
+constexpr int kBuckets = 1 << 16;
+
+template <typename U, typename X>
+__device__ __forceinline__ uint32_t bucket_of(U k, int s1, int s2, X xf) {
+    const U u = xf(k);
+    return (static_cast<uint32_t>(u >> s1) & 0xffu) << 8 | (static_cast<uint32_t>(u >> s2) & 0xffu);
+}
+
+// off[v] = first index whose prefix is >= v (v = 0..65536): a lower_bound per
+// bucket over the prefix-ordered keys instead of a pass over all of them.
+template <typename U, typename X>
+__global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ keys, uint64_t n, int s1, int s2, X xf,
+                                                        uint64_t* __restrict__ off) {
+    const uint32_t v = blockIdx.x * 256 + threadIdx.x;
+    if (v > static_cast<uint32_t>(kBuckets)) return;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (bucket_of(keys[mid], s1, s2, xf) < v) lo = mid + 1;
+        else hi = mid;
+    }
+    off[v] = lo;
+}
+
+// --------------------------------------------------------- segment sort
+// One workgroup sorts one segment (a run of whole buckets, at most
+// THREADS*ITEMS keys) completely in LDS and writes it back in place.  The
+// segment's keys agree on every bit at or above `top` (the highest bit in
+// which its first and last keys differ, or -- one bucket -- the top of the
+// next live digit).  Below it:
+//   1. two stable LDS passes (the onesweep's wave match ranking, per-wave
+//      16-bit counters) on the 16 bits under `top`: the keys are then in
+//      order up to runs that agree on all those bits (for 2^30 random keys a
+//      16384-key bucket has runs of 1.1 keys on average, rarely over 5);
+//   2. odd-even transposition of neighbours by whole keys until a round
+//      swaps nothing -- an inversion can only sit inside one run, so the
+//      rounds needed are the longest run's length;
+//   3. a segment whose runs do not settle within OE_MAX rounds (skewed low
+//      bits) is finished by stable LSD passes over every bit under `top`.
+// Six 8-bit LDS passes for the 48 bits under a 16-bit prefix took 2.4 ms
+// each at 2^30 keys (VALU-bound ranking); this form replaces four of them.
+template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16>
+__global__ __launch_bounds__(THREADS) void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg,
+                                                          int top_single, X xf) {
+    constexpr int WAVES = THREADS / kWave;
+    constexpr int CHUNK = ITEMS * kWave;
+    constexpr int BITS = static_cast<int>(sizeof(U) * 8);
+    static_assert(THREADS * ITEMS < 65536, "16-bit LDS counters");
+    __shared__ alignas(16) U s_keys[THREADS * ITEMS];
+    __shared__ uint16_t s_whist[WAVES][kRadix];
+    __shared__ uint32_t s_local[kRadix];
+    __shared__ uint32_t s_wsum[kRadix / kWave];
+
+    const int t = threadIdx.x;
+    const int wave = t / kWave;
+    const int lane = lane_id();
+    const uint64_t b = seg[2 * blockIdx.x];  // (begin, end) pairs
+    const uint32_t m = static_cast<uint32_t>(seg[2 * blockIdx.x + 1] - b);
+    if (m < 2) return;
+    const U diff = xf(keys[b]) ^ xf(keys[b + m - 1]);
+    int top = top_single;
+    if (diff) {
+        const int hb = BITS - (sizeof(U) == 8 ? __builtin_clzll(static_cast<uint64_t>(diff))
+                                               : __builtin_clz(static_cast<uint32_t>(diff)));
+        top = hb > top ? hb : top;
+    }
+    if (top <= 0) return;  // all keys equal
+
+    const uint32_t wbase = static_cast<uint32_t>(wave) * CHUNK;
+    const uint32_t have = m > wbase ? m - wbase : 0u;
+    const int nfull = static_cast<int>(have >= static_cast<uint32_t>(CHUNK) ? ITEMS : have / kWave);
+    const uint64_t tail_mask = (have % kWave) ? (~0ull >> (kWave - have % kWave)) : 0ull;
+    auto active = [&](int r) -> uint64_t { return r < nfull ? ~0ull : (r == nfull ? tail_mask : 0ull); };
+    U* gkeys = keys + b;
+    U* lkeys = s_keys + wbase;
+
+    U k[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r)
+        k[r] = ((active(r) >> lane) & 1u) ? ld_stream(&gkeys[wbase + r * kWave + lane]) : U(0);
+
+    // one stable pass on the digit at `shift`: registers -> s_keys (ranked)
+    auto pass = [&](int shift) {
+        __syncthreads();  // earlier readers of s_keys / s_whist are done
+        for (int i = t; i < WAVES * kRadix / 2; i += THREADS) reinterpret_cast<uint32_t*>(&s_whist[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t rank[ITEMS];
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const uint64_t act = active(r);
+            if (act == 0) break;  // uniform
+            const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
+            const uint64_t peers = match_digit(d, act);
+            const uint32_t below = peers_below(peers);
+            const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(peers));
+            const uint32_t old = s_whist[wave][d];
+            rank[r] = old + below;
+            if (((act >> lane) & 1u) && below == 0) s_whist[wave][d] = static_cast<uint16_t>(old + cnt);
+        }
+        __syncthreads();
+        uint32_t count = 0, incl = 0;
+        if (t < kRadix) {
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) {
+                const uint32_t c = s_whist[w][t];
+                s_whist[w][t] = static_cast<uint16_t>(count);
+                count += c;
+            }
+            incl = wave_inclusive_scan(count, op_plus{});
+            if (lane == kWave - 1) s_wsum[wave] = incl;
+        }
+        __syncthreads();
+        if (t < kRadix) {
+            uint32_t pre = 0;
+#pragma unroll
+            for (int w = 0; w < kRadix / kWave; ++w)
+                if (w < wave) pre += s_wsum[w];
+            s_local[t] = pre + incl - count;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const uint64_t act = active(r);
+            if (act == 0) break;
+            if ((act >> lane) & 1u) {
+                const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
+                s_keys[s_local[d] + s_whist[wave][d] + rank[r]] = k[r];
+            }
+        }
+        __syncthreads();
+    };
+    auto reload = [&] {
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) k[r] = ((active(r) >> lane) & 1u) ? lkeys[r * kWave + lane] : U(0);
+    };
+
+    // pass schedule (one inlined copy of `pass`): the two passes under
+    // `top`, then -- only for a segment the odd-even rounds do not settle --
+    // the full LSD over every bit under `top`
+    bool lsd = false;
+    int npass = 2;
+    for (int q = 0; q < npass;) {
+        const int lo = lsd ? top - 8 * (npass - q) : top - 8 * (2 - q);
+        pass(lo > 0 ? lo : 0);
+        if (++q < npass) {
+            reload();
+            continue;
+        }
+        if (lsd || top <= 16 || OE_MAX < 0) break;  // OE_MAX < 0: ablation (two passes only)
+        bool settled = false;
+        for (int it = 0; it < OE_MAX && !settled; ++it) {
+            int swapped = 0;
+            using V2 = vec<U, 2>;
+            for (uint32_t i = t; 2 * i + 1 < m; i += THREADS) {  // pairs (2i, 2i+1): one 16-B LDS access
+                V2 p = reinterpret_cast<V2*>(s_keys)[i];
+                if (xf(p.v[0]) > xf(p.v[1])) {
+                    const U x = p.v[0];
+                    p.v[0] = p.v[1];
+                    p.v[1] = x;
+                    reinterpret_cast<V2*>(s_keys)[i] = p;
+                    swapped = 1;
+                }
+            }
+            __syncthreads();
+            for (uint32_t i = t; 2 * i + 2 < m; i += THREADS) {  // pairs (2i+1, 2i+2)
+                const U a = s_keys[2 * i + 1], c = s_keys[2 * i + 2];
+                if (xf(a) > xf(c)) {
+                    s_keys[2 * i + 1] = c;
+                    s_keys[2 * i + 2] = a;
+                    swapped = 1;
+                }
+            }
+            settled = !__syncthreads_or(swapped);
+        }
+        if (settled) break;
+        // stable LSD over every bit under `top`, from the keys as the rounds left them
+        lsd = true;
+        npass = (top + 7) / 8;
+        q = 0;
+        __syncthreads();
+        reload();
+    }
+    for (uint32_t i = t; i < m; i += THREADS) st_stream(&gkeys[i], s_keys[i]);
 }
 
 }  // namespace sort_detail

@@ -1,0 +1,93 @@
+"""The hybrid tail of the 64-bit keys-only sort (sort.hip: two onesweep passes
+on the two most significant non-constant digits, bucket bounds by lower_bound,
+one LDS-resident LSD sort per segment of whole buckets; oversized buckets
+finished by per-bucket LSD, many of them by plain LSD), checked element for
+element against numpy's sort on the distributions that steer it down each
+branch.  Sizes start at the hybrid's 2^22-key threshold.
+
+Parity: std::sort's order for integer keys (sort.hpp:78-229 via the oracle's
+O.sort, itself numpy's stable sort) and the IEEE total order for doubles."""
+import numpy as np
+import pytest
+
+import hpx_amd as hpx
+from hpx_amd import execution as ex, functional as F
+from hpx_amd import parallel as P
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pol(gpu_target):
+    return ex.par.on(hpx.default_executor(gpu_target))
+
+
+def check(pol, tgt, h, desc=False):
+    v = hpx.vector.from_host(h, tgt)
+    P.sort(pol, v.begin(), v.end(), F.greater if desc else F.less)
+    got = v.to_host()
+    v.free()
+    np.testing.assert_array_equal(got, O.sort(h, desc))
+
+
+@pytest.mark.parametrize("logn", [22, 24])
+@pytest.mark.parametrize("desc", [False, True])
+def test_uniform_u64(pol, gpu_target, logn, desc):
+    # 2^22: buckets of ~64 keys packed into multi-bucket segments (prefix passes
+    # run in LDS); 2^24: ~256-key buckets
+    h = np.random.default_rng(logn).integers(0, 2**64 - 1, 1 << logn, dtype=np.uint64, endpoint=True)
+    check(pol, gpu_target, h, desc)
+
+
+@pytest.mark.parametrize("dt", [np.int64, np.float64])
+def test_signed_and_double(pol, gpu_target, dt):
+    rng = np.random.default_rng(5)
+    n = (1 << 23) + 12345
+    if dt is np.float64:
+        h = rng.standard_normal(n) * np.exp2(rng.integers(-60, 60, n))
+        h[:5] = [0.0, -0.0, np.inf, -np.inf, 1e-310]
+    else:
+        h = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    check(pol, gpu_target, h)
+    check(pol, gpu_target, h, True)
+
+
+def test_constant_middle_digits(pol, gpu_target):
+    # bits 40..59 zero: live digits 7, 4, 3, 2, 1, 0 -> prefix (7, 4), 1024 buckets of ~8K
+    rng = np.random.default_rng(11)
+    n = 1 << 23
+    h = (rng.integers(0, 4, n, dtype=np.uint64) << np.uint64(60)) | rng.integers(0, 1 << 40, n, dtype=np.uint64)
+    check(pol, gpu_target, h)
+
+
+def test_few_oversized_buckets(pol, gpu_target):
+    # one prefix (0x12, 0x34) holds 30000 extra keys: its bucket exceeds the LDS
+    # segment (18432 keys) and is finished by per-bucket LSD; the marginal
+    # histograms alone do not reveal it
+    rng = np.random.default_rng(12)
+    n = 1 << 23
+    h = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    h[:30000] = (np.uint64(0x1234) << np.uint64(48)) | rng.integers(0, 1 << 48, 30000, dtype=np.uint64)
+    h[30000:30100] = np.uint64(0x1234) << np.uint64(48)  # duplicates inside the big bucket
+    check(pol, gpu_target, h)
+
+
+def test_many_oversized_buckets(pol, gpu_target):
+    # digit 6 == digit 7 for every key: 256 buckets of 32K keys -> plain LSD finish
+    rng = np.random.default_rng(13)
+    n = 1 << 23
+    top = rng.integers(0, 256, n, dtype=np.uint64)
+    h = (top << np.uint64(56)) | (top << np.uint64(48)) | rng.integers(0, 1 << 48, n, dtype=np.uint64)
+    check(pol, gpu_target, h)
+
+
+def test_heavy_duplicates(pol, gpu_target):
+    # few distinct values: most digits constant -> fewer than three live digits (LSD)
+    rng = np.random.default_rng(14)
+    n = 1 << 23
+    vals = rng.integers(0, 2**64 - 1, 3, dtype=np.uint64, endpoint=True)
+    check(pol, gpu_target, vals[rng.integers(0, 3, n)])
+    # 2^16 distinct values spread over all digits: buckets of duplicates
+    vals = rng.integers(0, 2**64 - 1, 1 << 16, dtype=np.uint64, endpoint=True)
+    check(pol, gpu_target, vals[rng.integers(0, 1 << 16, n)])
