@@ -64,7 +64,7 @@ struct tile_shape {
 
 struct sort_layout {
     uint64_t ntiles;
-    size_t alt_keys, alt_vals, hist, start, bounds, segs, counter, lb, lb_bytes, total;
+    size_t alt_keys, alt_vals, hist, bits, start, bounds, segs, counter, lb, lb_bytes, total;
     bool wide;  // 64-bit granules
 };
 
@@ -79,6 +79,8 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     off = align_up(off + n * vsize, 256);
     L.hist = off;
     off += 8 * kRadix * 8;
+    L.bits = off;  // OR / AND of the ordered keys
+    off += 256;
     L.start = off;
     off += 8 * kRadix * 8;
     L.bounds = off;  // hybrid: bucket bounds and segment table (65537 u64 each)
@@ -119,11 +121,15 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     const int passes = static_cast<int>(sizeof(U));
     const unsigned hist_grid = static_cast<unsigned>(current_device_info().cus * kHistBlocksPerCU);
 
-    // all passes' histograms of keys[0, cnt) -> hist, exclusive bin starts -> start
-    auto histogram = [&](const U* k, uint64_t cnt) -> int {
+    auto* bits = reinterpret_cast<unsigned long long*>(base + L.bits);
+    // histograms of digits [first, passes) of keys[0, cnt) -> hist, their
+    // exclusive bin starts -> start, OR / AND of the keys -> bits
+    auto histogram = [&](const U* k, uint64_t cnt, int first) -> int {
         HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8, s));
-        hipLaunchKernelGGL((k_hist<U, X, kHistThreads>), dim3(hist_grid), dim3(kHistThreads), 0, s, k, cnt, passes,
-                           X{}, hist);
+        HPXHIP_CHECK(hipMemsetAsync(bits, 0, 8, s));
+        HPXHIP_CHECK(hipMemsetAsync(bits + 1, 0xff, 8, s));
+        hipLaunchKernelGGL((k_hist<U, X, kHistThreads>), dim3(hist_grid), dim3(kHistThreads), 0, s, k, cnt, first, passes,
+                           X{}, hist, bits);
         HPXHIP_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_bin_offsets, dim3(passes), dim3(256), 0, s, hist, start);
         HPXHIP_CHECK_LAUNCH();
@@ -146,18 +152,28 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         return 0;
     };
 
-    if ((rc = histogram(static_cast<const U*>(keys), n))) return rc;
-    // Pass skipping needs the histogram on the host.
+    // Pass skipping needs the live digits on the host (a digit is live iff
+    // OR and AND of the keys differ on it).  A sort that may take the hybrid
+    // path counts only the two top digits first (the LDS atomics, not the
+    // read, bound k_hist) and counts the rest only when it needs them.
     std::vector<unsigned long long> h(static_cast<size_t>(passes) * kRadix);
-    HPXHIP_CHECK(hipMemcpyAsync(h.data(), hist, h.size() * 8, hipMemcpyDeviceToHost, s));
-    HPXHIP_CHECK(hipStreamSynchronize(s));
     std::vector<int> live;  // non-constant digits, most significant first
-    for (int p = passes - 1; p >= 0; --p) {
-        bool constant = false;
-        for (int d = 0; d < kRadix; ++d)
-            if (h[p * kRadix + d] == n) constant = true;
-        if (!constant) live.push_back(p);
-    }
+    int counted = (!HAS_VAL && sizeof(U) == 8 && n >= kHybridMin) ? passes - 2 : 0;
+    auto count_digits = [&](int first) -> int {
+        if ((rc = histogram(static_cast<const U*>(keys), n, first))) return rc;
+        unsigned long long ob[2];
+        HPXHIP_CHECK(hipMemcpyAsync(h.data(), hist, h.size() * 8, hipMemcpyDeviceToHost, s));
+        HPXHIP_CHECK(hipMemcpyAsync(ob, bits, 16, hipMemcpyDeviceToHost, s));
+        HPXHIP_CHECK(hipStreamSynchronize(s));
+        live.clear();
+        for (int p = passes - 1; p >= 0; --p)
+            if (((ob[0] ^ ob[1]) >> (8 * p)) & 0xffu) live.push_back(p);
+        counted = first;
+        return 0;
+    };
+    if ((rc = count_digits(counted))) return rc;
+    if (counted > 0 && !(live.size() >= 3 && live[0] == passes - 1 && live[1] == passes - 2))
+        if ((rc = count_digits(0))) return rc;
 
     U* kc = static_cast<U*>(keys);
     U* ka = reinterpret_cast<U*>(base + L.alt_keys);
@@ -165,6 +181,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     VAL* va = reinterpret_cast<VAL*>(base + L.alt_vals);
     // LSD over live[from..] (least significant first), whole array, result in keys
     auto lsd = [&](size_t from) -> int {
+        if (counted > 0 && (rc = histogram(kc, n, 0))) return rc;  // a permutation: same counts
         int executed = 0;
         for (size_t i = live.size(); i-- > from;) {
             if ((rc = pass(kc, ka, vc, va, n, live[i]))) return rc;
@@ -247,7 +264,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     }
     // oversized buckets: LSD over the low digits of each, with its own histogram
     for (const auto& [bs, len] : big) {
-        if ((rc = histogram(kc + bs, len))) return rc;
+        if ((rc = histogram(kc + bs, len, 0))) return rc;
         U* a = kc + bs;
         U* b = ka + bs;
         for (size_t i = live.size(); i-- > 2;) {

@@ -50,9 +50,13 @@ __device__ __forceinline__ uint32_t peers_below(uint64_t peers) {
 // 32/COPIES, instead of mod 32 (the single-copy histogram spent 72 % of its
 // LDS cycles in bank conflicts, profiles/r01_pmc_sort.txt).  Keys are read
 // with nontemporal 16-B loads.
+// Digits [first, passes) are counted; bits[0] / bits[1] receive the OR / AND
+// of all ordered keys (a digit is constant iff OR and AND agree on it), so a
+// caller may count only the digits it needs first.
 template <typename U, typename X, int THREADS = 256, int COPIES = 4>
-__global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, uint64_t n, int passes, X xf,
-                                                   unsigned long long* __restrict__ hist) {
+__global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, uint64_t n, int first, int passes, X xf,
+                                                   unsigned long long* __restrict__ hist,
+                                                   unsigned long long* __restrict__ bits) {
     constexpr int P = static_cast<int>(sizeof(U));
     __shared__ uint32_t h[P * kRadix * COPIES];
     for (int i = threadIdx.x; i < P * kRadix * COPIES; i += THREADS) h[i] = 0;
@@ -64,10 +68,13 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
     const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * THREADS + threadIdx.x;
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * THREADS;
     const VT* vk = reinterpret_cast<const VT*>(keys);
+    U any = 0, all = static_cast<U>(~U(0));
     auto count = [&](U b) {
+        any |= b;
+        all &= b;
 #pragma unroll
         for (int p = 0; p < P; ++p)
-            if (p < passes) atomicAdd(&h[(p * kRadix + ((b >> (8 * p)) & 0xff)) * COPIES + copy], 1u);
+            if (p >= first && p < passes) atomicAdd(&h[(p * kRadix + ((b >> (8 * p)) & 0xff)) * COPIES + copy], 1u);
     };
     for (uint64_t i = tid; i < nvec; i += stride * 4) {
         VT x[4];
@@ -82,8 +89,14 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
             }
     }
     if (tid < n - nvec * V) count(xf(keys[nvec * V + tid]));
+    any = wave_reduce(any, op_bit_or{});
+    all = wave_reduce(all, op_bit_and{});
+    if (lane_id() == 0) {
+        atomicOr(&bits[0], static_cast<unsigned long long>(any));
+        atomicAnd(&bits[1], static_cast<unsigned long long>(all) | (sizeof(U) == 8 ? 0ull : ~0ull << 32));
+    }
     __syncthreads();
-    for (int i = threadIdx.x; i < passes * kRadix; i += THREADS) {
+    for (int i = threadIdx.x + first * kRadix; i < passes * kRadix; i += THREADS) {
         uint32_t c = 0;
 #pragma unroll
         for (int k = 0; k < COPIES; ++k) c += h[i * COPIES + k];

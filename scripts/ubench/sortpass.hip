@@ -21,7 +21,7 @@ int main() {
   const uint64_t N = 1ull << 30;
   U *kin, *kout; unsigned long long *hist, *start; uint32_t *lbws, *err;
   CK(hipMalloc(&kin, N * 8)); CK(hipMalloc(&kout, N * 8)); CK(hipMalloc(&hist, 8 * 256 * 8));
-  CK(hipMalloc(&start, 8 * 256 * 8)); CK(hipMalloc(&lbws, 256 + (N / 4096 + 1) * 256 * 4)); CK(hipMalloc(&err, 64));
+  CK(hipMalloc(&start, 9 * 256 * 8)); CK(hipMalloc(&lbws, 256 + (N / 4096 + 1) * 256 * 4)); CK(hipMalloc(&err, 64));
   CK(hipMemset(err, 0, 64)); CK(hipMemset(hist, 0, 8 * 256 * 8));
 
   gen<<<N / 256, 256>>>(kin, N);
@@ -35,9 +35,9 @@ int main() {
     printf("%-40s min %7.3f ms med %7.3f ms  %7.1f GB/s\n", name, t[0], t[3], bytes / t[0] / 1e6);
   };
   run("hist (8 passes)", 8.0 * N, [&] { CK(hipMemsetAsync(hist, 0, 8*256*8, 0));
-      k_hist<U, X, 256><<<512, 256>>>(kin, N, 8, X{}, hist); });
+      k_hist<U, X, 256><<<512, 256>>>(kin, N, 0, 8, X{}, hist, start + 8 * 256); });
   run("hist (8 passes) 1024 blocks", 8.0 * N, [&] { CK(hipMemsetAsync(hist, 0, 8*256*8, 0));
-      k_hist<U, X, 256><<<1024, 256>>>(kin, N, 8, X{}, hist); });
+      k_hist<U, X, 256><<<1024, 256>>>(kin, N, 0, 8, X{}, hist, start + 8 * 256); });
   k_bin_offsets<<<8, 256>>>(hist, start);
   CK(hipDeviceSynchronize());
   auto pass = [&](auto th_c, auto it_c, auto lb_c, const char* name) {

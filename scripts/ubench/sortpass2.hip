@@ -45,13 +45,14 @@ void bench(const char* name, F f, double keys) {
 int main() {
     const uint64_t n = 1ull << 30;
     uint64_t *kin, *kout;
-    unsigned long long *hist, *start;
+    unsigned long long *hist, *start, *bits;
     uint32_t *counter, *err;
     void* lb;
     CK(hipMalloc(&kin, n * 8));
     CK(hipMalloc(&kout, n * 8));
     CK(hipMalloc(&hist, 8 * 256 * 8));
     CK(hipMalloc(&start, 8 * 256 * 8));
+    CK(hipMalloc(&bits, 256));
     CK(hipMalloc(&counter, 256));
     CK(hipMalloc(&err, 64));
     const size_t lb_bytes = (n / 2048 + 1) * 256 * 4;  // >= ntiles * 256 granules for tiles >= 2048 keys
@@ -61,12 +62,12 @@ int main() {
     CK(hipEventCreate(&e1));
     hipLaunchKernelGGL(k_fill_rand, dim3(n / 256), dim3(256), 0, 0, kin, n);
     using X = ordered_bits<uint64_t, false>;
-#define HIST(C, G)                                                                                     \
-    bench("hist copies" #C " grid" #G, [&] {                                                          \
+#define HIST(C, G, FIRST)                                                                                     \
+    bench("hist copies" #C " grid" #G " digits from " #FIRST, [&] {                                                          \
         CK(hipMemsetAsync(hist, 0, 8 * 256 * 8));                                                    \
-        hipLaunchKernelGGL((k_hist<uint64_t, X, 256, C>), dim3(G), dim3(256), 0, 0, kin, n, 8, X{}, hist); \
+        hipLaunchKernelGGL((k_hist<uint64_t, X, 256, C>), dim3(G), dim3(256), 0, 0, kin, n, FIRST, 8, X{}, hist, bits); \
     }, n / 2.0)  // 8 B/key: GB/s column = read bandwidth
-    HIST(1, 512); HIST(4, 512); HIST(8, 512); HIST(8, 1024); HIST(4, 1024);
+    HIST(4, 1024, 0); HIST(4, 1024, 6); HIST(4, 1024, 7);
     hipLaunchKernelGGL(k_bin_offsets, dim3(8), dim3(256), 0, 0, hist, start);
     CK(hipDeviceSynchronize());
 
