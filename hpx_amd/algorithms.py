@@ -497,6 +497,8 @@ def _for_loop_reduce(pol, n, vars_, red, body):
         raise IndexError("for_loop_n: loop body refers to a variable that is not passed") from None
     if not all(isinstance(v, iterator) for v in ins):
         raise TypeError("for_loop_n: the reduction body must read device iterators")
+    if n > 0 and any(it.pos < 0 or it.pos + n - 1 >= it.vec.size() for it in ins):
+        raise ValueError("for_loop_n: an induction walks outside its vector")
     stream, tgt, is_task = _context(pol, *ins)
     adt = dtype_code(red.var.dtype)
     dev, host = _slots_for(tgt).next()

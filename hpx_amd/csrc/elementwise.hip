@@ -358,11 +358,22 @@ int hpxhip_transform_binary(int in_dtype, int compute_dtype, int out_dtype, int 
     });
 }
 
+// A strided walk must stay inside a 47-bit address span (the GPU's virtual
+// address space): any larger |stride| * (n - 1) is a caller error (e.g. an
+// unsigned stride wrapped into a huge one), never a valid range.
+static bool strided_span_ok(int64_t stride, uint64_t n, size_t elem) {
+    if (n < 2) return true;
+    const unsigned __int128 mag = static_cast<unsigned __int128>(stride < 0 ? -static_cast<__int128>(stride) : stride);
+    return mag * (n - 1) * elem < (static_cast<unsigned __int128>(1) << 47);
+}
+
 int hpxhip_transform_strided(int in_dtype, int compute_dtype, int out_dtype, int unary_kind, const void* scalars,
                              const void* in, int64_t in_stride, void* out, int64_t out_stride, uint64_t n,
                              hpxhip_stream stream) {
     if (n == 0) return 0;
     if (!in || !out || (out_stride == 0 && n > 1)) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    if (!strided_span_ok(in_stride, n, dtype_size(in_dtype)) || !strided_span_ok(out_stride, n, dtype_size(out_dtype)))
+        return HPXHIP_ERROR_INVALID_ARGUMENT;
     if (in_stride == 1 && out_stride == 1)
         return hpxhip_transform(in_dtype, compute_dtype, out_dtype, unary_kind, scalars, in, out, n, stream);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -389,6 +400,9 @@ int hpxhip_transform_binary_strided(int in_dtype, int compute_dtype, int out_dty
                                     hpxhip_stream stream) {
     if (n == 0) return 0;
     if (!in1 || !in2 || !out || (out_stride == 0 && n > 1)) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    if (!strided_span_ok(in1_stride, n, dtype_size(in_dtype)) || !strided_span_ok(in2_stride, n, dtype_size(in_dtype)) ||
+        !strided_span_ok(out_stride, n, dtype_size(out_dtype)))
+        return HPXHIP_ERROR_INVALID_ARGUMENT;
     if (in1_stride == 1 && in2_stride == 1 && out_stride == 1)
         return hpxhip_transform_binary(in_dtype, compute_dtype, out_dtype, binary_kind, scalars, in1, in2, out, n,
                                        stream);

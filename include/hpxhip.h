@@ -242,7 +242,12 @@ int hpxhip_transform_binary(int in_dtype, int compute_dtype, int out_dtype, int 
  *   out[i*out_stride] = (out_t) f((compute_t) in1[i*s1], (compute_t) in2[i*s2]) (binary)
  * Strides are in elements and may be negative; an input stride may be 0.  An
  * output stride of 0 with n > 1 is HPXHIP_ERROR_INVALID_ARGUMENT (every
- * iteration would write one element). */
+ * iteration would write one element), and so is a walk whose span
+ * |stride| * (n-1) * size reaches 2^47 bytes.  Like the reference's raw
+ * pointer inductions, the ABI does not know the allocations: a walk that
+ * leaves its buffer within that span is the caller's error (the Python mirror
+ * checks it against the vector; the C++ layer, pointer-based as HPX's
+ * iterators are, does not). */
 int hpxhip_transform_strided(int in_dtype, int compute_dtype, int out_dtype, int unary_kind,
                              const void* scalars, const void* in, int64_t in_stride, void* out,
                              int64_t out_stride, uint64_t n, hpxhip_stream stream);

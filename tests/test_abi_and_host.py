@@ -61,6 +61,15 @@ def test_error_strings_and_no_device_behaviour():
     assert lib.hpxhip_fill(L.F64, None, None, 10, None) == L.ERROR_INVALID_ARGUMENT
     assert lib.hpxhip_scan(L.I64, L.PLUS, 1, 0, None, None, None, None, None, 5, None, None, 0) == L.ERROR_INVALID_ARGUMENT
     assert lib.hpxhip_fill(L.F64, None, None, 0, None) == 0  # empty range: no-op
+    # strided walks: span |stride| * (n-1) * size must stay below 2^47 bytes
+    import ctypes
+    fake = ctypes.c_void_p(1 << 20)
+    big = ctypes.c_int64(-(1 << 44))   # e.g. a wrapped unsigned stride
+    assert lib.hpxhip_transform_strided(L.I64, L.I64, L.I64, L.U_IDENTITY, None, fake, big, fake, ctypes.c_int64(1),
+                                        ctypes.c_uint64(10), None) == L.ERROR_INVALID_ARGUMENT
+    assert lib.hpxhip_transform_binary_strided(L.I64, L.I64, L.I64, L.B_ADD, None, fake, ctypes.c_int64(1), fake,
+                                               ctypes.c_int64(1), fake, big, ctypes.c_uint64(10),
+                                               None) == L.ERROR_INVALID_ARGUMENT
 
 
 def test_scratch_size_queries():

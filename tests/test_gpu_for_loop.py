@@ -159,6 +159,10 @@ def test_for_loop_reduction_argument_checks(gpu_target):
     with pytest.raises(TypeError):
         P.for_loop_n(pol, d.begin(), 16, P.reduction_plus(s), P.reduction_plus(s),
                      F.accumulate(1, F.identity(), 0))
+    with pytest.raises(ValueError):  # the induction read by the body runs past its vector
+        P.for_loop_n(pol, d.begin(), 16, P.induction(d.begin() + 1), P.reduction_plus(s),
+                     F.accumulate(2, F.multiply(), 0, 1))
+    assert int(s[0]) == 0
 
 
 # ---------------------------------------------- strided pointer inductions
