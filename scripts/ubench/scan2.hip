@@ -78,7 +78,7 @@ struct bench {
       k_abl<ID, LB, SCAN><<<ntiles, 1024>>>((const int64_t*)in, (int64_t*)out, N, reinterpret_cast<uint32_t*>(ws), st);
     }, SCAN ? tile : 0);
   }
-  template <int R, int TH, int LBK = 1>
+  template <int R, int TH, int LBK = 1, int MINW = 1>
   void shipped(const char* name) {
     const uint64_t tile = scan_detail::tile_elems<T, R, TH>();
     const uint64_t ntiles = (N + tile - 1) / tile;
@@ -86,7 +86,7 @@ struct bench {
     tile_state<T> st{reinterpret_cast<uint64_t*>(ws + 256), err};
     run(name, [&] {
       CK(hipMemsetAsync(ws, 0, total, 0));
-      scan_detail::k_scan<T, Conv, op_plus, true, true, R, TH, true, 1, false, LBK><<<ntiles, TH>>>(
+      scan_detail::k_scan<T, Conv, op_plus, true, true, R, TH, true, MINW, false, LBK><<<ntiles, TH>>>(
             in, out, N, Conv{0, 0}, op_plus{}, T(0), nullptr, reinterpret_cast<uint32_t*>(ws), st);
     }, tile);
   }
@@ -120,15 +120,15 @@ int main() {
   int cus = 0; CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   bench<int64_t> bi{N, (int64_t*)in, (int64_t*)out, ws, err, e0, e1, cus};
   bench<double> bd{N, (double*)in, (double*)out, ws, err, e0, e1, cus};
-  for (int rep = 0; rep < 3; ++rep) {
+  for (int rep = 0; rep < 2; ++rep) {
     k_ones<int64_t><<<8192, 256>>>((int64_t*)in, N); CK(hipDeviceSynchronize());
-    bi.shipped<16, 1024>("i64 shipped T1024 R16 K1");
-    bi.shipped<16, 1024, 2>("i64 shipped T1024 R16 K2");
-    bi.shipped<16, 1024, 4>("i64 shipped T1024 R16 K4");
-    bi.abl<0, false, true>("i64 abl atomic, no lookback");
-    k_ones<double><<<8192, 256>>>((double*)in, N); CK(hipDeviceSynchronize());
-    bd.shipped<12, 1024>("f64 shipped T1024 R12 K1");
-    bd.shipped<12, 1024, 4>("f64 shipped T1024 R12 K4");
+    bi.shipped<16, 1024>("i64 shipped T1024 R16 (256 KiB, 1/CU)");
+    bi.shipped<16, 512, 1, 2>("i64 T512 R16 MINW2 (128 KiB, 2/CU)");
+    bi.shipped<8, 1024, 1, 2>("i64 T1024 R8 MINW2 (128 KiB, 2/CU)");
+    bi.shipped<16, 256, 1, 4>("i64 T256 R16 MINW4 (64 KiB, 4/CU)");
+    bi.shipped<8, 512, 1, 4>("i64 T512 R8 MINW4 (64 KiB, 4/CU)");
+    bi.shipped<8, 512, 4, 4>("i64 T512 R8 MINW4 K4 (64 KiB, 4/CU)");
+    bi.shipped<12, 512, 1, 2>("i64 T512 R12 MINW2 (96 KiB, 2/CU)");
   }
   uint32_t h = 0; CK(hipMemcpy(&h, err, 4, hipMemcpyDeviceToHost)); printf("deverr %u\n", h);
   return 0;
