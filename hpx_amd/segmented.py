@@ -169,14 +169,76 @@ def ring_halo_ops(dist, rank, size, first, last, left_halo, right_halo):
             dist.P2POp(dist.irecv, left_halo, left), dist.P2POp(dist.irecv, right_halo, right)]
 
 
+class _DeviceMemory:
+    """TorchComm's view of the library's device memory (the product path):
+    torch tensors on the target's GPU, collectives enqueued on the library
+    stream through torch.cuda.ExternalStream, library buffers wrapped
+    without a copy through __cuda_array_interface__."""
+
+    def __init__(self, torch, tgt):
+        self.torch = torch
+        self.device = torch.device("cuda", tgt.device)
+
+    def ctx(self, stream):
+        s = self.torch.cuda.ExternalStream(stream.value if hasattr(stream, "value") else int(stream),
+                                           device=self.device)
+        return self.torch.cuda.stream(s)
+
+    def handle(self, t):
+        return t.data_ptr()
+
+    def span(self, buf, off, count, itemsize):
+        nbytes, addr = int(count) * itemsize, buf.data() + int(off) * itemsize
+
+        class _cai:
+            __cuda_array_interface__ = {"shape": (max(1, nbytes),), "typestr": "|u1", "data": (int(addr), False),
+                                        "version": 2, "strides": None}
+        return self.torch.as_tensor(_cai(), device=self.device)[:nbytes]
+
+    def put(self, t, src, nbytes, stream):  # halo staging: library memory -> tensor
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(src), nbytes, L.D2D, stream)
+
+    def get(self, dst, t, nbytes, stream):  # tensor -> library memory
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(dst), ctypes.c_void_p(t.data_ptr()), nbytes, L.D2D, stream)
+
+
+class _HostMemory:
+    """The same calls over host numpy buffers (gloo on the CPU): lets the
+    multi-rank tests run TorchComm's own collective sequence -- packed
+    all_gather_into_tensor, uneven all_to_all_single into views of the
+    destination, the batch_isend_irecv halo ring -- with numpy test engines."""
+
+    def __init__(self, torch):
+        self.torch = torch
+        self.device = torch.device("cpu")
+
+    def ctx(self, stream):
+        import contextlib
+        return contextlib.nullcontext()
+
+    def handle(self, t):
+        return t.numpy()
+
+    def span(self, buf, off, count, itemsize):
+        b = buf.view(np.uint8)
+        return self.torch.from_numpy(b[int(off) * itemsize:(int(off) + int(count)) * itemsize])
+
+    def put(self, t, src, nbytes, stream):
+        t.numpy().view(np.uint8)[:nbytes] = np.asarray(src).view(np.uint8)[:nbytes]
+
+    def get(self, dst, t, nbytes, stream):
+        np.asarray(dst).view(np.uint8)[:nbytes] = t.numpy().view(np.uint8)[:nbytes]
+
+
 class TorchComm:
     """One rank per GPU over torch.distributed (backend "nccl" = RCCL on ROCm).
 
     The small exchange buffers are torch device tensors; the library's kernels
     write into them and the collectives run on the library's stream
-    (torch.cuda.ExternalStream), so stream order replaces host syncs."""
+    (torch.cuda.ExternalStream), so stream order replaces host syncs.
+    memory="host" runs the same sequence over numpy buffers (gloo, CPU tests)."""
 
-    def __init__(self, tgt: target):
+    def __init__(self, tgt: target | None, memory: str = "device"):
         import torch
         import torch.distributed as dist
         self.torch = torch
@@ -184,28 +246,25 @@ class TorchComm:
         self.tgt = tgt
         self.rank = dist.get_rank()
         self.size = dist.get_world_size()
-        self.device = torch.device("cuda", tgt.device)
+        self.mem = _DeviceMemory(torch, tgt) if memory == "device" else _HostMemory(torch)
+        self.device = self.mem.device
         self._send = torch.zeros(8, dtype=torch.int64, device=self.device)
         self._recv = torch.zeros(8 * self.size, dtype=torch.int64, device=self.device)
         self._halo = torch.zeros(4 * HALO_MAX, dtype=torch.float64, device=self.device)
-
-    def _stream(self, stream):
-        return self.torch.cuda.ExternalStream(stream.value if hasattr(stream, "value") else int(stream),
-                                              device=self.device)
 
     def slots(self, nbytes: int):
         words = max(1, -(-int(nbytes) // 8))
         if self._send.numel() < words:
             self._send = self.torch.zeros(words, dtype=self.torch.int64, device=self.device)
             self._recv = self.torch.zeros(words * self.size, dtype=self.torch.int64, device=self.device)
-        return self._send.data_ptr(), self._recv.data_ptr()
+        return self.mem.handle(self._send), self.mem.handle(self._recv)
 
     def allgather(self, nbytes: int, stream):
         """Packed all-gather: recv bytes [r*nbytes, (r+1)*nbytes) <- rank r's
         send[0:nbytes] (nbytes a multiple of 8, sized by slots()), so the
         segment values sit contiguously for hpxhip_fold."""
         words = max(1, nbytes // 8)
-        with self.torch.cuda.stream(self._stream(stream)):
+        with self.mem.ctx(stream):
             self.dist.all_gather_into_tensor(self._recv[:self.size * words], self._send[:words])
         return None
 
@@ -220,44 +279,33 @@ class TorchComm:
         self.dist.all_gather_into_tensor(out, w)
         return out.cpu().numpy().reshape(self.size, -1)
 
-    def _bytes_view(self, addr, nbytes):
-        """A uint8 torch view of device memory the library allocated
-        (__cuda_array_interface__, no copy)."""
-        class _cai:
-            __cuda_array_interface__ = {"shape": (int(nbytes),), "typestr": "|u1", "data": (int(addr), False),
-                                        "version": 2, "strides": None}
-        return self.torch.as_tensor(_cai(), device=self.device)
-
     def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream, recv_off=0):
-        """RCCL all-to-all with uneven splits: send_counts[j] elements from
+        """All-to-all with uneven splits: send_counts[j] elements from
         send_buf[send_off:] go to rank j (in rank order); recv_counts[i]
-        elements from rank i land in recv_buf[recv_off:] in rank order."""
+        elements from rank i land in recv_buf[recv_off:] in rank order
+        (views of both buffers, no staging copy)."""
         sb = [int(c) * itemsize for c in send_counts]
         rb = [int(c) * itemsize for c in recv_counts]
-        src = self._bytes_view(send_buf.data() + send_off * itemsize, max(1, sum(sb)))[:sum(sb)]
-        dst = self._bytes_view(recv_buf.data() + recv_off * itemsize, max(1, sum(rb)))[:sum(rb)]
-        with self.torch.cuda.stream(self._stream(stream)):
+        src = self.mem.span(send_buf, send_off, sum(sb) // itemsize, itemsize)
+        dst = self.mem.span(recv_buf, recv_off, sum(rb) // itemsize, itemsize)
+        with self.mem.ctx(stream):
             self.dist.all_to_all_single(dst, src, rb, sb)
 
     def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream, count=1):
         """Ring halo of `count` points: my first points go to the left
         neighbour (its right halo), my last points to the right neighbour
         (its left halo)."""
-        torch, dist = self.torch, self.dist
+        dist = self.dist
         c, M, nb = int(count), HALO_MAX, 8 * int(count)
-        with torch.cuda.stream(self._stream(stream)):
+        with self.mem.ctx(stream):
             h = self._halo
-            base = h.data_ptr()
-            L.call("hpxhip_memcpy_async", ctypes.c_void_p(base), ctypes.c_void_p(send_left), nb, L.D2D, stream)
-            L.call("hpxhip_memcpy_async", ctypes.c_void_p(base + 8 * M), ctypes.c_void_p(send_right), nb, L.D2D,
-                   stream)
+            self.mem.put(h[0:c], send_left, nb, stream)
+            self.mem.put(h[M:M + c], send_right, nb, stream)
             for w in dist.batch_isend_irecv(ring_halo_ops(dist, self.rank, self.size, h[0:c], h[M:M + c],
                                                            h[2 * M:2 * M + c], h[3 * M:3 * M + c])):
                 w.wait()
-            L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_left), ctypes.c_void_p(base + 16 * M), nb, L.D2D,
-                   stream)
-            L.call("hpxhip_memcpy_async", ctypes.c_void_p(recv_right), ctypes.c_void_p(base + 24 * M), nb, L.D2D,
-                   stream)
+            self.mem.get(recv_left, h[2 * M:2 * M + c], nb, stream)
+            self.mem.get(recv_right, h[3 * M:3 * M + c], nb, stream)
 
 
 # ------------------------------------------------------------------ engine

@@ -111,10 +111,12 @@ def main():
           "scalar": 3.0},
          input=A, input2=B, expected=C)
 
-    # --- for_each_compute.cu:28-70: i += 5 over N = 100 ints
+    # --- for_each_compute.cu:28-70: i += 5 over N = 100 ints; the input is
+    # std::iota(h_A.begin(), h_A.end(), dis(gen)) with dis = uniform int in
+    # [2, 101] (for_each_compute.cu:62-67): 100 consecutive ints from that start
     rng = np.random.default_rng(0xF0E)
-    A = np.arange(int(rng.integers(2, 102)), 0, -1, dtype=np.int32)[:100]
-    A = np.resize(A, 100).astype(np.int32)
+    start = int(rng.integers(2, 102))
+    A = np.arange(start, start + 100, dtype=np.int32)
     save("for_each_compute",
          {"ref": "tests/unit/computeapi/cuda/for_each_compute.cu:28-51",
           "algo": "for_each", "dtype": "int32", "kind": "add_scalar", "scalar": 5},

@@ -4,7 +4,9 @@ all-gathered totals, scan carries, copy_if offsets and the stencil halo ring.
 
 The per-partition kernels are replaced by a numpy test engine *in this test
 only* (the product engine is HipEngine, exercised by tests/test_gpu_*.py);
-the code under test is hpx_amd.segmented's orchestration."""
+the code under test is hpx_amd.segmented's orchestration and the product's
+TorchComm collective sequence (all_gather_into_tensor, uneven
+all_to_all_single into views) run over host buffers on gloo."""
 import os
 import socket
 
@@ -21,35 +23,6 @@ from hpx_amd import functional as F  # noqa: E402
 from hpx_amd import segmented as S  # noqa: E402
 
 OPS = {0: np.add, 1: np.multiply, 2: np.minimum, 3: np.maximum, 4: np.bitwise_and, 5: np.bitwise_or, 6: np.bitwise_xor}
-
-
-class GlooComm:
-    def __init__(self):
-        self.rank, self.size = dist.get_rank(), dist.get_world_size()
-
-    def slots(self, nbytes):
-        w = max(1, nbytes // 8)
-        self._send = np.zeros(w, np.int64)
-        self._recv = np.zeros(self.size * w, np.int64)
-        return self._send, self._recv
-
-    def allgather(self, nbytes, stream):
-        w = max(1, nbytes // 8)
-        out = [torch.zeros(w, dtype=torch.int64) for _ in range(self.size)]
-        dist.all_gather(out, torch.from_numpy(self._send[:w].copy()))
-        self._recv[:self.size * w] = np.concatenate([t.numpy() for t in out])
-
-    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream, recv_off=0):
-        n = int(sum(send_counts))
-        src = torch.from_numpy(send_buf[send_off:send_off + n].view(np.uint8).copy())
-        dst = torch.zeros(int(sum(recv_counts)) * itemsize, dtype=torch.uint8)
-        dist.all_to_all_single(dst, src, [int(c) * itemsize for c in recv_counts],
-                               [int(c) * itemsize for c in send_counts])
-        m = int(sum(recv_counts))
-        recv_buf[recv_off:recv_off + m] = dst.numpy().view(recv_buf.dtype)
-
-    def barrier(self):
-        dist.barrier()
 
 
 class NumpyEngine:
@@ -141,7 +114,7 @@ def _layout_worker(rank, size, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=size)
     try:
-        comm = GlooComm()
+        comm = S.TorchComm(None, memory="host")  # the product comm over host buffers
         alg = S.segmented(NumpyEngine())
         CL = S.container_layout
         res = {}
@@ -187,7 +160,7 @@ def _worker(rank, size, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=size)
     try:
-        comm = GlooComm()
+        comm = S.TorchComm(None, memory="host")  # the product comm over host buffers
         alg = S.segmented(NumpyEngine())
         res = {}
         n = 10007

@@ -41,28 +41,6 @@ def _ordered(x, desc):
     return ~o if desc else o
 
 
-class GlooComm:
-    def __init__(self):
-        self.rank, self.size = dist.get_rank(), dist.get_world_size()
-
-    def allgather_host(self, words):
-        w = torch.from_numpy(np.ascontiguousarray(words, np.int64))
-        out = [torch.zeros_like(w) for _ in range(self.size)]
-        dist.all_gather(out, w)
-        return np.stack([o.numpy() for o in out])
-
-    def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream, recv_off=0):
-        n = int(sum(send_counts))
-        src = torch.from_numpy(send_buf[send_off:send_off + n].view(np.uint8).copy())
-        dst = torch.zeros(int(sum(recv_counts)) * itemsize, dtype=torch.uint8)
-        dist.all_to_all_single(dst, src, [int(c) * itemsize for c in recv_counts],
-                               [int(c) * itemsize for c in send_counts])
-        recv_buf[recv_off:recv_off + int(sum(recv_counts))] = dst.numpy().view(recv_buf.dtype)
-
-    def barrier(self):
-        dist.barrier()
-
-
 class SortEngine:
     stream = None
 
@@ -121,7 +99,7 @@ def _worker(rank, size, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=size)
     try:
-        comm = GlooComm()
+        comm = S.TorchComm(None, memory="host")  # the product comm over host buffers
         alg = S.segmented(SortEngine())
         res = {}
         for name, x in cases().items():

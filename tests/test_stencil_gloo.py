@@ -20,26 +20,14 @@ import torch.multiprocessing as mp  # noqa: E402
 from hpx_amd import segmented as S  # noqa: E402
 
 
-class RingComm:
-    def __init__(self):
-        self.rank, self.size = dist.get_rank(), dist.get_world_size()
+class OneRankComm:
+    """A ring of one (the product's LocalComm does this on the device)."""
+    rank, size = 0, 1
 
     def halo_exchange(self, send_left, send_right, recv_left, recv_right, stream, count=1):
-        """The product's P2P message order (segmented.ring_halo_ops, used by
-        TorchComm over RCCL) on gloo point-to-point, `count` points a side."""
         c = int(count)
-        (a0, i0), (a1, i1) = send_left, send_right
-        first = torch.tensor(a0[i0:i0 + c], dtype=torch.float64)
-        last = torch.tensor(a1[i1:i1 + c], dtype=torch.float64)
-        lh, rh = torch.zeros(c, dtype=torch.float64), torch.zeros(c, dtype=torch.float64)
-        if self.size == 1:
-            lh, rh = last.clone(), first.clone()
-        else:
-            for w in dist.batch_isend_irecv(S.ring_halo_ops(dist, self.rank, self.size, first, last, lh, rh)):
-                w.wait()
-        (b0, j0), (b1, j1) = recv_left, recv_right
-        b0[j0:j0 + c] = lh.numpy()    # left neighbour's last points
-        b1[j1:j1 + c] = rh.numpy()    # right neighbour's first points
+        recv_left[:c] = send_right[:c]
+        recv_right[:c] = send_left[:c]
 
 
 class HeatEngine:
@@ -53,13 +41,12 @@ class HeatEngine:
         return np.zeros(4 * S.HALO_MAX)
 
     def loc(self, buf, idx):
-        return (buf, int(idx))
+        return buf[int(idx):]  # a view: the comm reads / writes through it
 
     def heat_steps(self, cur, nxt, n, lo, hi, left, right, steps, k, dt, dx, stream):
         """`steps` oracle single steps on [left halo | cur | right halo]; its
         inner points [steps + lo, steps + hi) are exact."""
-        (lb, li), (rb, ri) = left, right
-        ext = np.concatenate([lb[li:li + steps], cur[:n], rb[ri:ri + steps]])
+        ext = np.concatenate([left[:steps], cur[:n], right[:steps]])
         for _ in range(steps):
             ext = O.stencil_heat_step(ext, 0.0, 0.0, k, dt, dx)
         nxt[lo:hi] = ext[steps + lo:steps + hi]
@@ -93,7 +80,8 @@ def _worker(rank, size, port, q, ckdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=size)
     try:
-        comm = RingComm()
+        # ranks >= 2: the product's TorchComm (ring_halo_ops over batch_isend_irecv)
+        comm = S.TorchComm(None, memory="host") if size > 1 else OneRankComm()
         res = {}
         for nx, nt, kind, fuse in CASES:
             init = None if kind == "ramp" else np.random.default_rng(nx).standard_normal(nx)
