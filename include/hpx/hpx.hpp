@@ -4,3 +4,4 @@
 #include <hpx/include/partitioned_vector.hpp>
 #include <hpx/parallel/algorithms.hpp>
 #include <hpx/parallel/execution.hpp>
+#include <hpx/parallel/heat_solver.hpp>

@@ -69,6 +69,7 @@ void f(hpx::compute::vector<int>& a) {
     ("for_loop_merge", []),
     ("device_closures", ["4242"]),
     ("partitioned_vector", []),
+    ("stencil_partitioned", []),
 ])
 def test_cxx_program(prog, args):
     exe = os.path.join(BIN, prog)
