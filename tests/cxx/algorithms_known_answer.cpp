@@ -257,6 +257,40 @@ void test_sort(hip::default_executor const& exec) {
     HPX_TEST(ok);
 }
 
+// container_algorithms/sort.hpp:102 (sort_range_tests.hpp test_sort1/2:
+// HPX_SORT_TEST_SIZE random values, default and std::greater, sync and task
+// policies) and is_sorted.hpp:40-120.  5,000,000 u64 keys take the hybrid
+// radix path (>= 2^22 keys).
+void test_sort_range_is_sorted(hip::default_executor const& exec) {
+    std::size_t const n = 5000000;
+    std::vector<uint64_t> h(n);
+    for (auto& x : h) x = gen();
+    hip::allocator<uint64_t> alloc(exec.target());
+    dvec<uint64_t> d(n, alloc);
+    from_host(h, d);
+    HPX_TEST(!hpx::parallel::is_sorted(ex::par.on(exec), d.begin(), d.end()));
+    auto r = hpx::parallel::sort(ex::par.on(exec), d);
+    HPX_TEST(r == d.end());
+    auto ref = h;
+    std::sort(ref.begin(), ref.end());
+    HPX_TEST(to_host(d) == ref);
+    HPX_TEST(hpx::parallel::is_sorted(ex::par.on(exec), d.begin(), d.end()));
+    HPX_TEST(!hpx::parallel::is_sorted(ex::par.on(exec), d.begin(), d.end(), std::greater<uint64_t>()));
+    hpx::parallel::sort(ex::par(ex::task).on(exec), d, std::greater<uint64_t>()).get();
+    std::sort(ref.begin(), ref.end(), std::greater<uint64_t>());
+    HPX_TEST(to_host(d) == ref);
+    HPX_TEST(hpx::parallel::is_sorted(ex::par(ex::task).on(exec), d.begin(), d.end(), std::greater<uint64_t>()).get());
+    // empty, one element, one pair out of order
+    HPX_TEST(hpx::parallel::is_sorted(ex::par.on(exec), d.begin(), d.begin()));
+    HPX_TEST(hpx::parallel::is_sorted(ex::par.on(exec), d.begin(), d.begin() + 1));
+    std::vector<int32_t> small = {1, 2, 3, 5, 4, 6};
+    hip::allocator<int32_t> ai(exec.target());
+    dvec<int32_t> ds(small.size(), ai);
+    from_host(small, ds);
+    HPX_TEST(hpx::parallel::is_sorted(ex::par.on(exec), ds.begin(), ds.begin() + 4));
+    HPX_TEST(!hpx::parallel::is_sorted(ex::par.on(exec), ds.begin(), ds.end()));
+}
+
 void test_elementwise(hip::default_executor const& exec) {
     hip::allocator<float> alloc(exec.target());
     dvec<float> a(1001, alloc), b(1001, alloc);
@@ -297,6 +331,7 @@ int hpx_main(int argc, char* argv[]) {
     test_copy_if(exec);
     test_reduce(exec);
     test_sort(exec);
+    test_sort_range_is_sorted(exec);
     test_elementwise(exec);
     return hpx::finalize();
 }
