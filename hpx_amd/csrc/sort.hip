@@ -37,6 +37,7 @@
 #include "sort_kernel.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <utility>
 #include <vector>
 
@@ -64,7 +65,7 @@ struct tile_shape {
 
 struct sort_layout {
     uint64_t ntiles;
-    size_t alt_keys, alt_vals, hist, bits, start, bounds, segs, counter, lb, lb_bytes, total;
+    size_t alt_keys, alt_vals, hist, xhist, bits, start, xstart, bounds, segs, counter, lb, lb_bytes, total;
     bool wide;  // 64-bit granules
 };
 
@@ -79,30 +80,52 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     off = align_up(off + n * vsize, 256);
     L.hist = off;
     off += 8 * kRadix * 8;
+    L.xhist = off;  // the 9-bit prefix field's histogram
+    off += kXBins * 8;
     L.bits = off;  // OR / AND of the ordered keys
     off += 256;
     L.start = off;
     off += 8 * kRadix * 8;
-    L.bounds = off;  // hybrid: bucket bounds and segment table (65537 u64 each)
-    off = align_up(off + 8 * (kBuckets + 1), 256);
-    L.segs = off;  // (begin, end) pairs
-    off = align_up(off + 16 * kBuckets, 256);
+    L.xstart = off;
+    off += kXBins * 8;
+    L.bounds = off;  // hybrid: bucket bounds (up to 2^17 + 1) and segment (begin, end) pairs
+    off = align_up(off + 8 * (kMaxBuckets + 1), 256);
+    L.segs = off;
+    off = align_up(off + 16 * kMaxBuckets, 256);
     L.counter = off;  // counter (16 B) immediately followed by lb: one memset
     off += 256;
     L.lb = off;
-    L.lb_bytes = L.ntiles * kRadix * (L.wide ? 8 : 4);
+    L.lb_bytes = L.ntiles * kXBins * (L.wide ? 8 : 4);  // room for a 9-bit pass
     off = align_up(off + L.lb_bytes, 256);
     L.total = off;
     return L;
 }
 
 // Hybrid tail (keys-only 64-bit sorts of at least 2^22 keys whose bucket
-// sizes, estimated from the two digits' histograms, fit one workgroup's LDS).
-constexpr int kBucketThreads = 1024;
-constexpr int kBucketItems = 18;
-constexpr uint64_t kBucketCap = static_cast<uint64_t>(kBucketThreads) * kBucketItems;
+// sizes, estimated from the prefix fields' histograms, fit the LDS):
+//   17-bit prefix (top byte + the 9 bits under it): segments of <= 9216 keys
+//     sorted by 512-thread workgroups, two per CU, so one workgroup's loads
+//     and stores overlap the other's LDS passes (7.2 vs 9.7 ms for the
+//     segment sort at 2^30, profiles/r02_ubench_segment_sort.log);
+//   16-bit prefix (the two top live bytes): segments of <= 18432 keys, one
+//     1024-thread workgroup per CU -- for buckets too large for the first
+//     form (more than ~2^30.1 random keys) or top bytes that are constant.
+// HPXHIP_SORT_HYBRID=0 / 16 turns the hybrid / its 17-bit form off (tests,
+// ablations).
+constexpr int kSegThreads16 = 1024, kSegThreads17 = 512, kSegItems = 18;
+constexpr uint64_t kCap16 = static_cast<uint64_t>(kSegThreads16) * kSegItems;
+constexpr uint64_t kCap17 = static_cast<uint64_t>(kSegThreads17) * kSegItems;
+constexpr int kField17Shift = 47;  // the 9-bit field [47, 56) under the top byte
 constexpr uint64_t kHybridMin = 1ull << 22;
 constexpr size_t kMaxBigBuckets = 64;  // more oversized buckets than this -> finish as plain LSD
+
+int hybrid_mode() {
+    const char* e = std::getenv("HPXHIP_SORT_HYBRID");
+    if (!e) return 17;
+    return std::atoi(e);
+}
+
+inline int top_bit(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
 
 template <typename T, bool DESC, typename VAL, bool HAS_VAL>
 int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, size_t scratch_bytes) {
@@ -115,64 +138,95 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     if (rc) return rc;
     char* base = static_cast<char*>(ws);
     auto* hist = reinterpret_cast<unsigned long long*>(base + L.hist);
+    auto* xhist = reinterpret_cast<unsigned long long*>(base + L.xhist);
     auto* start = reinterpret_cast<unsigned long long*>(base + L.start);
+    auto* xstart = reinterpret_cast<unsigned long long*>(base + L.xstart);
     uint32_t* counter = reinterpret_cast<uint32_t*>(base + L.counter);
     uint32_t* err = device_error_word(s);
     const int passes = static_cast<int>(sizeof(U));
     const unsigned hist_grid = static_cast<unsigned>(current_device_info().cus * kHistBlocksPerCU);
+    const int mode = (!HAS_VAL && sizeof(U) == 8 && n >= kHybridMin) ? hybrid_mode() : 0;
 
     auto* bits = reinterpret_cast<unsigned long long*>(base + L.bits);
     // histograms of digits [first, passes) of keys[0, cnt) -> hist, their
-    // exclusive bin starts -> start, OR / AND of the keys -> bits
-    auto histogram = [&](const U* k, uint64_t cnt, int first) -> int {
-        HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8, s));
+    // exclusive bin starts -> start, OR / AND of the keys -> bits; with
+    // xfield, also the 9-bit field under the top byte -> xhist / xstart
+    auto histogram = [&](const U* k, uint64_t cnt, int first, bool xfield) -> int {
+        HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8 + kXBins * 8, s));  // hist and xhist
         HPXHIP_CHECK(hipMemsetAsync(bits, 0, 8, s));
         HPXHIP_CHECK(hipMemsetAsync(bits + 1, 0xff, 8, s));
         hipLaunchKernelGGL((k_hist<U, X, kHistThreads>), dim3(hist_grid), dim3(kHistThreads), 0, s, k, cnt, first, passes,
-                           X{}, hist, bits);
+                           X{}, hist, bits, xfield ? kField17Shift : -1, xhist);
         HPXHIP_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_bin_offsets, dim3(passes), dim3(256), 0, s, hist, start);
+        hipLaunchKernelGGL(k_bin_offsets<kRadix>, dim3(passes), dim3(kRadix), 0, s, hist, start);
+        HPXHIP_CHECK_LAUNCH();
+        if (xfield) {
+            hipLaunchKernelGGL(k_bin_offsets<kXBins>, dim3(1), dim3(kXBins), 0, s, xhist, xstart);
+            HPXHIP_CHECK_LAUNCH();
+        }
+        return 0;
+    };
+    // one stable onesweep pass of the rb-bit digit at `shift` over cnt keys
+    auto pass = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, uint64_t cnt, int shift, int rb,
+                    const unsigned long long* bstart) -> int {
+        const uint64_t nt = (cnt + TS::tile - 1) / TS::tile;
+        HPXHIP_CHECK(hipMemsetAsync(counter, 0, 256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), s));
+        const dim3 grid(static_cast<unsigned>(nt)), block(TS::threads);
+        auto launch = [&](auto gtag, auto rbtag) {
+            using G = decltype(gtag);
+            constexpr int RB = decltype(rbtag)::value;
+            hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB>), grid, block, 0,
+                               s, kin, kout, vin, vout, cnt, shift, bstart, reinterpret_cast<G*>(base + L.lb), counter,
+                               err, X{});
+        };
+        using R8 = std::integral_constant<int, 8>;
+        using R9 = std::integral_constant<int, 9>;
+        if (rb == 9) {
+            if constexpr (!HAS_VAL && sizeof(U) == 8) {
+                if (L.wide) launch((unsigned long long)0, R9{});
+                else launch(uint32_t(0), R9{});
+            } else {
+                return HPXHIP_ERROR_INVALID_ARGUMENT;
+            }
+        } else {
+            if (L.wide) launch((unsigned long long)0, R8{});
+            else launch(uint32_t(0), R8{});
+        }
         HPXHIP_CHECK_LAUNCH();
         return 0;
     };
-    // one stable onesweep pass of digit p over cnt keys
-    auto pass = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, uint64_t cnt, int p) -> int {
-        const uint64_t nt = (cnt + TS::tile - 1) / TS::tile;
-        HPXHIP_CHECK(hipMemsetAsync(counter, 0, 256 + nt * kRadix * (L.wide ? 8 : 4), s));
-        const dim3 grid(static_cast<unsigned>(nt)), block(TS::threads);
-        if (L.wide)
-            hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, unsigned long long, X, TS::threads, TS::items, TS::lbb>), grid,
-                               block, 0, s, kin, kout, vin, vout, cnt, 8 * p, start + p * kRadix,
-                               reinterpret_cast<unsigned long long*>(base + L.lb), counter, err, X{});
-        else
-            hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, uint32_t, X, TS::threads, TS::items, TS::lbb>), grid, block, 0,
-                               s, kin, kout, vin, vout, cnt, 8 * p, start + p * kRadix,
-                               reinterpret_cast<uint32_t*>(base + L.lb), counter, err, X{});
-        HPXHIP_CHECK_LAUNCH();
-        return 0;
+    auto pass8 = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, uint64_t cnt, int p) -> int {
+        return pass(kin, kout, vin, vout, cnt, 8 * p, 8, start + p * kRadix);
     };
 
     // Pass skipping needs the live digits on the host (a digit is live iff
     // OR and AND of the keys differ on it).  A sort that may take the hybrid
-    // path counts only the two top digits first (the LDS atomics, not the
-    // read, bound k_hist) and counts the rest only when it needs them.
+    // path counts only the two top digits (and the 9-bit field under the top
+    // byte) first -- the LDS atomics, not the read, bound k_hist -- and counts
+    // the rest only when it needs them.
     std::vector<unsigned long long> h(static_cast<size_t>(passes) * kRadix);
+    std::vector<unsigned long long> hx(kXBins);
     std::vector<int> live;  // non-constant digits, most significant first
-    int counted = (!HAS_VAL && sizeof(U) == 8 && n >= kHybridMin) ? passes - 2 : 0;
+    uint64_t diff = 0;      // bits in which the keys differ (ordered form)
+    int counted = mode ? passes - 2 : 0;
     auto count_digits = [&](int first) -> int {
-        if ((rc = histogram(static_cast<const U*>(keys), n, first))) return rc;
+        const bool xf17 = mode == 17 && first > 0;
+        if ((rc = histogram(static_cast<const U*>(keys), n, first, xf17))) return rc;
         unsigned long long ob[2];
         HPXHIP_CHECK(hipMemcpyAsync(h.data(), hist, h.size() * 8, hipMemcpyDeviceToHost, s));
+        if (xf17) HPXHIP_CHECK(hipMemcpyAsync(hx.data(), xhist, hx.size() * 8, hipMemcpyDeviceToHost, s));
         HPXHIP_CHECK(hipMemcpyAsync(ob, bits, 16, hipMemcpyDeviceToHost, s));
         HPXHIP_CHECK(hipStreamSynchronize(s));
+        diff = ob[0] ^ ob[1];
         live.clear();
         for (int p = passes - 1; p >= 0; --p)
-            if (((ob[0] ^ ob[1]) >> (8 * p)) & 0xffu) live.push_back(p);
+            if ((diff >> (8 * p)) & 0xffu) live.push_back(p);
         counted = first;
         return 0;
     };
     if ((rc = count_digits(counted))) return rc;
-    if (counted > 0 && !(live.size() >= 3 && live[0] == passes - 1 && live[1] == passes - 2))
+    const bool top_two = live.size() >= 3 && live[0] == passes - 1 && live[1] == passes - 2;
+    if (counted > 0 && !top_two)
         if ((rc = count_digits(0))) return rc;
 
     U* kc = static_cast<U*>(keys);
@@ -181,10 +235,10 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     VAL* va = reinterpret_cast<VAL*>(base + L.alt_vals);
     // LSD over live[from..] (least significant first), whole array, result in keys
     auto lsd = [&](size_t from) -> int {
-        if (counted > 0 && (rc = histogram(kc, n, 0))) return rc;  // a permutation: same counts
+        if (counted > 0 && (rc = histogram(kc, n, 0, false))) return rc;  // a permutation: same counts
         int executed = 0;
         for (size_t i = live.size(); i-- > from;) {
-            if ((rc = pass(kc, ka, vc, va, n, live[i]))) return rc;
+            if ((rc = pass8(kc, ka, vc, va, n, live[i]))) return rc;
             std::swap(kc, ka);
             std::swap(vc, va);
             ++executed;
@@ -199,31 +253,43 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     if constexpr (HAS_VAL || sizeof(U) != 8) {
         return lsd(0);
     } else {
-    bool hybrid = n >= kHybridMin && live.size() >= 3;
-    if (hybrid) {
-        unsigned long long m1 = 0, m2 = 0;
-        for (int d = 0; d < kRadix; ++d) {
-            m1 = std::max(m1, h[live[0] * kRadix + d]);
-            m2 = std::max(m2, h[live[1] * kRadix + d]);
-        }
-        hybrid = static_cast<double>(m1) * static_cast<double>(m2) / static_cast<double>(n) <= 0.95 * kBucketCap;
-    }
-    if (!hybrid) return lsd(0);
+    if (!mode || live.size() < 3) return lsd(0);
+    auto max_of = [](const unsigned long long* c, int bins) {
+        unsigned long long m = 0;
+        for (int d = 0; d < bins; ++d) m = std::max(m, c[d]);
+        return static_cast<double>(m);
+    };
+    const double dn = static_cast<double>(n);
+    const double m_top = max_of(&h[live[0] * kRadix], kRadix);
+    int variant = 0;  // 17 or 16 (prefix bits), 0 = plain LSD
+    if (mode == 17 && counted > 0 && top_two && m_top * max_of(hx.data(), kXBins) / dn <= 0.95 * kCap17)
+        variant = 17;
+    else if (mode >= 16 && m_top * max_of(&h[live[1] * kRadix], kRadix) / dn <= 0.95 * kCap16)
+        variant = 16;
+    if (!variant) return lsd(0);
 
-    // ---- hybrid: prefix passes (p2, then p1: keys -> alt -> keys)
-    const int p1 = live[0], p2 = live[1];
-    if ((rc = pass(kc, ka, nullptr, nullptr, n, p2))) return rc;
-    if ((rc = pass(ka, kc, nullptr, nullptr, n, p1))) return rc;
+    // ---- prefix passes (low field, then the top live byte: keys -> alt -> keys)
+    const int p1 = live[0];
+    const int s2 = variant == 17 ? kField17Shift : 8 * live[1];
+    const int b2 = variant == 17 ? 9 : 8;
+    if (variant == 17) {
+        if ((rc = pass(kc, ka, nullptr, nullptr, n, s2, 9, xstart))) return rc;
+    } else {
+        if ((rc = pass8(kc, ka, nullptr, nullptr, n, live[1]))) return rc;
+    }
+    if ((rc = pass8(ka, kc, nullptr, nullptr, n, p1))) return rc;
+    const uint32_t nb = 256u << b2;
     auto* bounds = reinterpret_cast<uint64_t*>(base + L.bounds);
-    hipLaunchKernelGGL((k_bucket_bounds<U, X>), dim3((kBuckets + 1 + 255) / 256), dim3(256), 0, s, kc, n, 8 * p1,
-                       8 * p2, X{}, bounds);
+    hipLaunchKernelGGL((k_bucket_bounds<U, X>), dim3((nb + 1 + 255) / 256), dim3(256), 0, s, kc, n, 8 * p1, s2, b2, nb,
+                       X{}, bounds);
     HPXHIP_CHECK_LAUNCH();
-    std::vector<uint64_t> off(kBuckets + 1);
+    std::vector<uint64_t> off(nb + 1);
     HPXHIP_CHECK(hipMemcpyAsync(off.data(), bounds, off.size() * 8, hipMemcpyDeviceToHost, s));
     HPXHIP_CHECK(hipStreamSynchronize(s));
 
-    // segments: runs of whole buckets of at most kBucketCap keys; larger
-    // buckets are finished separately
+    // segments: runs of whole buckets of at most `cap` keys; larger buckets
+    // are finished separately
+    const uint64_t cap = variant == 17 ? kCap17 : kCap16;
     std::vector<uint64_t> segs;
     std::vector<std::pair<uint64_t, uint64_t>> big;
     uint64_t sb = 0, se = 0;
@@ -233,42 +299,49 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             segs.push_back(se);
         }
     };
-    for (int v = 0; v < kBuckets; ++v) {
+    for (uint32_t v = 0; v < nb; ++v) {
         const uint64_t bs = off[v], be = off[v + 1];
         if (be == bs) continue;
-        if (be - bs > kBucketCap) {
+        if (be - bs > cap) {
             close();
             big.emplace_back(bs, be - bs);
             sb = se = be;
             continue;
         }
-        if (be - sb > kBucketCap) {
+        if (be - sb > cap) {
             close();
             sb = bs;
         }
         se = be;
     }
     close();
-    if (big.size() > kMaxBigBuckets) {
-        // finish as plain LSD: low digits, then the prefix digits again
-        return lsd(0);
-    }
+    if (big.size() > kMaxBigBuckets) return lsd(0);  // plain LSD from here (the prefix passes are wasted)
 
-    if (!segs.empty()) {
+    // the highest bit in which keys of one bucket can differ
+    const int top_single = top_bit(diff & ((uint64_t(1) << s2) - 1));
+    if (!segs.empty() && top_single > 0) {
         auto* segd = reinterpret_cast<uint64_t*>(base + L.segs);
         HPXHIP_CHECK(hipMemcpyAsync(segd, segs.data(), segs.size() * 8, hipMemcpyHostToDevice, s));
         HPXHIP_CHECK(hipStreamSynchronize(s));  // `segs` is pageable and local
-        hipLaunchKernelGGL((k_bucket_sort<U, X, kBucketThreads, kBucketItems>), dim3(static_cast<unsigned>(segs.size() / 2)),
-                           dim3(kBucketThreads), 0, s, kc, segd, 8 * live[2] + 8, X{});
+        const dim3 grid(static_cast<unsigned>(segs.size() / 2));
+        if (variant == 17)
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems>), grid, dim3(kSegThreads17), 0, s, kc,
+                               segd, top_single, X{});
+        else
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItems>), grid, dim3(kSegThreads16), 0, s, kc,
+                               segd, top_single, X{});
         HPXHIP_CHECK_LAUNCH();
     }
-    // oversized buckets: LSD over the low digits of each, with its own histogram
+    // oversized buckets: LSD over the live bytes under the prefix, with the
+    // bucket's own histogram (the byte that holds bit 47 under a 17-bit
+    // prefix is included: its prefix bit is constant inside the bucket)
     for (const auto& [bs, len] : big) {
-        if ((rc = histogram(kc + bs, len, 0))) return rc;
+        if ((rc = histogram(kc + bs, len, 0, false))) return rc;
         U* a = kc + bs;
         U* b = ka + bs;
-        for (size_t i = live.size(); i-- > 2;) {
-            if ((rc = pass(a, b, nullptr, nullptr, len, live[i]))) return rc;
+        for (size_t i = live.size(); i-- > 0;) {
+            if (8 * live[i] >= s2) continue;
+            if ((rc = pass8(a, b, nullptr, nullptr, len, live[i]))) return rc;
             std::swap(a, b);
         }
         if (a != kc + bs) HPXHIP_CHECK(hipMemcpyAsync(kc + bs, a, len * sizeof(U), hipMemcpyDeviceToDevice, s));

@@ -24,10 +24,11 @@ __device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 
 // into both halves of the peer mask with one v_bitop3 each (acc & ~(m ^ x),
 // truth table 0x90): 4 VALU per bit where the select/xor/and form took 9
 // (scripts/ubench/bucket.hip; the ranking is the VALU-bound part of a pass).
+template <int BITS = 8>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
     uint32_t lo = static_cast<uint32_t>(active), hi = static_cast<uint32_t>(active >> 32);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < BITS; ++b) {
         const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(d), b, 1));
         uint64_t m;
         asm("v_cmp_ne_u32_e64 %0, 0, %1" : "=s"(m) : "v"(x));
@@ -52,14 +53,20 @@ __device__ __forceinline__ uint32_t peers_below(uint64_t peers) {
 // with nontemporal 16-B loads.
 // Digits [first, passes) are counted; bits[0] / bits[1] receive the OR / AND
 // of all ordered keys (a digit is constant iff OR and AND agree on it), so a
-// caller may count only the digits it needs first.
+// caller may count only the digits it needs first.  xshift >= 0 also counts
+// the 9-bit field at bits [xshift, xshift + 9) into xhist (512 bins; the
+// hybrid sort's 9-bit prefix pass).
+constexpr int kXBins = 512;
 template <typename U, typename X, int THREADS = 256, int COPIES = 4>
 __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, uint64_t n, int first, int passes, X xf,
                                                    unsigned long long* __restrict__ hist,
-                                                   unsigned long long* __restrict__ bits) {
+                                                   unsigned long long* __restrict__ bits, int xshift,
+                                                   unsigned long long* __restrict__ xhist) {
     constexpr int P = static_cast<int>(sizeof(U));
     __shared__ uint32_t h[P * kRadix * COPIES];
+    __shared__ uint32_t hx[kXBins * COPIES];
     for (int i = threadIdx.x; i < P * kRadix * COPIES; i += THREADS) h[i] = 0;
+    for (int i = threadIdx.x; i < kXBins * COPIES; i += THREADS) hx[i] = 0;
     __syncthreads();
     constexpr int V = 16 / sizeof(U);
     using VT = vec<U, V>;
@@ -75,6 +82,7 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
 #pragma unroll
         for (int p = 0; p < P; ++p)
             if (p >= first && p < passes) atomicAdd(&h[(p * kRadix + ((b >> (8 * p)) & 0xff)) * COPIES + copy], 1u);
+        if (xshift >= 0) atomicAdd(&hx[static_cast<uint32_t>((b >> xshift) & (kXBins - 1)) * COPIES + copy], 1u);
     };
     for (uint64_t i = tid; i < nvec; i += stride * 4) {
         VT x[4];
@@ -102,22 +110,30 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
         for (int k = 0; k < COPIES; ++k) c += h[i * COPIES + k];
         if (c) atomicAdd(&hist[i], static_cast<unsigned long long>(c));
     }
+    if (xshift >= 0)
+        for (int i = threadIdx.x; i < kXBins; i += THREADS) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int k = 0; k < COPIES; ++k) c += hx[i * COPIES + k];
+            if (c) atomicAdd(&xhist[i], static_cast<unsigned long long>(c));
+        }
 }
 
-// Exclusive scan of each pass's 256 counts (one 256-thread block per pass).
-__global__ __launch_bounds__(256) void k_bin_offsets(const unsigned long long* __restrict__ hist,
-                                                      unsigned long long* __restrict__ start) {
-    __shared__ uint64_t s_w[4];
+// Exclusive scan of each pass's R counts (one R-thread block per pass).
+template <int R = kRadix>
+__global__ __launch_bounds__(R) void k_bin_offsets(const unsigned long long* __restrict__ hist,
+                                                    unsigned long long* __restrict__ start) {
+    __shared__ uint64_t s_w[R / kWave];
     const int p = blockIdx.x;
     const int d = threadIdx.x;
-    const uint64_t c = hist[p * kRadix + d];
+    const uint64_t c = hist[p * R + d];
     const uint64_t incl = wave_inclusive_scan(c, op_plus{});
     const int wave = d / kWave;
     if (lane_id() == kWave - 1) s_w[wave] = incl;
     __syncthreads();
     uint64_t pre = 0;
     for (int w = 0; w < wave; ++w) pre += s_w[w];
-    start[p * kRadix + d] = pre + incl - c;
+    start[p * R + d] = pre + incl - c;
 }
 
 // ----------------------------------------------------------------- onesweep
@@ -130,22 +146,27 @@ __global__ __launch_bounds__(256) void k_bin_offsets(const unsigned long long* _
 // 512 x 16 keys with LBB = 4 was the fastest pass (4.88 ms at 2^30 u64);
 // staging the tile in two LDS phases, a cooperative look-back over all
 // threads (64-128 tiles per round trip) and 32 keys per thread were slower.
+// RB = 9 (hybrid sort's 9-bit prefix pass): 512 digits, one per thread, with
+// 16-bit per-wave counters so two workgroups still fit a CU's LDS.
 template <typename U, typename VAL, bool HAS_VAL, typename G, typename X, int THREADS = 512, int ITEMS = 16,
-          int LBB = 8>
+          int LBB = 8, int RB = 8>
 __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin, U* __restrict__ kout,
                                                        const VAL* __restrict__ vin, VAL* __restrict__ vout,
                                                        uint64_t n, int shift,
                                                        const unsigned long long* __restrict__ bin_start,
                                                        G* __restrict__ lb, uint32_t* __restrict__ counter,
                                                        uint32_t* __restrict__ err, X xf) {
-    static_assert(THREADS >= kRadix && THREADS % kRadix == 0, "one thread per digit for the look-back");
+    constexpr int R = 1 << RB;
+    constexpr uint32_t DMASK = R - 1;
+    using CT = std::conditional_t<(RB > 8), uint16_t, uint32_t>;
+    static_assert(THREADS >= R && THREADS % R == 0, "one thread per digit for the look-back");
     constexpr int WAVES = THREADS / kWave;
     constexpr int TILE = THREADS * ITEMS;
     __shared__ uint32_t s_tile;
-    __shared__ uint32_t s_whist[WAVES][kRadix];
-    __shared__ uint32_t s_local[kRadix];
-    __shared__ uint32_t s_wsum[kRadix / kWave];
-    __shared__ uint64_t s_adj[kRadix];
+    __shared__ CT s_whist[WAVES][R];
+    __shared__ uint32_t s_local[R];
+    __shared__ uint32_t s_wsum[R / kWave];
+    __shared__ uint64_t s_adj[R];
     __shared__ U s_keys[TILE];
     __shared__ VAL s_vals[HAS_VAL ? TILE : 1];
 
@@ -153,7 +174,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     const int wave = t / kWave;
     const int lane = lane_id();
     if (t == 0) s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int i = t; i < WAVES * kRadix; i += THREADS) (&s_whist[0][0])[i] = 0;
+    for (int i = t; i < WAVES * R; i += THREADS) (&s_whist[0][0])[i] = 0;
     __syncthreads();
     const uint64_t tile = s_tile;
     const uint64_t tile_base = tile * TILE;
@@ -180,25 +201,25 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = wbase + r * kWave + lane;
         const bool valid = full || i < n;
-        const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
-        const uint64_t peers = match_digit(d, __ballot(valid));
+        const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
+        const uint64_t peers = match_digit<RB>(d, __ballot(valid));
         const uint32_t below = peers_below(peers);
         const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(peers));
         const uint32_t old = s_whist[wave][d];
         rank[r] = old + below;
-        if (valid && below == 0) s_whist[wave][d] = old + cnt;
+        if (valid && below == 0) s_whist[wave][d] = static_cast<CT>(old + cnt);
     }
     __syncthreads();
 
-    // ---- per-digit tile count and per-wave offsets (thread t < 256 owns digit t)
+    // ---- per-digit tile count and per-wave offsets (thread t < R owns digit t)
     uint32_t tile_count = 0;
     uint32_t count_incl = 0;
-    G* my = lb + tile * kRadix;
-    if (t < kRadix) {
+    G* my = lb + tile * R;
+    if (t < R) {
 #pragma unroll
         for (int w = 0; w < WAVES; ++w) {
             const uint32_t c = s_whist[w][t];
-            s_whist[w][t] = tile_count;
+            s_whist[w][t] = static_cast<CT>(tile_count);
             tile_count += c;
         }
         // publish this tile's aggregate for digit t as early as possible
@@ -208,10 +229,10 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
         if (lane == kWave - 1) s_wsum[wave] = count_incl;
     }
     __syncthreads();
-    if (t < kRadix) {
+    if (t < R) {
         uint32_t pre = 0;
 #pragma unroll
-        for (int w = 0; w < kRadix / kWave; ++w)
+        for (int w = 0; w < R / kWave; ++w)
             if (w < wave) pre += s_wsum[w];
         s_local[t] = pre + count_incl - tile_count;
     }
@@ -222,15 +243,15 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = wbase + r * kWave + lane;
         if (full || i < n) {
-            const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
+            const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
             const uint32_t pos = s_local[d] + s_whist[wave][d] + rank[r];
             s_keys[pos] = k[r];
             if constexpr (HAS_VAL) s_vals[pos] = v[r];
         }
     }
 
-    // ---- per-digit look-back across tiles (thread t < 256 owns digit t)
-    if (t < kRadix) {
+    // ---- per-digit look-back across tiles (thread t < R owns digit t)
+    if (t < R) {
         uint64_t excl = 0;
         if (tile == 0) {
             if (LBB > 0) __hip_atomic_store(&my[t], enc_incl<G>(tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -242,7 +263,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
                 G g[LBB];
 #pragma unroll
                 for (int j = 0; j < LBB; ++j)
-                    g[j] = (pred - j >= 0) ? __hip_atomic_load(&lb[static_cast<uint64_t>(pred - j) * kRadix + t],
+                    g[j] = (pred - j >= 0) ? __hip_atomic_load(&lb[static_cast<uint64_t>(pred - j) * R + t],
                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                            : enc_incl<G>(0);
                 int used = 0;
@@ -282,7 +303,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
         const uint32_t i = r * THREADS + t;
         if (i < nvalid) {
             const U key = s_keys[i];
-            const uint32_t d = static_cast<uint32_t>(xf(key) >> shift) & 0xffu;
+            const uint32_t d = static_cast<uint32_t>(xf(key) >> shift) & DMASK;
             const uint64_t dst = s_adj[d] + i;
             kout[dst] = key;
             if constexpr (HAS_VAL) vout[dst] = s_vals[i];
@@ -291,28 +312,29 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
 }
 
 // ------------------------------------------------------- hybrid (MSD) tail
-// After two onesweep passes on the two most significant non-constant digits
-// (p2, then p1) the keys are ordered by the 16-bit prefix (digit p1, digit
-// p2); every prefix value is a contiguous bucket.
-constexpr int kBuckets = 1 << 16;
+// After two onesweep passes on the most significant live bits (the low
+// prefix field of b2 = 8 or 9 bits at s2, then the top live byte at s1) the
+// keys are ordered by a (8 + b2)-bit prefix; every prefix value is a
+// contiguous bucket.
+constexpr int kMaxBuckets = 1 << 17;
 
 template <typename U, typename X>
-__device__ __forceinline__ uint32_t bucket_of(U k, int s1, int s2, X xf) {
+__device__ __forceinline__ uint32_t bucket_of(U k, int s1, int s2, int b2, X xf) {
     const U u = xf(k);
-    return (static_cast<uint32_t>(u >> s1) & 0xffu) << 8 | (static_cast<uint32_t>(u >> s2) & 0xffu);
+    return (static_cast<uint32_t>(u >> s1) & 0xffu) << b2 | (static_cast<uint32_t>(u >> s2) & ((1u << b2) - 1u));
 }
 
-// off[v] = first index whose prefix is >= v (v = 0..65536): a lower_bound per
+// off[v] = first index whose prefix is >= v (v = 0..nb): a lower_bound per
 // bucket over the prefix-ordered keys instead of a pass over all of them.
 template <typename U, typename X>
-__global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ keys, uint64_t n, int s1, int s2, X xf,
-                                                        uint64_t* __restrict__ off) {
+__global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ keys, uint64_t n, int s1, int s2, int b2,
+                                                        uint32_t nb, X xf, uint64_t* __restrict__ off) {
     const uint32_t v = blockIdx.x * 256 + threadIdx.x;
-    if (v > static_cast<uint32_t>(kBuckets)) return;
+    if (v > nb) return;
     uint64_t lo = 0, hi = n;
     while (lo < hi) {
         const uint64_t mid = lo + (hi - lo) / 2;
-        if (bucket_of(keys[mid], s1, s2, xf) < v) lo = mid + 1;
+        if (bucket_of(keys[mid], s1, s2, b2, xf) < v) lo = mid + 1;
         else hi = mid;
     }
     off[v] = lo;
@@ -336,8 +358,8 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 // Six 8-bit LDS passes for the 48 bits under a 16-bit prefix took 2.4 ms
 // each at 2^30 keys (VALU-bound ranking); this form replaces four of them.
 template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16>
-__global__ __launch_bounds__(THREADS) void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg,
-                                                          int top_single, X xf) {
+__global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
+    void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf) {
     constexpr int WAVES = THREADS / kWave;
     constexpr int CHUNK = ITEMS * kWave;
     constexpr int BITS = static_cast<int>(sizeof(U) * 8);

@@ -14,13 +14,13 @@ using namespace hpxhip::sort_detail;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
 // key i: top 16 bits = segment (i / 16384), low 48 bits random
-__global__ void k_fill(uint64_t* k, uint64_t n, uint64_t lowmask) {
+__global__ void k_fill(uint64_t* k, uint64_t n, uint64_t lowmask, int segbits = 14, int topbit = 48) {
     const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
     if (i >= n) return;
     uint64_t z = (i ^ 0x5EEDull) + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    k[i] = ((i >> 14) << 48) | ((z ^ (z >> 31)) & lowmask);
+    k[i] = ((i >> segbits) << topbit) | ((z ^ (z >> 31)) & lowmask);
 }
 __global__ void k_check(const uint64_t* k, uint64_t n, unsigned long long* bad) {
     const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
@@ -67,6 +67,23 @@ void run(uint64_t* k, uint64_t* seg, uint64_t n, uint64_t mask, const char* tag)
     printf("%-56s %7.3f ms (fill subtracted)  %7.1f GB/s (16 B/key)\n", name, both - fill, 16.0 * n / (both - fill) / 1e6);
 }
 
+// 2^30 keys in 131072 segments of 8192 (17-bit prefix, one bucket each)
+template <int T, int I>
+void run_small(uint64_t* k, uint64_t* seg, uint64_t n, const char* tag) {
+    const unsigned nseg = static_cast<unsigned>(n / 8192);
+    const uint64_t m47 = (1ull << 47) - 1;
+    char name[96];
+    snprintf(name, sizeof name, "%s T%d I%d", tag, T, I);
+    const float fill = bench("  (fill only)", [&] { hipLaunchKernelGGL(k_fill, dim3(n / 256), dim3(256), 0, 0, k, n, m47, 13, 47); },
+                             double(n));
+    const float both = bench(name, [&] {
+        hipLaunchKernelGGL(k_fill, dim3(n / 256), dim3(256), 0, 0, k, n, m47, 13, 47);
+        hipLaunchKernelGGL((k_bucket_sort<uint64_t, ordered_bits<uint64_t, false>, T, I>), dim3(nseg), dim3(T), 0, 0, k,
+                           seg, 47, ordered_bits<uint64_t, false>{});
+    }, double(n));
+    printf("%-56s %7.3f ms (fill subtracted)  %7.1f GB/s (16 B/key)\n", name, both - fill, 16.0 * n / (both - fill) / 1e6);
+}
+
 int main() {
     const uint64_t n = 1ull << 30;
     uint64_t *k, *seg;
@@ -84,6 +101,19 @@ int main() {
     run<1024, 18, -1>(k, seg, n, m48, "segment sort, random low 48 bits (2 passes only)");
     run<1024, 18>(k, seg, n, m48, "segment sort, random low 48 bits");
     run<1024, 18>(k, seg, n, m24, "segment sort, low 24 bits (fallback)");
+    {
+        std::vector<uint64_t> hs2(2 * (n / 8192));
+        for (uint64_t s2 = 0; s2 < n / 8192; ++s2) { hs2[2 * s2] = s2 * 8192; hs2[2 * s2 + 1] = (s2 + 1) * 8192; }
+        uint64_t* seg2;
+        CK(hipMalloc(&seg2, hs2.size() * 8));
+        CK(hipMemcpy(seg2, hs2.data(), hs2.size() * 8, hipMemcpyHostToDevice));
+        run_small<512, 18>(k, seg2, n, "segment sort 8192-key segments, 2/CU");
+        CK(hipMemset(bad, 0, 8));
+        hipLaunchKernelGGL(k_check, dim3(n / 256), dim3(256), 0, 0, k, n, bad);
+        unsigned long long hb = 0;
+        CK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+        printf("unsorted pairs after the 8192-key segment sorts: %llu\n", hb);
+    }
     CK(hipMemset(bad, 0, 8));
     for (uint64_t mask : {m48, m24}) {
         CK(hipMemset(bad, 0, 8));

@@ -35,10 +35,10 @@ int main() {
     printf("%-40s min %7.3f ms med %7.3f ms  %7.1f GB/s\n", name, t[0], t[3], bytes / t[0] / 1e6);
   };
   run("hist (8 passes)", 8.0 * N, [&] { CK(hipMemsetAsync(hist, 0, 8*256*8, 0));
-      k_hist<U, X, 256><<<512, 256>>>(kin, N, 0, 8, X{}, hist, start + 8 * 256); });
+      k_hist<U, X, 256><<<512, 256>>>(kin, N, 0, 8, X{}, hist, start + 8 * 256, -1, nullptr); });
   run("hist (8 passes) 1024 blocks", 8.0 * N, [&] { CK(hipMemsetAsync(hist, 0, 8*256*8, 0));
-      k_hist<U, X, 256><<<1024, 256>>>(kin, N, 0, 8, X{}, hist, start + 8 * 256); });
-  k_bin_offsets<<<8, 256>>>(hist, start);
+      k_hist<U, X, 256><<<1024, 256>>>(kin, N, 0, 8, X{}, hist, start + 8 * 256, -1, nullptr); });
+  k_bin_offsets<256><<<8, 256>>>(hist, start);
   CK(hipDeviceSynchronize());
   auto pass = [&](auto th_c, auto it_c, auto lb_c, const char* name) {
     constexpr int TH = decltype(th_c)::value, IT = decltype(it_c)::value, LBB = decltype(lb_c)::value;

@@ -65,10 +65,10 @@ int main() {
 #define HIST(C, G, FIRST)                                                                                     \
     bench("hist copies" #C " grid" #G " digits from " #FIRST, [&] {                                                          \
         CK(hipMemsetAsync(hist, 0, 8 * 256 * 8));                                                    \
-        hipLaunchKernelGGL((k_hist<uint64_t, X, 256, C>), dim3(G), dim3(256), 0, 0, kin, n, FIRST, 8, X{}, hist, bits); \
+        hipLaunchKernelGGL((k_hist<uint64_t, X, 256, C>), dim3(G), dim3(256), 0, 0, kin, n, FIRST, 8, X{}, hist, bits, -1, nullptr); \
     }, n / 2.0)  // 8 B/key: GB/s column = read bandwidth
     HIST(4, 1024, 0); HIST(4, 1024, 6); HIST(4, 1024, 7);
-    hipLaunchKernelGGL(k_bin_offsets, dim3(8), dim3(256), 0, 0, hist, start);
+    hipLaunchKernelGGL(k_bin_offsets<256>, dim3(8), dim3(256), 0, 0, hist, start);
     CK(hipDeviceSynchronize());
 
 #define PASS(T, I, B)                                                                                         \

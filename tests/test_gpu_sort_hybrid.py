@@ -1,9 +1,11 @@
 """The hybrid tail of the 64-bit keys-only sort (sort.hip: two onesweep passes
-on the two most significant non-constant digits, bucket bounds by lower_bound,
-one LDS-resident LSD sort per segment of whole buckets; oversized buckets
-finished by per-bucket LSD, many of them by plain LSD), checked element for
-element against numpy's sort on the distributions that steer it down each
-branch.  Sizes start at the hybrid's 2^22-key threshold.
+on the prefix -- the top byte and the 9 bits under it (17-bit form, 9216-key
+segments) or the two top live bytes (16-bit form, 18432-key segments) --,
+bucket bounds by lower_bound, one LDS-resident sort per segment of whole
+buckets; oversized buckets finished by per-bucket LSD, many of them by plain
+LSD), checked element for element against numpy's sort on the distributions
+that steer it down each branch, in both forms (HPXHIP_SORT_HYBRID=17 / 16).
+Sizes start at the hybrid's 2^22-key threshold.
 
 Parity: std::sort's order for integer keys (sort.hpp:78-229 via the oracle's
 O.sort, itself numpy's stable sort) and the IEEE total order for doubles."""
@@ -23,6 +25,12 @@ def pol(gpu_target):
     return ex.par.on(hpx.default_executor(gpu_target))
 
 
+@pytest.fixture(params=["17", "16"], autouse=True)
+def form(request, monkeypatch):
+    monkeypatch.setenv("HPXHIP_SORT_HYBRID", request.param)
+    return request.param
+
+
 def check(pol, tgt, h, desc=False):
     v = hpx.vector.from_host(h, tgt)
     P.sort(pol, v.begin(), v.end(), F.greater if desc else F.less)
@@ -31,7 +39,7 @@ def check(pol, tgt, h, desc=False):
     np.testing.assert_array_equal(got, O.sort(h, desc))
 
 
-@pytest.mark.parametrize("logn", [22, 24])
+@pytest.mark.parametrize("logn", [22, 24, 25])
 @pytest.mark.parametrize("desc", [False, True])
 def test_uniform_u64(pol, gpu_target, logn, desc):
     # 2^22: buckets of ~64 keys packed into multi-bucket segments (prefix passes
