@@ -208,7 +208,8 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     std::vector<unsigned long long> hx(kXBins);
     std::vector<int> live;  // non-constant digits, most significant first
     uint64_t diff = 0;      // bits in which the keys differ (ordered form)
-    int counted = mode ? passes - 2 : 0;
+    // 17-bit form: the top byte and the 9-bit field; 16-bit form: the two top bytes
+    int counted = mode ? passes - (mode == 17 ? 1 : 2) : 0;
     auto count_digits = [&](int first) -> int {
         const bool xf17 = mode == 17 && first > 0;
         if ((rc = histogram(static_cast<const U*>(keys), n, first, xf17))) return rc;
@@ -228,6 +229,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     const bool top_two = live.size() >= 3 && live[0] == passes - 1 && live[1] == passes - 2;
     if (counted > 0 && !top_two)
         if ((rc = count_digits(0))) return rc;
+    const int counted_first = counted;  // the digits [counted_first, passes) have histograms
 
     U* kc = static_cast<U*>(keys);
     U* ka = reinterpret_cast<U*>(base + L.alt_keys);
@@ -262,10 +264,12 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     const double dn = static_cast<double>(n);
     const double m_top = max_of(&h[live[0] * kRadix], kRadix);
     int variant = 0;  // 17 or 16 (prefix bits), 0 = plain LSD
-    if (mode == 17 && counted > 0 && top_two && m_top * max_of(hx.data(), kXBins) / dn <= 0.95 * kCap17)
+    if (mode == 17 && counted_first > 0 && top_two && m_top * max_of(hx.data(), kXBins) / dn <= 0.95 * kCap17) {
         variant = 17;
-    else if (mode >= 16 && m_top * max_of(&h[live[1] * kRadix], kRadix) / dn <= 0.95 * kCap16)
-        variant = 16;
+    } else if (mode >= 16) {
+        if (live[1] < counted_first && (rc = count_digits(0))) return rc;  // the second byte was not counted
+        if (m_top * max_of(&h[live[1] * kRadix], kRadix) / dn <= 0.95 * kCap16) variant = 16;
+    }
     if (!variant) return lsd(0);
 
     // ---- prefix passes (low field, then the top live byte: keys -> alt -> keys)
