@@ -99,3 +99,13 @@ def test_heavy_duplicates(pol, gpu_target):
     # 2^16 distinct values spread over all digits: buckets of duplicates
     vals = rng.integers(0, 2**64 - 1, 1 << 16, dtype=np.uint64, endpoint=True)
     check(pol, gpu_target, vals[rng.integers(0, 1 << 16, n)])
+
+
+@pytest.mark.parametrize("bits", [24, 56])
+def test_low_bit_ranges(pol, gpu_target, bits):
+    # keys below 2^24 (three live bytes, many duplicates: the prefix is bytes 2
+    # and 1) and below 2^56 (top byte constant: the prefix moves down a byte)
+    rng = np.random.default_rng(bits)
+    h = rng.integers(0, 1 << bits, (1 << 23) + 5, dtype=np.uint64)
+    check(pol, gpu_target, h)
+    check(pol, gpu_target, h, True)
