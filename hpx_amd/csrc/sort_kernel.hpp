@@ -148,8 +148,12 @@ __global__ __launch_bounds__(R) void k_bin_offsets(const unsigned long long* __r
 // threads (64-128 tiles per round trip) and 32 keys per thread were slower.
 // RB = 9 (hybrid sort's 9-bit prefix pass): 512 digits, one per thread, with
 // 16-bit per-wave counters so two workgroups still fit a CU's LDS.
+// STAGE = false (ablation, scripts/ubench/sortpass2.hip): no LDS staging --
+// every key is stored from registers straight to its final position.  It
+// frees 64 KiB of LDS but the scattered 8-B stores make the pass 3x slower
+// (14.3 vs 4.85 ms at 2^30 u64, profiles/r02_ubench_onesweep_direct.log).
 template <typename U, typename VAL, bool HAS_VAL, typename G, typename X, int THREADS = 512, int ITEMS = 16,
-          int LBB = 8, int RB = 8>
+          int LBB = 8, int RB = 8, bool STAGE = true>
 __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin, U* __restrict__ kout,
                                                        const VAL* __restrict__ vin, VAL* __restrict__ vout,
                                                        uint64_t n, int shift,
@@ -167,8 +171,8 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     __shared__ uint32_t s_local[R];
     __shared__ uint32_t s_wsum[R / kWave];
     __shared__ uint64_t s_adj[R];
-    __shared__ U s_keys[TILE];
-    __shared__ VAL s_vals[HAS_VAL ? TILE : 1];
+    __shared__ U s_keys[STAGE ? TILE : 1];
+    __shared__ VAL s_vals[(HAS_VAL && STAGE) ? TILE : 1];
 
     const int t = threadIdx.x;
     const int wave = t / kWave;
@@ -242,7 +246,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = wbase + r * kWave + lane;
-        if (full || i < n) {
+        if (STAGE && (full || i < n)) {
             const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
             const uint32_t pos = s_local[d] + s_whist[wave][d] + rank[r];
             s_keys[pos] = k[r];
@@ -292,9 +296,22 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             }
             __hip_atomic_store(&my[t], enc_incl<G>(excl + tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        s_adj[t] = static_cast<uint64_t>(bin_start[t]) + excl - s_local[t];
+        s_adj[t] = static_cast<uint64_t>(bin_start[t]) + excl - (STAGE ? s_local[t] : 0u);
     }
     __syncthreads();
+    if constexpr (!STAGE) {
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const uint64_t i = wbase + r * kWave + lane;
+            if (full || i < n) {
+                const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
+                const uint64_t dst = s_adj[d] + s_whist[wave][d] + rank[r];
+                kout[dst] = k[r];
+                if constexpr (HAS_VAL) vout[dst] = v[r];
+            }
+        }
+        return;
+    }
 
     // ---- coalesced write of the LDS-sorted tile
     const uint32_t nvalid = full ? TILE : static_cast<uint32_t>(n - tile_base);

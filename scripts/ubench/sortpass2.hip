@@ -81,14 +81,31 @@ int main() {
                            0, 0, kin, kout, (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, start,        \
                            (uint32_t*)lb, counter, err, X{});                                               \
     }, n)
+    // 9-bit digit [0, 9) offsets for the RB = 9 variants
+    unsigned long long *xhist, *xstart;
+    CK(hipMalloc(&xhist, 512 * 8));
+    CK(hipMalloc(&xstart, 512 * 8));
+    CK(hipMemset(xhist, 0, 512 * 8));
+    CK(hipMemset(hist, 0, 8 * 256 * 8));
+    hipLaunchKernelGGL((k_hist<uint64_t, X, 256, 4>), dim3(1024), dim3(256), 0, 0, kin, n, 0, 8, X{}, hist, bits, 0, xhist);
+    hipLaunchKernelGGL(k_bin_offsets<256>, dim3(8), dim3(256), 0, 0, hist, start);
+    hipLaunchKernelGGL(k_bin_offsets<512>, dim3(1), dim3(512), 0, 0, xhist, xstart);
+    void* lb9;
+    CK(hipMalloc(&lb9, (n / 8192 + 1) * 512 * 4));
+#define PASSX(RB, ST, BS)                                                                                      \
+    bench("onesweep T512 I16 LBB4 RB" #RB " stage " #ST, [&] {                                               \
+        const uint64_t ntiles = (n + 8191) / 8192;                                                           \
+        CK(hipMemsetAsync(counter, 0, 256));                                                                 \
+        CK(hipMemsetAsync(lb9, 0, ntiles * (1 << RB) * 4));                                                  \
+        hipLaunchKernelGGL((k_onesweep<uint64_t, uint32_t, false, uint32_t, X, 512, 16, 4, RB, ST>), dim3(ntiles), \
+                           dim3(512), 0, 0, kin, kout, (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, BS,    \
+                           (uint32_t*)lb9, counter, err, X{});                                              \
+    }, n)
     for (int rep = 0; rep < 2; ++rep) {
-        PASS(512, 16, 4);
-        PASS(256, 16, 4);
-        PASS(256, 24, 4);
-        PASS(256, 32, 4);
-        PASS(256, 8, 4);
-        PASS(512, 8, 4);
-        PASS(256, 16, 8);
+        PASSX(8, true, start);
+        PASSX(8, false, start);
+        PASSX(9, true, xstart);
+        PASSX(9, false, xstart);
     }
     uint32_t herr;
     CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
