@@ -262,6 +262,27 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
                           "gbs_lsd_equivalent_136B": round(136 * n / ms_sort / 1e6, 1)}
     res["sort_uint64"].update(sort_check(P, F, pol, tgt, keys, regen))
     keys.free()
+    # the LSD paths: 32-bit keys (4 passes, 40 B/key with the histogram) and
+    # sort_by_key with 64-bit values (8 passes over keys and values)
+    k32 = hpx.vector(n, dtype=np.uint32, tgt=tgt)
+    regen32 = lambda: P.generate(pol, k32.begin(), k32.end(), "bits", 11)  # noqa: E731
+    ms_gen = timed(L, tgt, regen32, reps=2)
+    ms32 = timed(L, tgt, lambda: (regen32(), P.sort(pol, k32.begin(), k32.end())), reps=2) - ms_gen
+    res["sort_uint32"] = {"keys": n, "ms": round(ms32, 3), "gkeys_per_s": round(n / ms32 / 1e6, 3),
+                          "gbs_executed_36B": round(36 * n / ms32 / 1e6, 1)}
+    k32.free()
+    nkv = n // 4
+    kk = hpx.vector(nkv, dtype=np.uint64, tgt=tgt)
+    vv = hpx.vector(nkv, dtype=np.uint64, tgt=tgt)
+    regenkv = lambda: (P.generate(pol, kk.begin(), kk.end(), "bits", 13),  # noqa: E731
+                       P.generate(pol, vv.begin(), vv.end(), "bits", 17))
+    ms_gen = timed(L, tgt, regenkv, reps=2)
+    mskv = timed(L, tgt, lambda: (regenkv(), P.sort_by_key(pol, kk.begin(), kk.end(), vv.begin())), reps=2) - ms_gen
+    ok = bool(P.is_sorted(pol, kk.begin(), kk.end()))
+    res["sort_by_key_u64_u64"] = {"pairs": nkv, "ms": round(mskv, 3), "gpairs_per_s": round(nkv / mskv / 1e6, 3),
+                                  "gbs_executed_264B": round(264 * nkv / mskv / 1e6, 1), "keys_sorted": ok}
+    kk.free()
+    vv.free()
     # 1d_stencil heat: 2^32 points, 100 steps (BASELINE.md plan), through the
     # partitioned solver -- the same row the N > 1 run reports
     res["stencil_heat_dist"] = stencil_row(S, comm, tgt, 1 << args.stencil_logn, args.stencil_steps)
