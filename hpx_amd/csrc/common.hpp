@@ -19,6 +19,13 @@
 #include <limits>
 #include <type_traits>
 
+// Ablation builds only (-DHPXHIP_TILE_DYN_ID=true): tile ids of the single-
+// pass kernels (scan, copy_if, onesweep sort passes) from an atomic counter
+// instead of blockIdx (lookback.hpp).
+#ifndef HPXHIP_TILE_DYN_ID
+#define HPXHIP_TILE_DYN_ID false
+#endif
+
 namespace hpxhip {
 
 constexpr int kWave = 64;

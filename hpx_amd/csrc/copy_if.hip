@@ -53,8 +53,11 @@ int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev,
     const uint64_t ntiles = ntiles_for<T, R>(n);
     HPXHIP_CHECK(hipMemsetAsync(ws, 0, align_up(kSlotsOff + ntiles * tile_state<SV>::bytes_per_tile(), 256), s));
     tile_state<SV> st{reinterpret_cast<uint64_t*>(ws + kSlotsOff), device_error_word(s)};
-    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, 4, 0, SV>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads), 0,
-                       s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles);
+    // Tile ids from the atomic counter: 2.33 ms vs 2.36 with blockIdx order
+    // for 2^30 int64 (profiles/r02_ubench_tile_order_ab.log).
+    constexpr bool kDynId = true;
+    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, 4, 0, SV, kDynId>), dim3(static_cast<unsigned>(ntiles)),
+                       dim3(kThreads), 0, s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles);
     HPXHIP_CHECK_LAUNCH();
     return 0;
 }

@@ -33,7 +33,8 @@ using hit_word = std::conditional_t<(BITS <= 32), uint32_t, uint64_t>;
 //   registers at their ranks (no LDS compaction), 4 = no write-out at all.
 // SV: tile-state value type (uint32_t halves the look-back granules; valid
 // while n < 2^32).
-template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4, int ABL = 0, typename SV = uint64_t>
+template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4, int ABL = 0, typename SV = uint64_t,
+          bool DYN_ID = HPXHIP_TILE_DYN_ID>
 __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out, uint64_t n, Pred pred,
                                                        uint64_t* count_dev, uint32_t* counter,
                                                        tile_state<SV> st, uint64_t ntiles) {
@@ -49,10 +50,12 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out,
     __shared__ uint64_t s_prefix;
     __shared__ T s_stage[kWaves][kWave * V];  // one wave round of hits, compacted
 
-    if (threadIdx.x == 0)
-        s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint64_t tile = s_tile;
+    if constexpr (DYN_ID) {  // ablation: tile ids from the atomic counter
+        if (threadIdx.x == 0)
+            s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+    }
+    const uint64_t tile = DYN_ID ? s_tile : blockIdx.x;  // tile order = dispatch order (lookback.hpp)
     const int wave = threadIdx.x / kWave;
     const int lane = lane_id();
     const uint64_t tile_base = tile * TILE;

@@ -7,9 +7,23 @@
 // loaded its input, then walks back over its predecessors (64 at a time, one
 // per lane of the look-back wave) until it meets an inclusive prefix.
 //
-// Tile ids come from an atomic counter, so a tile only ever waits on tiles
-// whose workgroups are already running (forward progress does not depend on
-// dispatch order).
+// Tile id = blockIdx.x (scan; onesweep passes over 32-bit keys) or an atomic
+// counter (copy_if; onesweep passes over 64-bit keys), whichever measured
+// faster per kernel (profiles/r02_ubench_tile_order_ab.log).
+// blockIdx forward progress: the dispatcher hands out a
+// kernel's workgroups in increasing id order (round robin over the XCDs,
+// each XCD in order), so the lowest unfinished tile is always resident (every
+// workgroup dispatched before it on its XCD has a lower id and has finished)
+// and all of its predecessors are done -- it completes, and by induction so
+// does the grid.  Round 1 took ids from an atomic counter instead, which
+// needs no dispatch-order argument but puts one device-scope round trip
+// (1-3 us while HBM is saturated) in front of every tile's first load:
+// 2.83-2.84 ms vs 2.70 ms for the 2^30 int64 scan, i.e. the scan's tile
+// copy floor (scripts/ubench/scan3.hip, profiles/r02_ubench_scan_tile_order.log).
+// With the atomic counter a tile only waits on tiles whose workgroups are
+// already running, with no dispatch-order argument.  Every wait is bounded
+// (kSpinLimit), so a broken ordering assumption raises the device error word
+// instead of hanging.
 //
 // Hand-off form: the data IS the flag (MI355X guide, Guideline 16 recipe R2).
 // A value is published as 8-byte granules {status tag : 32, value word : 32},

@@ -10,10 +10,12 @@ namespace hpxhip {
 namespace scan_detail {
 
 // Shipped tile shape: 1024 threads x 16 vectors of 16 B = 256 KiB per tile,
-// one workgroup per CU (122 VGPRs).  Tile ids come from one atomic counter,
-// which saturates at ~88 increments per microsecond (MI355X guide, row
-// `dequeue`): at 32 KiB tiles the counter, not HBM, bounded the scan
-// (measured 3.3 ms for 2^30 int64 even with the look-back removed).  Fewer,
+// one workgroup per CU (122 VGPRs).  Tile id = blockIdx.x (lookback.hpp; the
+// round-1 atomic counter is the DYN_ID ablation: its dequeue round trip in
+// front of every tile cost 0.11-0.13 ms at 2^30 int64).  The counter also
+// saturates at ~88 increments per microsecond (MI355X guide, row `dequeue`):
+// at 32 KiB tiles it, not HBM, bounded the scan (measured 3.3 ms for 2^30
+// int64 even with the look-back removed).  Fewer,
 // larger tiles also mean fewer look-back hand-offs: at 2^30 int64 the same
 // kernel takes 2.99 ms with 128 KiB tiles (two workgroups per CU), 2.85 ms
 // with 192 KiB and 2.82 ms with 256 KiB (scripts/ubench/scan.hip,
@@ -68,7 +70,8 @@ __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& 
 }
 
 template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED, int ROUNDS = kRounds,
-          int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false, int LBK = 1>
+          int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false, int LBK = 1,
+          bool DYN_ID = HPXHIP_TILE_DYN_ID>
 __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init,
                                                    const T* prefix_dev, uint32_t* counter, tile_state<T> st) {
     constexpr int V = 16 / sizeof(T);
@@ -80,10 +83,12 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
     __shared__ uint32_t s_tile;
     __shared__ T s_wave_total[WAVES];
 
-    if (threadIdx.x == 0)
-        s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint64_t tile = s_tile;
+    if constexpr (DYN_ID) {
+        if (threadIdx.x == 0)
+            s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+    }
+    const uint64_t tile = DYN_ID ? s_tile : blockIdx.x;
     const int wave = threadIdx.x / kWave;
     const int lane = lane_id();
     const T id = Op::template identity<T>();

@@ -175,7 +175,13 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         auto launch = [&](auto gtag, auto rbtag) {
             using G = decltype(gtag);
             constexpr int RB = decltype(rbtag)::value;
-            hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB>), grid, block, 0,
+            // Tile ids: blockIdx for 32-bit keys (4 x 8-bit passes 15.9 vs
+            // 16.3 ms at 2^30), the atomic counter for 64-bit keys (9-bit
+            // pass 5.85 vs 6.23 ms, byte pass 4.93 vs 5.00;
+            // profiles/r02_ubench_tile_order_ab.log).
+            constexpr bool DYN = sizeof(U) == 8;
+            hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB, true, DYN>),
+                               grid, block, 0,
                                s, kin, kout, vin, vout, cnt, shift, bstart, reinterpret_cast<G*>(base + L.lb), counter,
                                err, X{});
         };

@@ -153,7 +153,7 @@ __global__ __launch_bounds__(R) void k_bin_offsets(const unsigned long long* __r
 // frees 64 KiB of LDS but the scattered 8-B stores make the pass 3x slower
 // (14.3 vs 4.85 ms at 2^30 u64, profiles/r02_ubench_onesweep_direct.log).
 template <typename U, typename VAL, bool HAS_VAL, typename G, typename X, int THREADS = 512, int ITEMS = 16,
-          int LBB = 8, int RB = 8, bool STAGE = true>
+          int LBB = 8, int RB = 8, bool STAGE = true, bool DYN_ID = HPXHIP_TILE_DYN_ID>
 __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin, U* __restrict__ kout,
                                                        const VAL* __restrict__ vin, VAL* __restrict__ vout,
                                                        uint64_t n, int shift,
@@ -177,10 +177,12 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     const int t = threadIdx.x;
     const int wave = t / kWave;
     const int lane = lane_id();
-    if (t == 0) s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // tile order = dispatch order (lookback.hpp); DYN_ID: ablation with ids
+    // from the atomic counter
+    if (DYN_ID && t == 0) s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int i = t; i < WAVES * R; i += THREADS) (&s_whist[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t tile = s_tile;
+    const uint64_t tile = DYN_ID ? s_tile : blockIdx.x;
     const uint64_t tile_base = tile * TILE;
     const uint64_t wbase = tile_base + static_cast<uint64_t>(wave) * (TILE / WAVES);
 
