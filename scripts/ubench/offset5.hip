@@ -1,0 +1,89 @@
+// Microbenchmark (round 2, session 2): do the relative base addresses of the
+// STREAM arrays matter?  With equal low-order address bits, b[i], c[i] and
+// a[i] of a triad map to the same HBM channel/bank at the same moment (the
+// classic STREAM array-padding effect).  Triad and copy at 2^30 doubles with
+// the shipped kernel shape (64-thread blocks, one 16-B vector per thread, nt
+// loads and stores), arrays placed inside one allocation at 8 GiB + delta
+// strides, against three separate hipMallocs.
+// build: hipcc -O3 --offload-arch=gfx950 -std=c++17 offset5.hip -o offset5
+#include "../../hpx_amd/csrc/common.hpp"
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+using namespace hpxhip;
+using V = vec<double, 2>;
+
+__global__ __launch_bounds__(64) void k_triad(const V* b, const V* c, V* a, uint64_t nv) {
+    const uint64_t i = blockIdx.x * 64ull + threadIdx.x;
+    if (i < nv) {
+        const V x = ld_stream(&b[i]), y = ld_stream(&c[i]);
+        V r;
+        r.v[0] = x.v[0] + 3.0 * y.v[0];
+        r.v[1] = x.v[1] + 3.0 * y.v[1];
+        st_stream(&a[i], r);
+    }
+}
+__global__ __launch_bounds__(64) void k_copy(const V* in, V* out, uint64_t nv) {
+    const uint64_t i = blockIdx.x * 64ull + threadIdx.x;
+    if (i < nv) st_stream(&out[i], ld_stream(&in[i]));
+}
+
+int main() {
+    const uint64_t n = 1ull << 30, nv = n / 2, bytes = n * 8;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto bench = [&](auto f) {
+        f();
+        CK(hipDeviceSynchronize());
+        std::vector<float> ts;
+        for (int r = 0; r < 7; ++r) {
+            CK(hipEventRecord(e0));
+            f();
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        return ts[0];
+    };
+    const unsigned grid = unsigned(nv / 64);
+    const uint64_t pad = 64 << 10;
+    // Each trial perturbs the placement with a dummy allocation, then times the
+    // triad on three plain hipMallocs and on three padded ones whose arrays
+    // start 0 / 4 / 8 KiB into their allocation (b, c, a).
+    for (int trial = 0; trial < 10; ++trial) {
+        void* dummy = nullptr;
+        if (trial) CK(hipMalloc(&dummy, uint64_t(trial) * (37ull << 20)));
+        char *a, *b, *c;
+        CK(hipExtMallocWithFlags((void**)&b, bytes, hipDeviceMallocContiguous));
+        CK(hipExtMallocWithFlags((void**)&c, bytes, hipDeviceMallocContiguous));
+        CK(hipExtMallocWithFlags((void**)&a, bytes, hipDeviceMallocContiguous));
+        CK(hipMemset(b, 0, bytes));
+        CK(hipMemset(c, 0, bytes));
+        const float t_plain = bench([&] {
+            hipLaunchKernelGGL(k_triad, dim3(grid), dim3(64), 0, 0, (const V*)b, (const V*)c, (V*)a, nv); });
+        const float c_plain = bench([&] {
+            hipLaunchKernelGGL(k_copy, dim3(grid), dim3(64), 0, 0, (const V*)b, (V*)a, nv); });
+        CK(hipFree(a)); CK(hipFree(b)); CK(hipFree(c));
+        // one 32 GiB segment, arrays carved consecutively with a 4 KiB stagger
+        char* seg;
+        CK(hipExtMallocWithFlags((void**)&seg, 32ull << 30, hipDeviceMallocContiguous));
+        char* B = seg; char* C = seg + bytes + 4096; char* A = seg + 2 * bytes + 8192;
+        CK(hipMemset(B, 0, bytes));
+        CK(hipMemset(C, 0, bytes));
+        const float t_col = bench([&] {
+            hipLaunchKernelGGL(k_triad, dim3(grid), dim3(64), 0, 0, (const V*)B, (const V*)C, (V*)A, nv); });
+        const float c_col = bench([&] {
+            hipLaunchKernelGGL(k_copy, dim3(grid), dim3(64), 0, 0, (const V*)B, (V*)C, nv); });
+        printf("trial %d  triad contig-sep %6.3f  contig-seg %6.3f ms | copy contig-sep %6.3f segment %6.3f ms | a-b %ld\n", trial,
+               t_plain, t_col, c_plain, c_col, (long)(a - b));
+        fflush(stdout);
+        CK(hipFree(seg));
+        if (dummy) CK(hipFree(dummy));
+    }
+    return 0;
+}
