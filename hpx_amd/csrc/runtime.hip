@@ -15,10 +15,7 @@
 #include "internal.hpp"
 
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
-#include <map>
-#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -338,168 +335,6 @@ int hpxhip_stream_wait_event(hpxhip_stream stream, hpxhip_event event) {
 }
 
 // -------------------------------------------------------------- memory
-// HBM segment arena for large allocations (>= 64 MiB).
-//
-// Where the driver places separately allocated multi-GiB arrays decides how
-// well their streams interleave in HBM: the same STREAM triad kernel over
-// three plain 8-GiB hipMallocs ran 3.78-3.84 ms in some placements and
-// 4.02-4.14 ms in others, within one process (5 of 14 and 5 of 12 trials
-// slow; scripts/ubench/offset{2,6,7}.hip).  Arrays carved from one
-// zero-filled segment ran 3.77-3.81 ms in 46 of 46 trials over segment sizes
-// of 25-48 GiB (offset6/offset8), with a 4-KiB stagger between consecutive
-// arrays worth another 0.02-0.05 ms (offset3) -- the "slow box" triads of
-// round 1 were this placement lottery.  So hpxhip_malloc carves large
-// requests from per-device segments (default 48 GiB, HPXHIP_ARENA_GIB, 0 =
-// off): first fit, 2-MiB aligned plus a rotating 4-KiB color.  hpxhip_free
-// synchronizes the device first (the hipFree contract: memory may still be
-// in use by queued work) and releases a segment to the driver once its last
-// block is freed.  A segment that cannot be had at full size is allocated at
-// the request's size; a request the driver cannot satisfy is out_of_memory.
-namespace {
-
-constexpr size_t kArenaMin = size_t(64) << 20;
-constexpr size_t kArenaAlign = size_t(2) << 20;
-constexpr size_t kArenaStagger = 4096;
-constexpr uint32_t kArenaColors = 16;
-
-struct arena_segment {
-    int device = 0;
-    char* base = nullptr;
-    size_t bytes = 0;
-    std::map<size_t, size_t> free;  // offset -> length, disjoint, coalesced
-    size_t live = 0;                // blocks in use
-};
-struct arena_block {
-    arena_segment* seg;
-    size_t off;
-    size_t len;
-};
-
-std::mutex g_arena_mutex;
-std::vector<std::unique_ptr<arena_segment>> g_segments;
-std::unordered_map<void*, arena_block> g_blocks;
-uint32_t g_color = 0;
-
-size_t arena_segment_bytes() {
-    static const size_t v = [] {
-        const char* e = std::getenv("HPXHIP_ARENA_GIB");
-        const long gib = e ? std::strtol(e, nullptr, 10) : 48;
-        return gib > 0 ? static_cast<size_t>(gib) << 30 : size_t(0);
-    }();
-    return v;
-}
-
-// First fit of `bytes` at a 2-MiB boundary + color * 4 KiB inside a free range.
-bool arena_carve(arena_segment& s, size_t bytes, uint32_t color, size_t* off) {
-    for (auto it = s.free.begin(); it != s.free.end(); ++it) {
-        const size_t start = it->first, end = it->first + it->second;
-        const size_t p = align_up(start, kArenaAlign) + color * kArenaStagger;
-        if (p + bytes > end) continue;
-        s.free.erase(it);
-        if (p > start) s.free[start] = p - start;
-        if (end > p + bytes) s.free[p + bytes] = end - (p + bytes);
-        *off = p;
-        return true;
-    }
-    return false;
-}
-
-void arena_release(arena_segment& s, size_t off, size_t len) {
-    auto next = s.free.lower_bound(off);
-    if (next != s.free.end() && next->first == off + len) {
-        len += next->second;
-        next = s.free.erase(next);
-    }
-    if (next != s.free.begin()) {
-        auto prev = std::prev(next);
-        if (prev->first + prev->second == off) {
-            prev->second += len;
-            return;
-        }
-    }
-    s.free[off] = len;
-}
-
-// Device already current.  0, or an allocation error (the caller falls back
-// to a plain hipMalloc).
-int arena_alloc(int device, size_t bytes, void** ptr) {
-    if (bytes > (size_t(1) << 50)) return HPXHIP_ERROR_OUT_OF_MEMORY;
-    std::lock_guard<std::mutex> lk(g_arena_mutex);
-    const uint32_t color = g_color++ % kArenaColors;
-    for (auto& sp : g_segments) {
-        size_t off = 0;
-        if (sp->device == device && arena_carve(*sp, bytes, color, &off)) {
-            ++sp->live;
-            *ptr = sp->base + off;
-            g_blocks[*ptr] = arena_block{sp.get(), off, bytes};
-            return 0;
-        }
-    }
-    const size_t need = align_up(bytes + kArenaAlign + kArenaColors * kArenaStagger, kArenaAlign);
-    size_t size = std::max(arena_segment_bytes(), need);
-    void* base = nullptr;
-    hipError_t e = hipMalloc(&base, size);
-    if (e != hipSuccess && size > need) {
-        (void)hipGetLastError();
-        size = need;
-        e = hipMalloc(&base, size);
-    }
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        return map_alloc_error(e);
-    }
-    // zero-filled once (the measured placement was of filled segments)
-    e = hipMemset(base, 0, size);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e != hipSuccess) {
-        (void)hipFree(base);
-        return static_cast<int>(e);
-    }
-    auto seg = std::make_unique<arena_segment>();
-    seg->device = device;
-    seg->base = static_cast<char*>(base);
-    seg->bytes = size;
-    seg->free[0] = size;
-    size_t off = 0;
-    if (!arena_carve(*seg, bytes, color, &off) && !arena_carve(*seg, bytes, 0, &off)) {
-        (void)hipFree(base);
-        return HPXHIP_ERROR_OUT_OF_MEMORY;
-    }
-    seg->live = 1;
-    *ptr = seg->base + off;
-    g_blocks[*ptr] = arena_block{seg.get(), off, bytes};
-    g_segments.push_back(std::move(seg));
-    return 0;
-}
-
-// 1 if ptr was an arena block (then *rc is the status), 0 otherwise.
-int arena_free(void* ptr, int* rc) {
-    std::lock_guard<std::mutex> lk(g_arena_mutex);
-    auto it = g_blocks.find(ptr);
-    if (it == g_blocks.end()) return 0;
-    arena_segment* s = it->second.seg;
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(s->device);
-    hipError_t e = hipDeviceSynchronize();
-    arena_release(*s, it->second.off, it->second.len);
-    g_blocks.erase(it);
-    if (--s->live == 0) {
-        hipError_t fe = hipFree(s->base);
-        if (e == hipSuccess) e = fe;
-        for (auto sit = g_segments.begin(); sit != g_segments.end(); ++sit)
-            if (sit->get() == s) {
-                g_segments.erase(sit);
-                break;
-            }
-    }
-    (void)hipSetDevice(prev);
-    *rc = static_cast<int>(e);
-    return 1;
-}
-
-}  // namespace
-
 int hpxhip_malloc(int device, void** ptr, size_t bytes) {
     if (!ptr) return HPXHIP_ERROR_INVALID_ARGUMENT;
     *ptr = nullptr;
@@ -507,21 +342,12 @@ int hpxhip_malloc(int device, void** ptr, size_t bytes) {
     int prev = 0;
     HPXHIP_CHECK(hipGetDevice(&prev));
     HPXHIP_CHECK(hipSetDevice(device));
-    if (bytes >= kArenaMin && arena_segment_bytes() > 0 && arena_alloc(device, bytes, ptr) == 0) {
-        (void)hipSetDevice(prev);
-        return 0;
-    }
     hipError_t e = hipMalloc(ptr, bytes);
     if (e != hipSuccess) (void)hipGetLastError();
     (void)hipSetDevice(prev);
     return e == hipSuccess ? 0 : map_alloc_error(e);
 }
-int hpxhip_free(void* ptr) {
-    if (!ptr) return 0;
-    int rc = 0;
-    if (arena_free(ptr, &rc)) return rc;
-    return static_cast<int>(hipFree(ptr));
-}
+int hpxhip_free(void* ptr) { return ptr ? static_cast<int>(hipFree(ptr)) : 0; }
 int hpxhip_malloc_host(void** ptr, size_t bytes) {
     if (!ptr) return HPXHIP_ERROR_INVALID_ARGUMENT;
     *ptr = nullptr;

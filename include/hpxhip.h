@@ -186,13 +186,8 @@ int hpxhip_event_elapsed_ms(hpxhip_event start, hpxhip_event stop, float* ms);
 int hpxhip_stream_wait_event(hpxhip_stream stream, hpxhip_event event);
 
 /* ------------------------------------------------------------- memory */
-/* hip::allocator::allocate/deallocate (allocator.hpp:108-160).  Requests of
-   64 MiB or more are carved from per-device zero-filled HBM segments
-   (default 48 GiB; HPXHIP_ARENA_GIB, 0 = plain hipMalloc), so the large
-   arrays of one program share a placement: the triad over three separately
-   allocated 8-GiB arrays varies 3.78-4.14 ms with where the driver put them,
-   over segment-carved arrays 3.77-3.81 ms.  hpxhip_free synchronizes the
-   device (as hipFree does) and returns an emptied segment to the driver. */
+/* hip::allocator::allocate/deallocate (allocator.hpp:108-160): hipMalloc /
+   hipFree; hipErrorOutOfMemory -> HPXHIP_ERROR_OUT_OF_MEMORY. */
 int hpxhip_malloc(int device, void** ptr, size_t bytes);
 int hpxhip_free(void* ptr);
 int hpxhip_malloc_host(void** ptr, size_t bytes); /* pinned */
