@@ -34,7 +34,7 @@ using hit_word = std::conditional_t<(BITS <= 32), uint32_t, uint64_t>;
 // SV: tile-state value type (uint32_t halves the look-back granules; valid
 // while n < 2^32).
 template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4, int ABL = 0, typename SV = uint64_t,
-          bool DYN_ID = HPXHIP_TILE_DYN_ID>
+          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = false>
 __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out, uint64_t n, Pred pred,
                                                        uint64_t* count_dev, uint32_t* counter,
                                                        tile_state<SV> st, uint64_t ntiles) {
@@ -158,7 +158,10 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out,
 #pragma unroll
         for (int k = 0; k < V; ++k) {
             const uint32_t j = k * kWave + lane;
-            if (j < cnt) out[base + round_base + j] = stage[j];
+            if (j < cnt) {
+                if constexpr (NT_STORE) st_stream(&out[base + round_base + j], stage[j]);
+                else out[base + round_base + j] = stage[j];
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next round's writes
         round_base += cnt;

@@ -16,7 +16,11 @@ namespace scan_detail {
 // saturates at ~88 increments per microsecond (MI355X guide, row `dequeue`):
 // at 32 KiB tiles it, not HBM, bounded the scan (measured 3.3 ms for 2^30
 // int64 even with the look-back removed).  Fewer,
-// larger tiles also mean fewer look-back hand-offs: at 2^30 int64 the same
+// larger tiles also mean fewer look-back hand-offs.  Output stores are `nt`
+// (NT_STORE): in blockIdx order 2.70-2.71 vs 2.78 ms for 2^30 int64 and
+// 2.82-2.85 vs 2.96 for f64 with plain stores; under the atomic counter `nt`
+// stores were slower, which is why round 1 rejected them
+// (profiles/r02_ubench_scan_nt_store.log).  At 2^30 int64 the same
 // kernel takes 2.99 ms with 128 KiB tiles (two workgroups per CU), 2.85 ms
 // with 192 KiB and 2.82 ms with 256 KiB (scripts/ubench/scan.hip,
 // profiles/r01_ubench_scan_structure.log).  A variant with a dedicated
@@ -71,7 +75,7 @@ __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& 
 
 template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED, int ROUNDS = kRounds,
           int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false, int LBK = 1,
-          bool DYN_ID = HPXHIP_TILE_DYN_ID>
+          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = true>
 __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init,
                                                    const T* prefix_dev, uint32_t* counter, tile_state<T> st) {
     constexpr int V = 16 / sizeof(T);
@@ -169,7 +173,8 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
             VT y;
 #pragma unroll
             for (int e = 0; e < V; ++e) y.v[e] = op(pre, x[r].v[e]);
-            dst[r * kWave + lane] = y;
+            if constexpr (NT_STORE) st_stream(&dst[r * kWave + lane], y);
+            else dst[r * kWave + lane] = y;
         }
     } else {
 #pragma unroll
