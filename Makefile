@@ -18,7 +18,7 @@ KHDR     := $(wildcard hpx_amd/csrc/*.hpp) include/hpxhip.h
 ORACLE   := oracle/_build/liboracle.so
 OFLAGS   := -O2 -fPIC -std=c++17 -ffp-contract=off -Wall -pthread
 
-.PHONY: all lib oracle clean cxxtests
+.PHONY: all lib oracle clean cxxtests oracle-sanitize
 
 # C++ tests of include/hpx (plain g++ host code linked to the C ABI library)
 CXXT     := compute_api algorithms_known_answer stream_hip for_loop_merge stencil_partitioned
@@ -43,6 +43,13 @@ $(LIB): $(KOBJ)
 $(ORACLE): oracle/oracle.cpp oracle/oracle.h
 	@mkdir -p $(dir $@)
 	$(CXX) $(OFLAGS) -shared -o $@ oracle/oracle.cpp
+
+# The oracle under ASan + UBSan (host code only)
+SANFLAGS := -O0 -std=c++17 -ffp-contract=off -pthread -fsanitize=address,undefined -fno-sanitize-recover=all
+oracle-sanitize: tests/cxx/bin/oracle_sanitize
+tests/cxx/bin/oracle_sanitize: tests/cxx/oracle_sanitize.cpp oracle/oracle.cpp oracle/oracle.h include/hpxhip.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(SANFLAGS) tests/cxx/oracle_sanitize.cpp oracle/oracle.cpp -o $@
 
 # ... and the hipcc-compiled ones (device closures, HPX_HOST_DEVICE lambdas)
 HIPT     := device_closures partitioned_vector
