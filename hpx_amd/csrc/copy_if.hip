@@ -81,6 +81,7 @@ size_t copy_if_scratch_bytes(int dtype, uint64_t n) {
 
 extern "C" int hpxhip_copy_if(int dtype, int pred_kind, const void* pred_arg, const void* in, void* out, uint64_t n,
                               uint64_t* count_dev, hpxhip_stream stream, void* scratch, size_t scratch_bytes) {
+    HPXHIP_ANNOTATE("hpxhip_copy_if");
     if (!count_dev || (n && (!in || !out))) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     device_guard g(s);

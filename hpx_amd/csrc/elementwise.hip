@@ -246,6 +246,7 @@ extern "C" {
 
 int hpxhip_generate_at(int dtype, int kind, uint64_t seed, uint64_t index_base, int64_t lo, int64_t hi, void* data,
                        uint64_t n, hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_generate_at");
     if (n == 0) return 0;
     if (!data || kind < HPXHIP_GEN_IOTA || kind > HPXHIP_GEN_UNIT) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -263,10 +264,12 @@ int hpxhip_generate_at(int dtype, int kind, uint64_t seed, uint64_t index_base, 
 
 int hpxhip_generate(int dtype, int kind, uint64_t seed, int64_t lo, int64_t hi, void* data, uint64_t n,
                     hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_generate");
     return hpxhip_generate_at(dtype, kind, seed, 0, lo, hi, data, n, stream);
 }
 
 int hpxhip_fill(int dtype, const void* value, void* data, uint64_t n, hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_fill");
     if (n == 0) return 0;
     if (!value || !data) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -291,6 +294,7 @@ int hpxhip_fill(int dtype, const void* value, void* data, uint64_t n, hpxhip_str
 }
 
 int hpxhip_copy(int dtype, const void* in, void* out, uint64_t n, hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_copy");
     if (n == 0) return 0;
     if (!in || !out) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -305,6 +309,7 @@ int hpxhip_copy(int dtype, const void* in, void* out, uint64_t n, hpxhip_stream 
 
 int hpxhip_for_each(int dtype, int unary_kind, const void* scalars, void* data, uint64_t n,
                     hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_for_each");
     if (n == 0) return 0;
     if (!data) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -320,6 +325,7 @@ int hpxhip_for_each(int dtype, int unary_kind, const void* scalars, void* data, 
 
 int hpxhip_transform(int in_dtype, int compute_dtype, int out_dtype, int unary_kind, const void* scalars,
                      const void* in, void* out, uint64_t n, hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_transform");
     if (n == 0) return 0;
     if (!in || !out) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -340,6 +346,7 @@ int hpxhip_transform(int in_dtype, int compute_dtype, int out_dtype, int unary_k
 int hpxhip_transform_binary(int in_dtype, int compute_dtype, int out_dtype, int binary_kind,
                             const void* scalars, const void* in1, const void* in2, void* out, uint64_t n,
                             hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_transform_binary");
     if (n == 0) return 0;
     if (!in1 || !in2 || !out) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -370,6 +377,7 @@ static bool strided_span_ok(int64_t stride, uint64_t n, size_t elem) {
 int hpxhip_transform_strided(int in_dtype, int compute_dtype, int out_dtype, int unary_kind, const void* scalars,
                              const void* in, int64_t in_stride, void* out, int64_t out_stride, uint64_t n,
                              hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_transform_strided");
     if (n == 0) return 0;
     if (!in || !out || (out_stride == 0 && n > 1)) return HPXHIP_ERROR_INVALID_ARGUMENT;
     if (!strided_span_ok(in_stride, n, dtype_size(in_dtype)) || !strided_span_ok(out_stride, n, dtype_size(out_dtype)))
@@ -398,6 +406,7 @@ int hpxhip_transform_binary_strided(int in_dtype, int compute_dtype, int out_dty
                                     const void* scalars, const void* in1, int64_t in1_stride, const void* in2,
                                     int64_t in2_stride, void* out, int64_t out_stride, uint64_t n,
                                     hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_transform_binary_strided");
     if (n == 0) return 0;
     if (!in1 || !in2 || !out || (out_stride == 0 && n > 1)) return HPXHIP_ERROR_INVALID_ARGUMENT;
     if (!strided_span_ok(in1_stride, n, dtype_size(in_dtype)) || !strided_span_ok(in2_stride, n, dtype_size(in_dtype)) ||

@@ -25,6 +25,30 @@ namespace hpxhip {
         if (e_ != hipSuccess) return static_cast<int>(e_);  \
     } while (0)
 
+// ------------------------------------------------------------ annotation
+// HPX names the work of each algorithm for its tracers (annotate_function,
+// hpx/util/annotated_function.hpp:38-115, used per chunk in
+// for_each.hpp:173 and transform.hpp:133).  Here each C-ABI algorithm call
+// is one roctx range ("hpxhip_scan", ...) on the calling host thread, around
+// the enqueue of its kernels -- visible with `rocprofv3 --marker-trace`.
+// Off unless HPXHIP_ROCTX=1; the roctx library is then dlopen'ed, so the
+// library has no link-time dependency on the profiler.
+bool roctx_enabled();
+void roctx_push(const char* name);
+void roctx_pop();
+struct annotate {
+    bool on;
+    explicit annotate(const char* name) : on(roctx_enabled()) {
+        if (on) roctx_push(name);
+    }
+    ~annotate() {
+        if (on) roctx_pop();
+    }
+    annotate(const annotate&) = delete;
+    annotate& operator=(const annotate&) = delete;
+};
+#define HPXHIP_ANNOTATE(name) ::hpxhip::annotate hpxhip_annotate_(name)
+
 template <typename T>
 struct tag {
     using type = T;

@@ -258,6 +258,7 @@ extern "C" {
 
 int hpxhip_merge(int dtype, const void* in1, uint64_t n1, const void* in2, uint64_t n2, void* out, int descending,
                  hpxhip_stream stream, void* scratch, size_t scratch_bytes) {
+    HPXHIP_ANNOTATE("hpxhip_merge");
     if (n1 + n2 == 0) return 0;
     if ((n1 && !in1) || (n2 && !in2) || !out) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -272,6 +273,7 @@ int hpxhip_merge(int dtype, const void* in1, uint64_t n1, const void* in2, uint6
 
 int hpxhip_sorted_bounds(int dtype, const void* sorted, uint64_t n, const void* values_dev, uint64_t m, int upper,
                          int descending, uint64_t* out_dev, hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_sorted_bounds");
     if (m == 0) return 0;
     if ((n && !sorted) || !values_dev || !out_dev) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -300,6 +302,7 @@ int hpxhip_sorted_bounds(int dtype, const void* sorted, uint64_t n, const void* 
 // add per wave); 0 <=> sorted.  *count_dev is overwritten.
 int hpxhip_unsorted_pairs(int dtype, const void* keys, uint64_t n, int descending, uint64_t* count_dev,
                           hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_unsorted_pairs");
     if (!count_dev || (n && !keys)) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     device_guard g(s);

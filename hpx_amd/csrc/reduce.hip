@@ -260,6 +260,7 @@ extern "C" {
 int hpxhip_transform_reduce(int in_dtype, int acc_dtype, int red_op, int conv_kind, const void* conv_scalars,
                             const void* init, const void* in, uint64_t n, void* out_dev, hpxhip_stream stream,
                             void* scratch, size_t scratch_bytes) {
+    HPXHIP_ANNOTATE("hpxhip_transform_reduce");
     if (!init || !out_dev || (n && !in)) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     device_guard g(s);
@@ -284,6 +285,7 @@ int hpxhip_transform_reduce(int in_dtype, int acc_dtype, int red_op, int conv_ki
 int hpxhip_transform_reduce_binary(int in_dtype, int acc_dtype, int red_op, int binary_kind, const void* bin_scalars,
                                    const void* init, const void* in1, const void* in2, uint64_t n, void* out_dev,
                                    hpxhip_stream stream, void* scratch, size_t scratch_bytes) {
+    HPXHIP_ANNOTATE("hpxhip_transform_reduce_binary");
     if (!init || !out_dev || (n && (!in1 || !in2))) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     device_guard g(s);

@@ -14,7 +14,10 @@
 //     hpx::out_of_memory as allocator.hpp:118-124 does).
 #include "internal.hpp"
 
+#include <dlfcn.h>
+
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -110,6 +113,32 @@ int scratch_get(hipStream_t s, size_t bytes, void** out) {
     *out = p;
     return 0;
 }
+
+namespace {
+struct roctx_api {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+};
+const roctx_api& roctx() {
+    static const roctx_api api = [] {
+        roctx_api a;
+        const char* e = std::getenv("HPXHIP_ROCTX");
+        if (!e || e[0] != '1') return a;
+        void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return a;
+        a.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+        a.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+        if (!a.push || !a.pop) a = roctx_api{};
+        return a;
+    }();
+    return api;
+}
+}  // namespace
+
+bool roctx_enabled() { return roctx().push != nullptr; }
+void roctx_push(const char* name) { roctx().push(name); }
+void roctx_pop() { roctx().pop(); }
 
 uint32_t* device_error_word(hipStream_t s) {
     int dev = 0;
@@ -407,6 +436,7 @@ int hpxhip_scratch_bytes(int algo, int dtype, int aux_dtype, uint64_t n, size_t*
 
 int hpxhip_fold(int dtype, int op, const void* init, const void* values_dev, uint64_t count,
                 void* out_dev, hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_fold");
     if (!init || !out_dev || (count && !values_dev)) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     return with_dtype(dtype, [&](auto t) -> int {

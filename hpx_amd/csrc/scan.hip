@@ -83,6 +83,7 @@ size_t scan_scratch_bytes(int dtype, uint64_t n) {
 extern "C" int hpxhip_scan(int dtype, int op, int inclusive, int conv_kind, const void* conv_scalars,
                            const void* init, const void* prefix_dev, const void* in, void* out, uint64_t n,
                            hpxhip_stream stream, void* scratch, size_t scratch_bytes) {
+    HPXHIP_ANNOTATE("hpxhip_scan");
     if (n == 0) return 0;
     if (!in || !out || (!init && !prefix_dev)) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);

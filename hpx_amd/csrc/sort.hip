@@ -381,6 +381,7 @@ extern "C" {
 
 int hpxhip_sort(int dtype, void* keys, uint64_t n, int descending, hpxhip_stream stream, void* scratch,
                 size_t scratch_bytes) {
+    HPXHIP_ANNOTATE("hpxhip_sort");
     if (n < 2) return 0;
     if (!keys) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -394,6 +395,7 @@ int hpxhip_sort(int dtype, void* keys, uint64_t n, int descending, hpxhip_stream
 
 int hpxhip_sort_by_key(int key_dtype, int value_dtype, void* keys, void* values, uint64_t n, int descending,
                        hpxhip_stream stream, void* scratch, size_t scratch_bytes) {
+    HPXHIP_ANNOTATE("hpxhip_sort_by_key");
     if (n < 2) return 0;
     if (!keys || !values) return HPXHIP_ERROR_INVALID_ARGUMENT;
     const size_t vs = dtype_size(value_dtype);

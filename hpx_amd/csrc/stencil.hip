@@ -283,6 +283,7 @@ extern "C" {
 
 int hpxhip_stencil_heat_step(const double* cur, double* next, uint64_t n, const double* left_halo_dev,
                              const double* right_halo_dev, double k, double dt, double dx, hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_stencil_heat_step");
     if (n == 0) return 0;
     if (!cur || !next || !left_halo_dev || !right_halo_dev || cur == next) return HPXHIP_ERROR_INVALID_ARGUMENT;
     if ((n / 2 + kThreads - 1) / kThreads > 0x7fffffffull) return HPXHIP_ERROR_INVALID_ARGUMENT;
@@ -296,6 +297,7 @@ int hpxhip_stencil_heat_step(const double* cur, double* next, uint64_t n, const 
 int hpxhip_stencil_heat_steps(const double* cur, double* next, uint64_t n, uint64_t out_lo, uint64_t out_hi,
                               const double* left_halo_dev, const double* right_halo_dev, int steps, double k,
                               double dt, double dx, hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_stencil_heat_steps");
     if (out_hi > n || out_lo > out_hi) return HPXHIP_ERROR_INVALID_ARGUMENT;
     if (out_hi == out_lo) return 0;
     if (!cur || !next || !left_halo_dev || !right_halo_dev || cur == next) return HPXHIP_ERROR_INVALID_ARGUMENT;
@@ -315,6 +317,7 @@ int hpxhip_stencil_heat_steps(const double* cur, double* next, uint64_t n, uint6
 
 int hpxhip_stencil_heat_run(double* u0, double* u1, uint64_t n, uint64_t nt, double k, double dt, double dx,
                             hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_stencil_heat_run");
     if (n == 0 || nt == 0) return 0;
     if (!u0 || !u1 || u0 == u1) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -326,6 +329,7 @@ int hpxhip_stencil_heat_run(double* u0, double* u1, uint64_t n, uint64_t nt, dou
 
 int hpxhip_stencil_heat_run_fused(double* u0, double* u1, uint64_t n, uint64_t nt, double k, double dt, double dx,
                                   int* result_in_u1, hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_stencil_heat_run_fused");
     if (!result_in_u1) return HPXHIP_ERROR_INVALID_ARGUMENT;
     *result_in_u1 = 0;
     if (n == 0 || nt == 0) return 0;

@@ -4,6 +4,7 @@ against the golden fixtures from the reference's known-answer tests, and
 size-independent properties at large n.  Calls go through the Python mirror
 of the HPX API into the C ABI (include/hpxhip.h)."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -13,6 +14,8 @@ from hpx_amd import execution as ex, functional as F
 from hpx_amd import parallel as P
 from conftest import golden_cases, load_golden
 from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -489,3 +492,27 @@ def test_copy_if_state64(pol, gpu_target, n, monkeypatch):
     exp = O.copy_if(a, "not_less_than", 0)
     assert end - o.begin() == exp.size
     np.testing.assert_array_equal(o.to_host()[: exp.size], exp)
+
+
+@pytest.mark.gpu
+def test_roctx_annotation_path():
+    """HPXHIP_ROCTX=1 (roctx range per C-ABI algorithm call, the
+    annotate_function analogue) leaves results unchanged: a scan and a sort
+    in a child process with the ranges on."""
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, hpx_amd as hpx\n"
+        "from hpx_amd import execution as ex, parallel as P\n"
+        "t = hpx.target(0); pol = ex.par.on(hpx.default_executor(t))\n"
+        "v = hpx.vector(100003, dtype=np.int64, tgt=t); P.generate(pol, v.begin(), v.end(), 'range', 5, -9, 9)\n"
+        "h = np.array([v[i] for i in range(0, 100003, 997)])\n"
+        "w = hpx.vector(100003, dtype=np.int64, tgt=t)\n"
+        "P.inclusive_scan(pol, v.begin(), v.end(), w.begin())\n"
+        "s = P.reduce(pol, v.begin(), v.end(), 0)\n"
+        "assert w[100002] == s, (w[100002], s)\n"
+        "P.sort(pol, v.begin(), v.end()); assert P.is_sorted(pol, v.begin(), v.end())\n"
+        "print('roctx ok')\n")
+    env = dict(os.environ, HPXHIP_ROCTX="1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "roctx ok" in r.stdout, r.stdout + r.stderr
