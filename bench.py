@@ -247,6 +247,7 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
     res["copy_if_int64"] = {"ms": round(ms, 4), "gbs_model_12B": round(12 * n / ms / 1e6, 1),
                             "pct_peak": pct(12 * n / ms / 1e6)}
     res["segmented_reduce_int64"] = seg_reduce_row(S, F, comm, tgt, pol, x)
+    res["double_reduce_scan"] = double_row(hpx, L, P, F, tgt, pol, n)
     # sort of 2^30 uint64 keys (8 GiB + 8 GiB workspace)
     keys = hpx.vector(n, dtype=np.uint64, tgt=tgt)
     regen = lambda: P.generate(pol, keys.begin(), keys.end(), "bits", 7)  # noqa: E731
@@ -304,6 +305,28 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
     dbuf.free()
     res["host_device_copy_1GiB"] = xfer
     return res
+
+
+def double_row(hpx, L, P, F, tgt, pol, n):
+    """configs[1]'s double leg: transform_reduce and inclusive_scan over 2^30
+    doubles in [0, 1) (53-bit mantissas, so the sums round).  Check: the last
+    inclusive value against the reduce within the FP-scan tolerance of
+    DESIGN.md ((ntiles + 64) * u * value)."""
+    xd = hpx.vector(n, dtype=np.float64, tgt=tgt)
+    yd = hpx.vector(n, dtype=np.float64, tgt=tgt)
+    P.generate(pol, xd.begin(), xd.end(), "unit", 3)
+    ms_r = timed(L, tgt, lambda: P.reduce(pol, xd.begin(), xd.end(), 0.0, F.plus))
+    ms_s = timed(L, tgt, lambda: P.inclusive_scan(pol, xd.begin(), xd.end(), yd.begin(), F.plus, 0.0))
+    r = float(P.reduce(pol, xd.begin(), xd.end(), 0.0, F.plus))
+    last = float(yd[n - 1])
+    ntiles = -(-n // (1024 * 12 * 2))
+    ok = abs(last - r) <= (ntiles + 64) * 2.0 ** -53 * abs(r) * 2
+    xd.free()
+    yd.free()
+    return {"elements": n, "reduce_ms": round(ms_r, 4), "reduce_gbs": round(8 * n / ms_r / 1e6, 1),
+            "reduce_pct_peak": pct(8 * n / ms_r / 1e6), "scan_ms": round(ms_s, 4),
+            "scan_gbs": round(16 * n / ms_s / 1e6, 1), "scan_pct_peak": pct(16 * n / ms_s / 1e6),
+            "sum": r, "scan_last_matches_reduce": bool(ok)}
 
 
 def sort_check(P, F, pol, tgt, keys, regen):
