@@ -34,7 +34,7 @@ using hit_word = std::conditional_t<(BITS <= 32), uint32_t, uint64_t>;
 // SV: tile-state value type (uint32_t halves the look-back granules; valid
 // while n < 2^32).
 template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4, int ABL = 0, typename SV = uint64_t,
-          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = false>
+          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = false, int RPB = 1>
 __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out, uint64_t n, Pred pred,
                                                        uint64_t* count_dev, uint32_t* counter,
                                                        tile_state<SV> st, uint64_t ntiles) {
@@ -48,7 +48,8 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out,
     __shared__ uint32_t s_tile;
     __shared__ uint32_t s_wave_total[kWaves];
     __shared__ uint64_t s_prefix;
-    __shared__ T s_stage[kWaves][kWave * V];  // one wave round of hits, compacted
+    static_assert(ROUNDS % RPB == 0, "rounds per write-out batch");
+    __shared__ T s_stage[kWaves][kWave * V * RPB];  // RPB wave rounds of hits, compacted
 
     if constexpr (DYN_ID) {  // ablation: tile ids from the atomic counter
         if (threadIdx.x == 0)
@@ -137,34 +138,43 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out,
         }
         return;
     }
+    // RPB rounds per batch: the batch's hits are compacted into LDS
+    // back to back (one LDS wait per batch instead of one per round) and
+    // stored as one contiguous run.
     T* stage = s_stage[wave];
-    uint32_t round_base = 0;
+    uint32_t out_base = 0;
 #pragma unroll
-    for (int r = 0; r < ROUNDS; ++r) {
-        uint32_t cnt = 0, below = 0;
+    for (int b = 0; b < ROUNDS / RPB; ++b) {
+        uint32_t bcnt = 0;
 #pragma unroll
-        for (int e = 0; e < V; ++e) {
-            const uint64_t m = __ballot((hit >> (r * V + e)) & 1u);
-            below += rank_below(m);
-            cnt += static_cast<uint32_t>(__builtin_popcountll(m));
+        for (int rr = 0; rr < RPB; ++rr) {
+            const int r = b * RPB + rr;
+            uint32_t cnt = 0, below = 0;
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const uint64_t m = __ballot((hit >> (r * V + e)) & 1u);
+                below += rank_below(m);
+                cnt += static_cast<uint32_t>(__builtin_popcountll(m));
+            }
+            uint32_t lane_before = 0;
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+                if ((hit >> (r * V + e)) & 1u) stage[bcnt + below + lane_before++] = x[r].v[e];
+            bcnt += cnt;
         }
-        uint32_t lane_before = 0;
-#pragma unroll
-        for (int e = 0; e < V; ++e)
-            if ((hit >> (r * V + e)) & 1u) stage[below + lane_before++] = x[r].v[e];
         // LDS is in order within a wave; the wait + clobber keep the compiler
         // from hoisting the reads above the writes of other lanes.
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int k = 0; k < V; ++k) {
+        for (int k = 0; k < V * RPB; ++k) {
             const uint32_t j = k * kWave + lane;
-            if (j < cnt) {
-                if constexpr (NT_STORE) st_stream(&out[base + round_base + j], stage[j]);
-                else out[base + round_base + j] = stage[j];
+            if (j < bcnt) {
+                if constexpr (NT_STORE) st_stream(&out[base + out_base + j], stage[j]);
+                else out[base + out_base + j] = stage[j];
             }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next round's writes
-        round_base += cnt;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next batch's writes
+        out_base += bcnt;
     }
 }
 
