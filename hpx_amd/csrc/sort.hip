@@ -23,7 +23,7 @@
 // read back once per sort).  Traffic: 8 B/key histogram + 16 B/key per
 // executed pass (+ values).
 //
-// Hybrid tail (64-bit keys only, >= 2^22 of them, >= 3 live digits, bucket
+// Hybrid tail (64-bit keys, >= 2^22 of them, >= 3 live digits, bucket
 // sizes estimated from the histograms within one workgroup's LDS): onesweep
 // passes on the two most significant live digits only (p2, then p1), which
 // orders the keys by a 16-bit prefix; k_bucket_bounds finds the 65536 bucket
@@ -32,7 +32,10 @@
 // CU's LDS (two stable LDS passes + odd-even rounds, see sort_kernel.hpp).
 // 56 B/key instead of 136 for random 2^30 u64 keys (42.3 -> 21.1 ms).
 // Buckets larger than a segment are finished by per-bucket LSD; more than
-// kMaxBigBuckets of them (skewed keys) by the plain LSD.
+// kMaxBigBuckets of them (skewed keys) by the plain LSD.  sort_by_key takes
+// the 16-bit form with the values moved by the prefix passes and staged in
+// LDS beside their keys (9216-pair segments): 2^28 u64/u64 pairs 20.7 ->
+// 9.2 ms, 104 instead of 264 B/pair (profiles/r02_sort_by_key_hybrid.log).
 #include "internal.hpp"
 #include "sort_kernel.hpp"
 
@@ -115,6 +118,11 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
 constexpr int kSegThreads16 = 1024, kSegThreads17 = 512, kSegItems = 18;
 constexpr uint64_t kCap16 = static_cast<uint64_t>(kSegThreads16) * kSegItems;
 constexpr uint64_t kCap17 = static_cast<uint64_t>(kSegThreads17) * kSegItems;
+// sort_by_key (64-bit keys): the 16-bit form with the values staged beside
+// the keys, segments of <= 1024 x 9 pairs (144 KiB of LDS with 8-B values,
+// one workgroup per CU); buckets fit up to about 2^29 random pairs.
+constexpr int kSegItemsKV = 9;
+constexpr uint64_t kCapKV = static_cast<uint64_t>(kSegThreads16) * kSegItemsKV;
 constexpr int kField17Shift = 47;  // the 9-bit field [47, 56) under the top byte
 constexpr uint64_t kHybridMin = 1ull << 22;
 constexpr size_t kMaxBigBuckets = 64;  // more oversized buckets than this -> finish as plain LSD
@@ -145,7 +153,8 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     uint32_t* err = device_error_word(s);
     const int passes = static_cast<int>(sizeof(U));
     const unsigned hist_grid = static_cast<unsigned>(current_device_info().cus * kHistBlocksPerCU);
-    const int mode = (!HAS_VAL && sizeof(U) == 8 && n >= kHybridMin) ? hybrid_mode() : 0;
+    int mode = (sizeof(U) == 8 && n >= kHybridMin) ? hybrid_mode() : 0;
+    if (HAS_VAL && mode > 16) mode = 16;  // no 9-bit pass with values
 
     auto* bits = reinterpret_cast<unsigned long long*>(base + L.bits);
     // histograms of digits [first, passes) of keys[0, cnt) -> hist, their
@@ -258,7 +267,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         return 0;
     };
 
-    if constexpr (HAS_VAL || sizeof(U) != 8) {
+    if constexpr (sizeof(U) != 8) {
         return lsd(0);
     } else {
     if (!mode || live.size() < 3) return lsd(0);
@@ -274,7 +283,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         variant = 17;
     } else if (mode >= 16) {
         if (live[1] < counted_first && (rc = count_digits(0))) return rc;  // the second byte was not counted
-        if (m_top * max_of(&h[live[1] * kRadix], kRadix) / dn <= 0.95 * kCap16) variant = 16;
+        if (m_top * max_of(&h[live[1] * kRadix], kRadix) / dn <= 0.95 * (HAS_VAL ? kCapKV : kCap16)) variant = 16;
     }
     if (!variant) return lsd(0);
 
@@ -285,9 +294,9 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     if (variant == 17) {
         if ((rc = pass(kc, ka, nullptr, nullptr, n, s2, 9, xstart))) return rc;
     } else {
-        if ((rc = pass8(kc, ka, nullptr, nullptr, n, live[1]))) return rc;
+        if ((rc = pass8(kc, ka, vc, va, n, live[1]))) return rc;
     }
-    if ((rc = pass8(ka, kc, nullptr, nullptr, n, p1))) return rc;
+    if ((rc = pass8(ka, kc, va, vc, n, p1))) return rc;
     const uint32_t nb = 256u << b2;
     auto* bounds = reinterpret_cast<uint64_t*>(base + L.bounds);
     hipLaunchKernelGGL((k_bucket_bounds<U, X>), dim3((nb + 1 + 255) / 256), dim3(256), 0, s, kc, n, 8 * p1, s2, b2, nb,
@@ -299,7 +308,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
 
     // segments: runs of whole buckets of at most `cap` keys; larger buckets
     // are finished separately
-    const uint64_t cap = variant == 17 ? kCap17 : kCap16;
+    const uint64_t cap = HAS_VAL ? kCapKV : variant == 17 ? kCap17 : kCap16;
     std::vector<uint64_t> segs;
     std::vector<std::pair<uint64_t, uint64_t>> big;
     uint64_t sb = 0, se = 0;
@@ -334,7 +343,10 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         HPXHIP_CHECK(hipMemcpyAsync(segd, segs.data(), segs.size() * 8, hipMemcpyHostToDevice, s));
         HPXHIP_CHECK(hipStreamSynchronize(s));  // `segs` is pageable and local
         const dim3 grid(static_cast<unsigned>(segs.size() / 2));
-        if (variant == 17)
+        if constexpr (HAS_VAL)
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true>), grid,
+                               dim3(kSegThreads16), 0, s, kc, segd, top_single, X{}, vc);
+        else if (variant == 17)
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems>), grid, dim3(kSegThreads17), 0, s, kc,
                                segd, top_single, X{});
         else
@@ -349,12 +361,19 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         if ((rc = histogram(kc + bs, len, 0, false))) return rc;
         U* a = kc + bs;
         U* b = ka + bs;
+        VAL* av = HAS_VAL ? vc + bs : nullptr;
+        VAL* bv = HAS_VAL ? va + bs : nullptr;
         for (size_t i = live.size(); i-- > 0;) {
             if (8 * live[i] >= s2) continue;
-            if ((rc = pass8(a, b, nullptr, nullptr, len, live[i]))) return rc;
+            if ((rc = pass8(a, b, av, bv, len, live[i]))) return rc;
             std::swap(a, b);
+            std::swap(av, bv);
         }
-        if (a != kc + bs) HPXHIP_CHECK(hipMemcpyAsync(kc + bs, a, len * sizeof(U), hipMemcpyDeviceToDevice, s));
+        if (a != kc + bs) {
+            HPXHIP_CHECK(hipMemcpyAsync(kc + bs, a, len * sizeof(U), hipMemcpyDeviceToDevice, s));
+            if constexpr (HAS_VAL)
+                HPXHIP_CHECK(hipMemcpyAsync(vc + bs, av, len * sizeof(VAL), hipMemcpyDeviceToDevice, s));
+        }
     }
     return 0;
     }

@@ -376,14 +376,20 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 //      bits) is finished by stable LSD passes over every bit under `top`.
 // Six 8-bit LDS passes for the 48 bits under a 16-bit prefix took 2.4 ms
 // each at 2^30 keys (VALU-bound ranking); this form replaces four of them.
-template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16>
+// HAS_VAL (sort_by_key): the values travel with their keys through the same
+// LDS passes and swaps (stable: the LDS passes rank in index order and the
+// odd-even rounds swap only strictly greater keys), staged in s_vals.
+template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16, typename VAL = uint32_t,
+          bool HAS_VAL = false>
 __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
-    void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf) {
+    void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf,
+                       VAL* __restrict__ vals = nullptr) {
     constexpr int WAVES = THREADS / kWave;
     constexpr int CHUNK = ITEMS * kWave;
     constexpr int BITS = static_cast<int>(sizeof(U) * 8);
     static_assert(THREADS * ITEMS < 65536, "16-bit LDS counters");
     __shared__ alignas(16) U s_keys[THREADS * ITEMS];
+    __shared__ alignas(16) VAL s_vals[HAS_VAL ? THREADS * ITEMS : 1];
     __shared__ uint16_t s_whist[WAVES][kRadix];
     __shared__ uint32_t s_local[kRadix];
     __shared__ uint32_t s_wsum[kRadix / kWave];
@@ -410,11 +416,17 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     auto active = [&](int r) -> uint64_t { return r < nfull ? ~0ull : (r == nfull ? tail_mask : 0ull); };
     U* gkeys = keys + b;
     U* lkeys = s_keys + wbase;
+    VAL* gvals = HAS_VAL ? vals + b : nullptr;
+    VAL* lvals = s_vals + (HAS_VAL ? wbase : 0);
 
     U k[ITEMS];
+    VAL v[HAS_VAL ? ITEMS : 1];
 #pragma unroll
-    for (int r = 0; r < ITEMS; ++r)
-        k[r] = ((active(r) >> lane) & 1u) ? ld_stream(&gkeys[wbase + r * kWave + lane]) : U(0);
+    for (int r = 0; r < ITEMS; ++r) {
+        const bool on = (active(r) >> lane) & 1u;
+        k[r] = on ? ld_stream(&gkeys[wbase + r * kWave + lane]) : U(0);
+        if constexpr (HAS_VAL) v[r] = on ? ld_stream(&gvals[wbase + r * kWave + lane]) : VAL(0);
+    }
 
     // one stable pass on the digit at `shift`: registers -> s_keys (ranked)
     auto pass = [&](int shift) {
@@ -461,14 +473,20 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
             if (act == 0) break;
             if ((act >> lane) & 1u) {
                 const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
-                s_keys[s_local[d] + s_whist[wave][d] + rank[r]] = k[r];
+                const uint32_t pos = s_local[d] + s_whist[wave][d] + rank[r];
+                s_keys[pos] = k[r];
+                if constexpr (HAS_VAL) s_vals[pos] = v[r];
             }
         }
         __syncthreads();
     };
     auto reload = [&] {
 #pragma unroll
-        for (int r = 0; r < ITEMS; ++r) k[r] = ((active(r) >> lane) & 1u) ? lkeys[r * kWave + lane] : U(0);
+        for (int r = 0; r < ITEMS; ++r) {
+            const bool on = (active(r) >> lane) & 1u;
+            k[r] = on ? lkeys[r * kWave + lane] : U(0);
+            if constexpr (HAS_VAL) v[r] = on ? lvals[r * kWave + lane] : VAL(0);
+        }
     };
 
     // pass schedule (one inlined copy of `pass`): the two passes under
@@ -495,6 +513,11 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
                     p.v[0] = p.v[1];
                     p.v[1] = x;
                     reinterpret_cast<V2*>(s_keys)[i] = p;
+                    if constexpr (HAS_VAL) {
+                        const VAL y = s_vals[2 * i];
+                        s_vals[2 * i] = s_vals[2 * i + 1];
+                        s_vals[2 * i + 1] = y;
+                    }
                     swapped = 1;
                 }
             }
@@ -504,6 +527,11 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
                 if (xf(a) > xf(c)) {
                     s_keys[2 * i + 1] = c;
                     s_keys[2 * i + 2] = a;
+                    if constexpr (HAS_VAL) {
+                        const VAL y = s_vals[2 * i + 1];
+                        s_vals[2 * i + 1] = s_vals[2 * i + 2];
+                        s_vals[2 * i + 2] = y;
+                    }
                     swapped = 1;
                 }
             }
@@ -517,7 +545,10 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
         __syncthreads();
         reload();
     }
-    for (uint32_t i = t; i < m; i += THREADS) st_stream(&gkeys[i], s_keys[i]);
+    for (uint32_t i = t; i < m; i += THREADS) {
+        st_stream(&gkeys[i], s_keys[i]);
+        if constexpr (HAS_VAL) st_stream(&gvals[i], s_vals[i]);
+    }
 }
 
 }  // namespace sort_detail

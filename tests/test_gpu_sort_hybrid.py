@@ -109,3 +109,51 @@ def test_low_bit_ranges(pol, gpu_target, bits):
     h = rng.integers(0, 1 << bits, (1 << 23) + 5, dtype=np.uint64)
     check(pol, gpu_target, h)
     check(pol, gpu_target, h, True)
+
+
+# ---- sort_by_key through the hybrid (16-bit form with the values staged in
+# LDS beside their keys; sort_by_key.hpp:42-78).  Checked pair for pair
+# against the oracle's stable sort_by_key: equal keys keep their input order
+# in the prefix passes, the LDS passes and the odd-even rounds.
+def check_kv(pol, tgt, k, v, desc=False):
+    dk = hpx.vector.from_host(k, tgt)
+    dv = hpx.vector.from_host(v, tgt)
+    P.sort_by_key(pol, dk.begin(), dk.end(), dv.begin(), F.greater if desc else F.less)
+    gk, gv = dk.to_host(), dv.to_host()
+    dk.free()
+    dv.free()
+    ek, ev = O.sort_by_key(k, v, desc)
+    np.testing.assert_array_equal(gk, ek)
+    np.testing.assert_array_equal(gv, ev)
+
+
+@pytest.mark.parametrize("vdt", [np.uint64, np.uint32])
+@pytest.mark.parametrize("desc", [False, True])
+def test_sort_by_key_uniform(pol, gpu_target, vdt, desc):
+    rng = np.random.default_rng(21)
+    n = (1 << 22) + 13
+    k = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    v = np.arange(n, dtype=vdt)
+    check_kv(pol, gpu_target, k, v, desc)
+
+
+def test_sort_by_key_duplicates_stable(pol, gpu_target):
+    # 2^23 keys over 2^24 values (3 live bytes: the prefix is bytes 2 and 1,
+    # buckets of ~128 pairs, many equal keys): stability decides the values
+    rng = np.random.default_rng(22)
+    n = 1 << 23
+    k = rng.integers(0, 1 << 24, n, dtype=np.uint64)
+    v = np.arange(n, dtype=np.uint64)
+    check_kv(pol, gpu_target, k, v)
+
+
+def test_sort_by_key_oversized_bucket(pol, gpu_target):
+    # one 16-bit prefix holds 20000 extra pairs (> the 9216-pair LDS segment):
+    # finished by the per-bucket LSD with its values
+    rng = np.random.default_rng(23)
+    n = 1 << 22
+    k = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    k[:20000] = (np.uint64(0xABCD) << np.uint64(48)) | rng.integers(0, 1 << 48, 20000, dtype=np.uint64)
+    k[20000:20050] = np.uint64(0xABCD) << np.uint64(48)
+    v = np.arange(n, dtype=np.uint64)
+    check_kv(pol, gpu_target, k, v)
