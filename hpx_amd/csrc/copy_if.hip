@@ -56,7 +56,12 @@ int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev,
     // Tile ids from the atomic counter: 2.33 ms vs 2.36 with blockIdx order
     // for 2^30 int64 (profiles/r02_ubench_tile_order_ab.log).
     constexpr bool kDynId = true;
-    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, 4, 0, SV, kDynId>), dim3(static_cast<unsigned>(ntiles)),
+    // Aligned, with the 32-bit look-back state: at most 64 VGPRs (8 waves per SIMD),
+    // so two workgroups share a CU.  4-byte elements compiled to 70 VGPRs
+    // at the old bound (4 waves per SIMD) and ran one workgroup per CU:
+    // int32 2^31 2.77 -> 2.38 ms (profiles/r02_ubench_copyif_occupancy.log).
+    constexpr int kMinWaves = (std::is_same_v<SV, uint32_t> && ALIGNED) ? 8 : 4;
+    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId>), dim3(static_cast<unsigned>(ntiles)),
                        dim3(kThreads), 0, s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles);
     HPXHIP_CHECK_LAUNCH();
     return 0;
