@@ -70,6 +70,7 @@ void f(hpx::compute::vector<int>& a) {
     ("device_closures", ["4242"]),
     ("partitioned_vector", []),
     ("stencil_partitioned", []),
+    ("call_overhead", []),
 ])
 def test_cxx_program(prog, args):
     exe = os.path.join(BIN, prog)
