@@ -37,9 +37,15 @@ uint64_t ntiles_for(uint64_t n) {
     return (n + tile_elems<T, ROUNDS>() - 1) / tile_elems<T, ROUNDS>();
 }
 
+// [counter | tile slots | head count]: the head count (misaligned inputs)
+// sits past the region the per-call memset clears.
+template <typename T>
+size_t head_count_off(uint64_t n) {
+    return align_up(kSlotsOff + ntiles_for<T, 8>(n) * tile_state<uint64_t>::bytes_per_tile(), 256);
+}
 template <typename T>
 size_t scratch_total(uint64_t n) {
-    return align_up(kSlotsOff + ntiles_for<T, 8>(n) * tile_state<uint64_t>::bytes_per_tile(), 256);
+    return head_count_off<T>(n) + 256;
 }
 
 // Look-back values are hit counts, at most n: below 2^32 elements they travel
@@ -48,7 +54,8 @@ size_t scratch_total(uint64_t n) {
 // one workgroup's look-back and write-out overlap the other's loads: 2^30
 // int64 at 50 % hits 2.55 -> 2.32 ms (profiles/r01_ubench_copyif_state.log).
 template <typename T, bool ALIGNED, typename SV, typename P>
-int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev, char* ws, hipStream_t s) {
+int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev, char* ws, hipStream_t s,
+                      const uint64_t* prefix0) {
     constexpr int R = rounds_for<ALIGNED>();
     const uint64_t ntiles = ntiles_for<T, R>(n);
     HPXHIP_CHECK(hipMemsetAsync(ws, 0, align_up(kSlotsOff + ntiles * tile_state<SV>::bytes_per_tile(), 256), s));
@@ -62,18 +69,21 @@ int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev,
     // int32 2^31 2.77 -> 2.38 ms (profiles/r02_ubench_copyif_occupancy.log).
     constexpr int kMinWaves = (std::is_same_v<SV, uint32_t> && ALIGNED) ? 8 : 4;
     hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId>), dim3(static_cast<unsigned>(ntiles)),
-                       dim3(kThreads), 0, s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles);
+                       dim3(kThreads), 0, s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles,
+                       prefix0);
     HPXHIP_CHECK_LAUNCH();
     return 0;
 }
 
 template <typename T, bool ALIGNED, typename P>
-int launch_copy_if(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev, char* ws, hipStream_t s) {
+int launch_copy_if(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev, char* ws, hipStream_t s,
+                   const uint64_t* prefix0 = nullptr) {
     // HPXHIP_COPY_IF_STATE64=1 forces the 64-bit form at any n (tests; read per call).
     const char* e = getenv("HPXHIP_COPY_IF_STATE64");
     const bool force64 = e && e[0] == '1';
-    if (n < (uint64_t{1} << 32) && !force64) return launch_copy_if_sv<T, ALIGNED, uint32_t>(in, out, n, p, count_dev, ws, s);
-    return launch_copy_if_sv<T, ALIGNED, uint64_t>(in, out, n, p, count_dev, ws, s);
+    if (n < (uint64_t{1} << 32) && !force64)
+        return launch_copy_if_sv<T, ALIGNED, uint32_t>(in, out, n, p, count_dev, ws, s, prefix0);
+    return launch_copy_if_sv<T, ALIGNED, uint64_t>(in, out, n, p, count_dev, ws, s, prefix0);
 }
 
 }  // namespace
@@ -104,9 +114,20 @@ extern "C" int hpxhip_copy_if(int dtype, int pred_kind, const void* pred_arg, co
             if (rc) return rc;
             const T* ip = static_cast<const T*>(in);
             T* op = static_cast<T*>(out);
-            return reinterpret_cast<uintptr_t>(in) % 16 == 0
-                       ? launch_copy_if<T, true>(ip, op, n, p, count_dev, static_cast<char*>(ws), s)
-                       : launch_copy_if<T, false>(ip, op, n, p, count_dev, static_cast<char*>(ws), s);
+            char* base = static_cast<char*>(ws);
+            const uint64_t h = head_to_align16(in, sizeof(T));
+            if (h == 0) return launch_copy_if<T, true>(ip, op, n, p, count_dev, base, s);
+            // A misaligned input whose elements are naturally aligned: the
+            // head (< 16 B) is compacted first, the rest takes the vector
+            // kernel seeded with the head's count (int64 offset by one
+            // element: 3.83 -> ~2.4 ms at 2^30, profiles/r02_unaligned_ranges.log).
+            if (h != UINT64_MAX && n > 4 * h) {
+                auto* hc = reinterpret_cast<uint64_t*>(base + head_count_off<T>(n));
+                hipLaunchKernelGGL((k_copy_if_head<T, decltype(p)>), dim3(1), dim3(64), 0, s, ip, op, h, p, hc);
+                HPXHIP_CHECK_LAUNCH();
+                return launch_copy_if<T, true>(ip + h, op, n - h, p, count_dev, base, s, hc);
+            }
+            return launch_copy_if<T, false>(ip, op, n, p, count_dev, base, s);
         });
     });
 }

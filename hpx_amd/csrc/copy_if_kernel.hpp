@@ -37,7 +37,8 @@ template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4, int
           bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = false, int RPB = 1>
 __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out, uint64_t n, Pred pred,
                                                        uint64_t* count_dev, uint32_t* counter,
-                                                       tile_state<SV> st, uint64_t ntiles) {
+                                                       tile_state<SV> st, uint64_t ntiles,
+                                                       const uint64_t* prefix0 = nullptr) {
     constexpr int V = 16 / sizeof(T);
     constexpr uint64_t TILE = tile_elems<T, ROUNDS>();
     constexpr uint64_t WAVE_ELEMS = TILE / kWaves;
@@ -101,7 +102,9 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out,
     if (wave == 0) {
         SV p = 0;
         if (tile == 0) {
-            if (lane == 0) st.publish(0, static_cast<SV>(agg), TILE_INCLUSIVE);
+            // prefix0: hits of a head the caller compacted first (misaligned input)
+            if (prefix0) p = static_cast<SV>(*prefix0);
+            if (lane == 0) st.publish(0, static_cast<SV>(p + agg), TILE_INCLUSIVE);
         } else if constexpr ((ABL & 1) == 0) {
             if (lane == 0) st.publish(tile, static_cast<SV>(agg), TILE_AGGREGATE);
             p = st.exclusive_prefix(tile, op_plus{});
@@ -176,6 +179,17 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out,
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next batch's writes
         out_base += bcnt;
     }
+}
+
+// Head of a misaligned input (fewer than 16 B of elements): compacted by one
+// thread into out[0..c), c -> *count; the aligned kernel continues from c.
+template <typename T, typename Pred>
+__global__ void k_copy_if_head(const T* in, T* out, uint64_t h, Pred pred, uint64_t* count) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint64_t c = 0;
+    for (uint64_t i = 0; i < h; ++i)
+        if (pred(in[i])) out[c++] = in[i];
+    *count = c;
 }
 
 __global__ void k_zero_count(uint64_t* c) {

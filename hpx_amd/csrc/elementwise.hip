@@ -112,10 +112,18 @@ __global__ __launch_bounds__(kThreads) void k_fill(T* out, span3 sp, T value) {
 
 // Split [0, n) into head/vector/tail for the given pointers (all must share
 // the same misalignment); returns false if they cannot be vectorised together.
+// The head also carries the written array (the last pointer) to a 1-KiB
+// boundary, so every wave's 1-KiB store covers whole 128-B lines: a range
+// that is 16-B but not line aligned otherwise writes a partial line at both
+// ends of every wave's run (triad over arrays offset by one double: 4.59 ms
+// vs 3.77 aligned, profiles/r02_unaligned_ranges.log).  The extra head (at
+// most 1008 B) is a few scalar threads.
+constexpr uintptr_t kStoreAlign = 1024;
 template <int V>
 bool make_span(uint64_t n, size_t esize, span3* sp, std::initializer_list<const void*> ptrs) {
     uint64_t head = UINT64_MAX;
     bool first = true;
+    const void* last = nullptr;
     for (const void* p : ptrs) {
         uint64_t h = head_to_align16(p, esize);
         if (h == UINT64_MAX) return false;
@@ -125,7 +133,10 @@ bool make_span(uint64_t n, size_t esize, span3* sp, std::initializer_list<const 
         } else if (h != head) {
             return false;
         }
+        last = p;
     }
+    const uintptr_t vstart = reinterpret_cast<uintptr_t>(last) + head * esize;  // 16-B aligned
+    head += ((kStoreAlign - vstart % kStoreAlign) % kStoreAlign) / esize;
     if (head > n) head = n;
     sp->head = head;
     sp->nvec = (n - head) / V;

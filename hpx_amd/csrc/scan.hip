@@ -35,9 +35,15 @@ uint64_t ntiles_for(uint64_t n) {
     return (n + tile_elems<T, ROUNDS>() - 1) / tile_elems<T, ROUNDS>();
 }
 
+// [counter | tile slots | head carry]: the carry of a split-off head
+// (misaligned ranges) sits past the region the per-call memset clears.
+template <typename T>
+size_t carry_off(uint64_t n) {
+    return align_up(kSlotsOff + ntiles_for<T, 8>(n) * tile_state<T>::bytes_per_tile(), 256);
+}
 template <typename T>
 size_t scratch_total(uint64_t n) {
-    return align_up(kSlotsOff + ntiles_for<T, 8>(n) * tile_state<T>::bytes_per_tile(), 256);
+    return carry_off<T>(n) + 256;
 }
 
 template <typename T, bool INCL, bool ALIGNED, typename Conv, typename Op>
@@ -51,6 +57,49 @@ int launch_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init, const
                        0, s, in, out, n, conv, op, init, prefix_dev, reinterpret_cast<uint32_t*>(ws), st);
     HPXHIP_CHECK_LAUNCH();
     return 0;
+}
+
+// Head of a range whose input and output share a misalignment: scanned by one
+// thread (left fold from the init / device prefix), its carry left in
+// *carry for the vector kernel over the rest.
+template <typename T, bool INCL, typename Conv, typename Op>
+__global__ void k_scan_head(const T* in, T* out, uint64_t h, Conv conv, Op op, T init, const T* prefix_dev,
+                            T* carry) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    T acc = prefix_dev ? *prefix_dev : init;
+    for (uint64_t i = 0; i < h; ++i) {
+        const T x = conv(in[i]);
+        if (INCL) {
+            acc = op(acc, x);
+            out[i] = acc;
+        } else {
+            out[i] = acc;
+            acc = op(acc, x);
+        }
+    }
+    *carry = acc;
+}
+
+// Misaligned input and output with the same offset inside 16 B: split off a
+// head that brings the output to a 1-KiB boundary (whole-line stores for
+// every wave) and scan the rest with the vector kernel seeded by the head's
+// carry.  int64 offset by one element: 3.8 -> ~2.7 ms at 2^30
+// (profiles/r02_unaligned_ranges.log).  Returns -1 when the split does not
+// apply (the element-wise kernel takes the range).
+template <typename T, bool INCL, typename Conv, typename Op>
+int launch_scan_split(const T* in, T* out, uint64_t n, Conv conv, Op op, T init, const T* prefix_dev, char* ws,
+                      hipStream_t s) {
+    const uintptr_t ia = reinterpret_cast<uintptr_t>(in), oa = reinterpret_cast<uintptr_t>(out);
+    if (ia % 16 != oa % 16 || ia % sizeof(T) != 0) return -1;
+    uint64_t h = head_to_align16(out, sizeof(T));
+    const uintptr_t v = oa + h * sizeof(T);
+    h += ((1024 - v % 1024) % 1024) / sizeof(T);
+    if (n <= 4 * h + 1024) return -1;
+    T* carry = reinterpret_cast<T*>(ws + carry_off<T>(n));
+    hipLaunchKernelGGL((k_scan_head<T, INCL, Conv, Op>), dim3(1), dim3(64), 0, s, in, out, h, conv, op, init,
+                       prefix_dev, carry);
+    HPXHIP_CHECK_LAUNCH();
+    return launch_scan<T, INCL, true>(in + h, out + h, n - h, conv, op, init, carry, ws, s);
 }
 
 template <typename T, typename F>
@@ -104,11 +153,14 @@ extern "C" int hpxhip_scan(int dtype, int op, int inclusive, int conv_kind, cons
                 const T* pd = static_cast<const T*>(prefix_dev);
                 const T* ip = static_cast<const T*>(in);
                 T* op_ = static_cast<T*>(out);
-                if (inclusive)
-                    return aligned ? launch_scan<T, true, true>(ip, op_, n, conv, o, iv, pd, base, s)
-                                   : launch_scan<T, true, false>(ip, op_, n, conv, o, iv, pd, base, s);
-                return aligned ? launch_scan<T, false, true>(ip, op_, n, conv, o, iv, pd, base, s)
-                               : launch_scan<T, false, false>(ip, op_, n, conv, o, iv, pd, base, s);
+                if (inclusive) {
+                    if (aligned) return launch_scan<T, true, true>(ip, op_, n, conv, o, iv, pd, base, s);
+                    const int r = launch_scan_split<T, true>(ip, op_, n, conv, o, iv, pd, base, s);
+                    return r >= 0 ? r : launch_scan<T, true, false>(ip, op_, n, conv, o, iv, pd, base, s);
+                }
+                if (aligned) return launch_scan<T, false, true>(ip, op_, n, conv, o, iv, pd, base, s);
+                const int r = launch_scan_split<T, false>(ip, op_, n, conv, o, iv, pd, base, s);
+                return r >= 0 ? r : launch_scan<T, false, false>(ip, op_, n, conv, o, iv, pd, base, s);
             });
         });
     });

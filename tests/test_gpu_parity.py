@@ -516,3 +516,50 @@ def test_roctx_annotation_path():
     env = dict(os.environ, HPXHIP_ROCTX="1")
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "roctx ok" in r.stdout, r.stdout + r.stderr
+
+
+# ---- misaligned sub-ranges through the head split (scan: input and output
+# with the same offset inside 16 B -> one-thread head scan to a 1-KiB output
+# boundary, vector kernel seeded with its carry; copy_if: misaligned input ->
+# head compacted first, vector kernel seeded with its count) and through the
+# element-wise kernels (mutually misaligned), against the oracle.
+@pytest.mark.parametrize("dt", [np.int64, np.int32, np.uint32])
+@pytest.mark.parametrize("oin,oout", [(1, 1), (2, 2), (3, 3), (1, 0), (0, 3), (5, 5)])
+@pytest.mark.parametrize("incl", [True, False])
+def test_scan_misaligned_subranges(pol, gpu_target, dt, oin, oout, incl):
+    n = 300007
+    a = rnd(dt, n, 31, *((-1000, 1000) if np.dtype(dt).kind == "i" else (0, 1000)))
+    d = dev(a, gpu_target)
+    o = hpx.vector(n, dtype=dt, tgt=gpu_target)
+    m = n - max(oin, oout) - 11
+    if incl:
+        P.inclusive_scan(pol, d.begin() + oin, d.begin() + oin + m, o.begin() + oout, F.plus, 7)
+    else:
+        P.exclusive_scan(pol, d.begin() + oin, d.begin() + oin + m, o.begin() + oout, 7)
+    np.testing.assert_array_equal(o.to_host()[oout:oout + m], O.scan(a[oin:oin + m], 7, incl))
+
+
+@pytest.mark.parametrize("off", [1, 3])
+def test_scan_misaligned_in_place_f64(pol, gpu_target, off):
+    # all-1.0 doubles (exact sums): in place, both ends trimmed
+    n = 1 << 20
+    a = np.ones(n, np.float64)
+    d = dev(a, gpu_target)
+    m = n - off - 5
+    P.inclusive_scan(pol, d.begin() + off, d.begin() + off + m, d.begin() + off, F.plus, 0.0)
+    got = d.to_host()
+    np.testing.assert_array_equal(got[off:off + m], np.arange(1, m + 1, dtype=np.float64))
+    assert got[0] == 1.0 and got[-1] == 1.0
+
+
+@pytest.mark.parametrize("dt,off", [(np.int64, 1), (np.int32, 1), (np.int32, 2), (np.int32, 3), (np.float64, 1)])
+@pytest.mark.parametrize("oout", [0, 1])
+def test_copy_if_misaligned_input(pol, gpu_target, dt, off, oout):
+    n = 500009
+    a = rnd(dt, n, 37, *((-1000, 1000) if np.dtype(dt).kind == "i" else ()))
+    a[off] = 5  # a hit inside the head
+    d, o = dev(a, gpu_target), hpx.vector(n, dtype=dt, tgt=gpu_target)
+    _, end = P.copy_if(pol, d.begin() + off, d.end(), o.begin() + oout, F.not_less_than(0))
+    exp = O.copy_if(a[off:], "not_less_than", 0)
+    assert end - (o.begin() + oout) == exp.size
+    np.testing.assert_array_equal(o.to_host()[oout:oout + exp.size], exp)
