@@ -94,6 +94,72 @@ __global__ __launch_bounds__(kRwThreads) void k_binary(const TI* a, const TI* b,
     }
 }
 
+// Inputs whose offset inside 16 B differs from the output's (a[i + 1] - a[i]
+// style ranges): the head brings the output to a 1-KiB boundary as above; a
+// misaligned input is read as the aligned 16-B vectors i and i + 1 and its
+// elements shifted by sh (in elements) in registers.  Plain loads: vector
+// i + 1 is the next lane's vector i, so the second read hits the cache.  The
+// caller moves the last vector to the scalar tail, so i + 1 stays inside the
+// range; head >= V keeps vector 0 at or after the range start.
+template <typename T, int V>
+__device__ __forceinline__ vec<T, V> ld_shifted(const vec<T, V>* p, uint64_t i, int sh) {
+    using VT = vec<T, V>;
+    if (sh == 0) return ld_stream(&p[i]);
+    const VT c = p[i], d = p[i + 1];
+    VT r;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+        T v = c.v[0];
+#pragma unroll
+        for (int k = 1; k < 2 * V; ++k)
+            if (k == e + sh) v = k < V ? c.v[k] : d.v[k - V];
+        r.v[e] = v;
+    }
+    return r;
+}
+
+template <typename TI, typename C, typename TO, typename F, int V>
+__global__ __launch_bounds__(kRwThreads) void k_unary_sh(const TI* in, TO* out, span3 sp, F f, int sh) {
+    using VO = vec<TO, V>;
+    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kRwThreads + threadIdx.x;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kRwThreads;
+    if (tid < sp.head) out[tid] = static_cast<TO>(f(static_cast<C>(in[tid])));
+    const uint64_t tail0 = sp.head + sp.nvec * V;
+    if (tid < sp.tail) out[tail0 + tid] = static_cast<TO>(f(static_cast<C>(in[tail0 + tid])));
+    const vec<TI, V>* vin = reinterpret_cast<const vec<TI, V>*>(in + sp.head - sh);
+    VO* vout = reinterpret_cast<VO*>(out + sp.head);
+    for (uint64_t i = tid; i < sp.nvec; i += stride) {
+        const vec<TI, V> x = ld_shifted<TI, V>(vin, i, sh);
+        VO y;
+#pragma unroll
+        for (int e = 0; e < V; ++e) y.v[e] = static_cast<TO>(f(static_cast<C>(x.v[e])));
+        st_stream(&vout[i], y);
+    }
+}
+
+template <typename TI, typename C, typename TO, typename F, int V>
+__global__ __launch_bounds__(kRwThreads) void k_binary_sh(const TI* a, const TI* b, TO* out, span3 sp, F f, int sha,
+                                                          int shb) {
+    using VO = vec<TO, V>;
+    const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kRwThreads + threadIdx.x;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kRwThreads;
+    if (tid < sp.head) out[tid] = static_cast<TO>(f(static_cast<C>(a[tid]), static_cast<C>(b[tid])));
+    const uint64_t tail0 = sp.head + sp.nvec * V;
+    if (tid < sp.tail)
+        out[tail0 + tid] = static_cast<TO>(f(static_cast<C>(a[tail0 + tid]), static_cast<C>(b[tail0 + tid])));
+    const vec<TI, V>* va = reinterpret_cast<const vec<TI, V>*>(a + sp.head - sha);
+    const vec<TI, V>* vb = reinterpret_cast<const vec<TI, V>*>(b + sp.head - shb);
+    VO* vout = reinterpret_cast<VO*>(out + sp.head);
+    for (uint64_t i = tid; i < sp.nvec; i += stride) {
+        const vec<TI, V> x = ld_shifted<TI, V>(va, i, sha);
+        const vec<TI, V> y = ld_shifted<TI, V>(vb, i, shb);
+        VO z;
+#pragma unroll
+        for (int e = 0; e < V; ++e) z.v[e] = static_cast<TO>(f(static_cast<C>(x.v[e]), static_cast<C>(y.v[e])));
+        st_stream(&vout[i], z);
+    }
+}
+
 // data[i] = value
 template <typename T, int V>
 __global__ __launch_bounds__(kThreads) void k_fill(T* out, span3 sp, T value) {
@@ -144,14 +210,43 @@ bool make_span(uint64_t n, size_t esize, span3* sp, std::initializer_list<const 
     return true;
 }
 
+// Span for inputs that are element aligned but offset from the output inside
+// 16 B: the head from the output alone (>= V elements), each input's shift,
+// and the last vector moved to the tail.  False if a pointer is not element
+// aligned or the range is too short to be worth it.
+template <int V>
+bool make_span_shifted(uint64_t n, size_t esize, span3* sp, const void* out, std::initializer_list<const void*> ins,
+                       int* sh) {
+    if (reinterpret_cast<uintptr_t>(out) % esize) return false;
+    uint64_t head = head_to_align16(out, esize);
+    const uintptr_t vstart = reinterpret_cast<uintptr_t>(out) + head * esize;
+    head += ((kStoreAlign - vstart % kStoreAlign) % kStoreAlign) / esize;
+    if (head < static_cast<uint64_t>(V)) head += kStoreAlign / esize;
+    if (n < head + 4 * kStoreAlign / esize) return false;
+    int k = 0;
+    for (const void* p : ins) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        if (a % esize) return false;
+        sh[k++] = static_cast<int>(((a + head * esize) % 16) / esize);
+    }
+    sp->head = head;
+    sp->nvec = (n - head) / V - 1;  // the last vector joins the tail
+    sp->tail = n - head - sp->nvec * V;
+    return true;
+}
+
 template <typename TI, typename C, typename TO, typename F>
 int launch_unary(const TI* in, TO* out, uint64_t n, F f, hipStream_t s) {
     constexpr int VW = 16 / (sizeof(TI) > sizeof(TO) ? sizeof(TI) : sizeof(TO));
     constexpr int V = VW < 1 ? 1 : VW;
     span3 sp;
+    int sh[1];
     if ((sizeof(TI) == sizeof(TO)) && make_span<V>(n, sizeof(TI), &sp, {in, out})) {
         hipLaunchKernelGGL((k_unary<TI, C, TO, F, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail, kRwThreads)),
                            dim3(kRwThreads), 0, s, in, out, sp, f);
+    } else if (V > 1 && sizeof(TI) == sizeof(TO) && make_span_shifted<V>(n, sizeof(TI), &sp, out, {in}, sh)) {
+        hipLaunchKernelGGL((k_unary_sh<TI, C, TO, F, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail, kRwThreads)),
+                           dim3(kRwThreads), 0, s, in, out, sp, f, sh[0]);
     } else {
         sp = span3{0, n, 0};
         hipLaunchKernelGGL((k_unary<TI, C, TO, F, 1>), dim3(grid_for(n, kRwThreads)), dim3(kRwThreads), 0, s, in, out,
@@ -166,9 +261,13 @@ int launch_binary(const TI* a, const TI* b, TO* out, uint64_t n, F f, hipStream_
     constexpr int VW = 16 / (sizeof(TI) > sizeof(TO) ? sizeof(TI) : sizeof(TO));
     constexpr int V = VW < 1 ? 1 : VW;
     span3 sp;
+    int sh[2];
     if ((sizeof(TI) == sizeof(TO)) && make_span<V>(n, sizeof(TI), &sp, {a, b, out})) {
         hipLaunchKernelGGL((k_binary<TI, C, TO, F, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail, kRwThreads)),
                            dim3(kRwThreads), 0, s, a, b, out, sp, f);
+    } else if (V > 1 && sizeof(TI) == sizeof(TO) && make_span_shifted<V>(n, sizeof(TI), &sp, out, {a, b}, sh)) {
+        hipLaunchKernelGGL((k_binary_sh<TI, C, TO, F, V>), dim3(grid_for(sp.nvec + sp.head + sp.tail, kRwThreads)),
+                           dim3(kRwThreads), 0, s, a, b, out, sp, f, sh[0], sh[1]);
     } else {
         sp = span3{0, n, 0};
         hipLaunchKernelGGL((k_binary<TI, C, TO, F, 1>), dim3(grid_for(n, kRwThreads)), dim3(kRwThreads), 0, s, a,

@@ -563,3 +563,32 @@ def test_copy_if_misaligned_input(pol, gpu_target, dt, off, oout):
     exp = O.copy_if(a[off:], "not_less_than", 0)
     assert end - (o.begin() + oout) == exp.size
     np.testing.assert_array_equal(o.to_host()[oout:oout + exp.size], exp)
+
+
+# ---- mutually misaligned elementwise ranges (inputs offset from the output
+# inside 16 B): the shifted-vector kernels (aligned vectors i and i+1 of each
+# misaligned input, elements shifted in registers), bit-exact against the
+# oracle for every relative offset of 8-B and 4-B elements.
+@pytest.mark.parametrize("dt", [np.float64, np.int64, np.int32, np.float32])
+@pytest.mark.parametrize("oa,ob,oo", [(1, 0, 0), (0, 1, 3), (1, 2, 0), (3, 1, 2), (2, 2, 1), (0, 0, 1)])
+def test_transform_binary_shifted(pol, gpu_target, dt, oa, ob, oo):
+    n = 100003
+    a, b = rnd(dt, n, 41, *((-1000, 1000) if np.dtype(dt).kind == "i" else ())), rnd(dt, n, 42, *((-1000, 1000) if np.dtype(dt).kind == "i" else ()))
+    da, db = dev(a, gpu_target), dev(b, gpu_target)
+    do = hpx.vector(n, dtype=dt, tgt=gpu_target)
+    m = n - 7
+    P.transform(pol, da.begin() + oa, da.begin() + oa + m, db.begin() + ob, db.begin() + ob + m, do.begin() + oo,
+                F.add_step())
+    np.testing.assert_array_equal(do.to_host()[oo:oo + m], O.transform_binary(a[oa:oa + m], b[ob:ob + m], "add"))
+
+
+@pytest.mark.parametrize("dt", [np.float64, np.int32])
+@pytest.mark.parametrize("oi,oo", [(1, 0), (0, 1), (3, 0), (2, 5)])
+def test_transform_unary_shifted(pol, gpu_target, dt, oi, oo):
+    n = 100003
+    x = rnd(dt, n, 43, *((-1000, 1000) if np.dtype(dt).kind == "i" else ()))
+    dx = dev(x, gpu_target)
+    do = hpx.vector(n, dtype=dt, tgt=gpu_target)
+    m = n - 9
+    P.copy(pol, dx.begin() + oi, dx.begin() + oi + m, do.begin() + oo)
+    np.testing.assert_array_equal(do.to_host()[oo:oo + m], x[oi:oi + m])
