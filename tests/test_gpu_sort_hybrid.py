@@ -157,3 +157,17 @@ def test_sort_by_key_oversized_bucket(pol, gpu_target):
     k[20000:20050] = np.uint64(0xABCD) << np.uint64(48)
     v = np.arange(n, dtype=np.uint64)
     check_kv(pol, gpu_target, k, v)
+
+
+@pytest.mark.parametrize("kdt", [np.int64, np.float64])
+def test_sort_by_key_signed_and_double_keys(pol, gpu_target, kdt):
+    rng = np.random.default_rng(24)
+    n = (1 << 22) + 5
+    if kdt is np.float64:
+        k = rng.standard_normal(n) * np.exp2(rng.integers(-40, 40, n))
+        k[:4] = [0.0, -0.0, np.inf, -np.inf]
+    else:
+        k = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    v = np.arange(n, dtype=np.uint64)
+    check_kv(pol, gpu_target, k, v)
+    check_kv(pol, gpu_target, k, v, True)
