@@ -137,6 +137,27 @@ __device__ __forceinline__ void st_stream(T* p, const T& v) {
     __builtin_nontemporal_store(w, reinterpret_cast<W*>(p));
 }
 
+// Elements [sh, sh + V) of the aligned vector pair (p[i], p[i + 1]): a
+// 16-B-vector read of a range that starts sh elements past a 16-B boundary
+// (elementwise and scan kernels for inputs offset from their output).  Plain
+// loads: p[i + 1] is the next lane's p[i], a cache hit.
+template <typename T, int V>
+__device__ __forceinline__ vec<T, V> ld_shifted(const vec<T, V>* p, uint64_t i, int sh) {
+    using VT = vec<T, V>;
+    if (sh == 0) return ld_stream(&p[i]);
+    const VT c = p[i], d = p[i + 1];
+    VT r;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+        T v = c.v[0];
+#pragma unroll
+        for (int k = 1; k < 2 * V; ++k)
+            if (k == e + sh) v = k < V ? c.v[k] : d.v[k - V];
+        r.v[e] = v;
+    }
+    return r;
+}
+
 // ---------------------------------------------------------------------------
 // Sort key order (radix sort, merge, sorted-range searches).
 // Storage bits -> ordered unsigned bits (ascending), optionally inverted:

@@ -100,24 +100,8 @@ __global__ __launch_bounds__(kRwThreads) void k_binary(const TI* a, const TI* b,
 // elements shifted by sh (in elements) in registers.  Plain loads: vector
 // i + 1 is the next lane's vector i, so the second read hits the cache.  The
 // caller moves the last vector to the scalar tail, so i + 1 stays inside the
-// range; head >= V keeps vector 0 at or after the range start.
-template <typename T, int V>
-__device__ __forceinline__ vec<T, V> ld_shifted(const vec<T, V>* p, uint64_t i, int sh) {
-    using VT = vec<T, V>;
-    if (sh == 0) return ld_stream(&p[i]);
-    const VT c = p[i], d = p[i + 1];
-    VT r;
-#pragma unroll
-    for (int e = 0; e < V; ++e) {
-        T v = c.v[0];
-#pragma unroll
-        for (int k = 1; k < 2 * V; ++k)
-            if (k == e + sh) v = k < V ? c.v[k] : d.v[k - V];
-        r.v[e] = v;
-    }
-    return r;
-}
-
+// range; head >= V keeps vector 0 at or after the range start (ld_shifted:
+// common.hpp).
 template <typename TI, typename C, typename TO, typename F, int V>
 __global__ __launch_bounds__(kRwThreads) void k_unary_sh(const TI* in, TO* out, span3 sp, F f, int sh) {
     using VO = vec<TO, V>;
