@@ -210,8 +210,9 @@ class default_executor:
         fn(self.stream_for_call(), *args)
 
     def sync_execute(self, fn, *args):
-        r = fn(self.stream_for_call(), *args)
-        self._target.synchronize()
+        s = self.stream_for_call()
+        r = fn(s, *args)
+        L.call("hpxhip_stream_synchronize", s)  # the stream the call ran on (concurrent_executor rotates)
         return r
 
     def async_execute(self, fn, *args) -> future:
