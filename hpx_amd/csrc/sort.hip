@@ -302,13 +302,54 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     hipLaunchKernelGGL((k_bucket_bounds<U, X>), dim3((nb + 1 + 255) / 256), dim3(256), 0, s, kc, n, 8 * p1, s2, b2, nb,
                        X{}, bounds);
     HPXHIP_CHECK_LAUNCH();
-    std::vector<uint64_t> off(nb + 1);
-    HPXHIP_CHECK(hipMemcpyAsync(off.data(), bounds, off.size() * 8, hipMemcpyDeviceToHost, s));
-    HPXHIP_CHECK(hipStreamSynchronize(s));
+    // the highest bit in which keys of one bucket can differ
+    const int top_single = top_bit(diff & ((uint64_t(1) << s2) - 1));
+    const uint64_t cap = HAS_VAL ? kCapKV : variant == 17 ? kCap17 : kCap16;
+    std::vector<uint64_t> off;
+    auto read_bounds = [&]() -> int {
+        off.resize(nb + 1);
+        HPXHIP_CHECK(hipMemcpyAsync(off.data(), bounds, off.size() * 8, hipMemcpyDeviceToHost, s));
+        HPXHIP_CHECK(hipStreamSynchronize(s));
+        return 0;
+    };
+    // Buckets of at least half a segment on average (random keys from about
+    // 2^29.2 up with the 17-bit prefix): one workgroup per bucket straight
+    // from the bounds, so no read-back and host packing (1.2 ms of idle GPU
+    // at 2^30, profiles/r02_sort_direct_buckets.log) sits between the prefix
+    // passes and the segment sort; only an oversized bucket brings the
+    // bounds to the host.
+    if (!HAS_VAL && variant == 17 && top_single > 0 && 2.0 * static_cast<double>(n) >= static_cast<double>(nb) * cap) {
+        auto* oversized = reinterpret_cast<uint32_t*>(bits + 2);
+        HPXHIP_CHECK(hipMemsetAsync(oversized, 0, 4, s));
+        hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true>), dim3(nb),
+                           dim3(kSegThreads17), 0, s, kc, bounds, top_single, X{}, nullptr, oversized);
+        HPXHIP_CHECK_LAUNCH();
+        uint32_t big_flag = 0;
+        HPXHIP_CHECK(hipMemcpyAsync(&big_flag, oversized, 4, hipMemcpyDeviceToHost, s));
+        HPXHIP_CHECK(hipStreamSynchronize(s));
+        if (!big_flag) return 0;
+        if ((rc = read_bounds())) return rc;
+        std::vector<std::pair<uint64_t, uint64_t>> big;
+        for (uint32_t v = 0; v < nb; ++v)
+            if (off[v + 1] - off[v] > cap) big.emplace_back(off[v], off[v + 1] - off[v]);
+        if (big.size() > kMaxBigBuckets) return lsd(0);
+        for (const auto& [bs, len] : big) {
+            if ((rc = histogram(kc + bs, len, 0, false))) return rc;
+            U* a = kc + bs;
+            U* b = ka + bs;
+            for (size_t i = live.size(); i-- > 0;) {
+                if (8 * live[i] >= s2) continue;
+                if ((rc = pass8(a, b, nullptr, nullptr, len, live[i]))) return rc;
+                std::swap(a, b);
+            }
+            if (a != kc + bs) HPXHIP_CHECK(hipMemcpyAsync(kc + bs, a, len * sizeof(U), hipMemcpyDeviceToDevice, s));
+        }
+        return 0;
+    }
+    if ((rc = read_bounds())) return rc;
 
     // segments: runs of whole buckets of at most `cap` keys; larger buckets
     // are finished separately
-    const uint64_t cap = HAS_VAL ? kCapKV : variant == 17 ? kCap17 : kCap16;
     std::vector<uint64_t> segs;
     std::vector<std::pair<uint64_t, uint64_t>> big;
     uint64_t sb = 0, se = 0;
@@ -336,8 +377,6 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     close();
     if (big.size() > kMaxBigBuckets) return lsd(0);  // plain LSD from here (the prefix passes are wasted)
 
-    // the highest bit in which keys of one bucket can differ
-    const int top_single = top_bit(diff & ((uint64_t(1) << s2) - 1));
     if (!segs.empty() && top_single > 0) {
         auto* segd = reinterpret_cast<uint64_t*>(base + L.segs);
         HPXHIP_CHECK(hipMemcpyAsync(segd, segs.data(), segs.size() * 8, hipMemcpyHostToDevice, s));

@@ -379,11 +379,16 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 // HAS_VAL (sort_by_key): the values travel with their keys through the same
 // LDS passes and swaps (stable: the LDS passes rank in index order and the
 // odd-even rounds swap only strictly greater keys), staged in s_vals.
+// BOUNDS: `seg` is the bucket-bounds array itself (segment = one bucket,
+// [seg[b], seg[b + 1])), as the host uses when buckets average at least half
+// a segment: no bounds read-back and no host packing between the prefix
+// passes and this kernel.  A bucket too large for the LDS is left alone and
+// raises *oversized (the host then finishes it by per-bucket LSD).
 template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16, typename VAL = uint32_t,
-          bool HAS_VAL = false>
+          bool HAS_VAL = false, bool BOUNDS = false>
 __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
     void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf,
-                       VAL* __restrict__ vals = nullptr) {
+                       VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr) {
     constexpr int WAVES = THREADS / kWave;
     constexpr int CHUNK = ITEMS * kWave;
     constexpr int BITS = static_cast<int>(sizeof(U) * 8);
@@ -397,8 +402,19 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     const int t = threadIdx.x;
     const int wave = t / kWave;
     const int lane = lane_id();
-    const uint64_t b = seg[2 * blockIdx.x];  // (begin, end) pairs
-    const uint32_t m = static_cast<uint32_t>(seg[2 * blockIdx.x + 1] - b);
+    uint64_t b, mm;
+    if constexpr (BOUNDS) {
+        b = seg[blockIdx.x];
+        mm = seg[blockIdx.x + 1] - b;
+        if (mm > static_cast<uint64_t>(THREADS) * ITEMS) {
+            if (t == 0) __hip_atomic_store(oversized, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    } else {
+        b = seg[2 * blockIdx.x];  // (begin, end) pairs
+        mm = seg[2 * blockIdx.x + 1] - b;
+    }
+    const uint32_t m = static_cast<uint32_t>(mm);
     if (m < 2) return;
     const U diff = xf(keys[b]) ^ xf(keys[b + m - 1]);
     int top = top_single;
