@@ -23,14 +23,17 @@
 // read back once per sort).  Traffic: 8 B/key histogram + 16 B/key per
 // executed pass (+ values).
 //
-// Hybrid tail (64-bit keys, >= 2^22 of them, >= 3 live digits, bucket
-// sizes estimated from the histograms within one workgroup's LDS): onesweep
-// passes on the two most significant live digits only (p2, then p1), which
-// orders the keys by a 16-bit prefix; k_bucket_bounds finds the 65536 bucket
-// starts by binary search; the host packs whole buckets into segments of at
-// most 18432 keys; k_bucket_sort sorts each segment completely inside one
-// CU's LDS (two stable LDS passes + odd-even rounds, see sort_kernel.hpp).
-// 56 B/key instead of 136 for random 2^30 u64 keys (42.3 -> 21.1 ms).
+// Hybrid tail (keys-only sorts and 64-bit sort_by_key, >= 2^22 keys, >= 3
+// live digits, bucket sizes estimated from the histograms within one
+// workgroup's LDS): onesweep passes on the most significant live bits only
+// (the 9-bit field under the top byte, then the top byte: a 17-bit prefix;
+// or the two top live bytes), so every prefix value is a contiguous bucket;
+// k_bucket_bounds finds the bucket starts by binary search; k_bucket_sort
+// sorts each bucket (or a host-packed run of small buckets) completely inside
+// one CU's LDS (two stable LDS passes + odd-even rounds, see sort_kernel.hpp).
+// 56 B/key instead of 136 for random 2^30 u64 keys (42.3 -> 19.0 ms); 28
+// instead of 36 for u32 keys, whose two LDS passes cover every bit under the
+// prefix (15.8 -> 13.7 ms, profiles/r02_sort_u32_hybrid.log).
 // Buckets larger than a segment are finished by per-bucket LSD; more than
 // kMaxBigBuckets of them (skewed keys) by the plain LSD.  sort_by_key takes
 // the 16-bit form with the values moved by the prefix passes and staged in
@@ -104,7 +107,7 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     return L;
 }
 
-// Hybrid tail (keys-only 64-bit sorts of at least 2^22 keys whose bucket
+// Hybrid tail (keys-only sorts of at least 2^22 keys whose bucket
 // sizes, estimated from the prefix fields' histograms, fit the LDS):
 //   17-bit prefix (top byte + the 9 bits under it): segments of <= 9216 keys
 //     sorted by 512-thread workgroups, two per CU, so one workgroup's loads
@@ -123,7 +126,9 @@ constexpr uint64_t kCap17 = static_cast<uint64_t>(kSegThreads17) * kSegItems;
 // one workgroup per CU); buckets fit up to about 2^29 random pairs.
 constexpr int kSegItemsKV = 9;
 constexpr uint64_t kCapKV = static_cast<uint64_t>(kSegThreads16) * kSegItemsKV;
-constexpr int kField17Shift = 47;  // the 9-bit field [47, 56) under the top byte
+// the 9-bit field under the top byte: bits [47, 56) of a 64-bit key, [15, 24) of a 32-bit one
+template <typename U>
+constexpr int field17_shift() { return static_cast<int>(8 * sizeof(U)) - 17; }
 constexpr uint64_t kHybridMin = 1ull << 22;
 constexpr size_t kMaxBigBuckets = 64;  // more oversized buckets than this -> finish as plain LSD
 
@@ -153,7 +158,10 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     uint32_t* err = device_error_word(s);
     const int passes = static_cast<int>(sizeof(U));
     const unsigned hist_grid = static_cast<unsigned>(current_device_info().cus * kHistBlocksPerCU);
-    int mode = (sizeof(U) == 8 && n >= kHybridMin) ? hybrid_mode() : 0;
+    constexpr int kField17Shift = field17_shift<U>();
+    // 32-bit keys: keys-only sorts (the two LDS passes under a 16/17-bit
+    // prefix then sort the whole key; no odd-even rounds needed)
+    int mode = (n >= kHybridMin && (sizeof(U) == 8 || !HAS_VAL)) ? hybrid_mode() : 0;
     if (HAS_VAL && mode > 16) mode = 16;  // no 9-bit pass with values
 
     auto* bits = reinterpret_cast<unsigned long long*>(base + L.bits);
@@ -197,7 +205,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         using R8 = std::integral_constant<int, 8>;
         using R9 = std::integral_constant<int, 9>;
         if (rb == 9) {
-            if constexpr (!HAS_VAL && sizeof(U) == 8) {
+            if constexpr (!HAS_VAL) {
                 if (L.wide) launch((unsigned long long)0, R9{});
                 else launch(uint32_t(0), R9{});
             } else {
@@ -267,9 +275,6 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         return 0;
     };
 
-    if constexpr (sizeof(U) != 8) {
-        return lsd(0);
-    } else {
     if (!mode || live.size() < 3) return lsd(0);
     auto max_of = [](const unsigned long long* c, int bins) {
         unsigned long long m = 0;
@@ -415,7 +420,6 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         }
     }
     return 0;
-    }
 }
 
 template <typename T, typename VAL, bool HAS_VAL>

@@ -32,7 +32,7 @@ timeit("incl scan f64", lambda: lib.hpxhip_scan(L.F64, L.PLUS, 1, L.U_IDENTITY, 
 gen = lambda: L.check(lib.hpxhip_generate(L.U64, L.GEN_BITS, 7, 0, 0, x, N, st))
 timeit("sort u64 (hybrid)", lambda: lib.hpxhip_sort(L.U64, x, N, 0, st, None, 0), 56 * N, reps=4, pre=gen)
 gen32 = lambda: L.check(lib.hpxhip_generate(L.U32, L.GEN_BITS, 11, 0, 0, x, N, st))
-timeit("sort u32 (LSD)", lambda: lib.hpxhip_sort(L.U32, x, N, 0, st, None, 0), 36 * N, reps=4, pre=gen32)
+timeit("sort u32 (hybrid)", lambda: lib.hpxhip_sort(L.U32, x, N, 0, st, None, 0), 36 * N, reps=4, pre=gen32)
 L.check(lib.hpxhip_stream_synchronize(st))
 d = ctypes.c_uint32()
 L.check(lib.hpxhip_device_error(0, ctypes.byref(d))); print("deverr", d.value)

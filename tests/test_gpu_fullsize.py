@@ -101,10 +101,12 @@ def test_mixed_sign_double_scan_bound(pol, gpu_target):
     assert float(np.max(np.abs(got[-1000:]))) < 0.01 * float(np.sum(np.abs(x)))
 
 
-@pytest.mark.parametrize("desc", [False, True])
-def test_sort_2p30_permutation_and_order(pol, gpu_target, desc):
+@pytest.mark.parametrize("desc,kdt", [(False, np.uint64), (True, np.uint64), (False, np.uint32)])
+def test_sort_2p30_permutation_and_order(pol, gpu_target, desc, kdt):
+    # u64: the 17-bit hybrid with direct per-bucket segments; u32: the same
+    # hybrid on 32-bit keys (two LDS passes finish each bucket)
     n = 1 << 30
-    keys = hpx.vector(n, dtype=np.uint64, tgt=gpu_target)
+    keys = hpx.vector(n, dtype=kdt, tgt=gpu_target)
     P.generate(pol, keys.begin(), keys.end(), "bits", 7)
     xor0 = P.reduce(pol, keys.begin(), keys.end(), 0, F.bit_xor)
     sum0 = P.reduce(pol, keys.begin(), keys.end(), 0, F.plus)

@@ -1,4 +1,4 @@
-"""The hybrid tail of the 64-bit keys-only sort (sort.hip: two onesweep passes
+"""The hybrid tail of the keys-only sort (64- and 32-bit keys) (sort.hip: two onesweep passes
 on the prefix -- the top byte and the 9 bits under it (17-bit form, 9216-key
 segments) or the two top live bytes (16-bit form, 18432-key segments) --,
 bucket bounds by lower_bound, one LDS-resident sort per segment of whole
@@ -109,6 +109,40 @@ def test_low_bit_ranges(pol, gpu_target, bits):
     h = rng.integers(0, 1 << bits, (1 << 23) + 5, dtype=np.uint64)
     check(pol, gpu_target, h)
     check(pol, gpu_target, h, True)
+
+
+# ---- 32-bit keys (keys-only): the same prefix passes on the top byte and the
+# 9 bits under it ([15, 24)) or the two top bytes; the two LDS passes then
+# cover every bit under the prefix, so a segment is sorted without odd-even
+# rounds.
+@pytest.mark.parametrize("logn", [22, 25])
+@pytest.mark.parametrize("dt", [np.uint32, np.int32, np.float32])
+def test_uniform_32bit(pol, gpu_target, logn, dt):
+    rng = np.random.default_rng(100 + logn)
+    n = (1 << logn) + 77
+    if dt is np.float32:
+        h = (rng.standard_normal(n) * np.exp2(rng.integers(-30, 30, n))).astype(np.float32)
+        h[:6] = [0.0, -0.0, np.inf, -np.inf, 1e-40, -1e-40]
+    else:
+        info = np.iinfo(dt)
+        h = rng.integers(info.min, info.max, n, dtype=dt, endpoint=True)
+    check(pol, gpu_target, h)
+    check(pol, gpu_target, h, True)
+
+
+def test_32bit_oversized_and_skewed(pol, gpu_target):
+    rng = np.random.default_rng(21)
+    n = 1 << 24
+    h = rng.integers(0, 2**32 - 1, n, dtype=np.uint32, endpoint=True)
+    # one 16/17-bit prefix holds 40000 extra keys (per-bucket LSD finish)
+    h[:40000] = np.uint32(0xABCD0000) | rng.integers(0, 1 << 16, 40000, dtype=np.uint32)
+    check(pol, gpu_target, h)
+    # top byte == second byte for every key: 256 oversized buckets (plain LSD)
+    top = rng.integers(0, 256, n, dtype=np.uint32)
+    h = (top << np.uint32(24)) | (top << np.uint32(16)) | rng.integers(0, 1 << 16, n, dtype=np.uint32)
+    check(pol, gpu_target, h)
+    # keys below 2^24: the prefix moves down a byte, many duplicates
+    check(pol, gpu_target, rng.integers(0, 1 << 24, n, dtype=np.uint32))
 
 
 # ---- sort_by_key through the hybrid (16-bit form with the values staged in
