@@ -159,9 +159,9 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     const int passes = static_cast<int>(sizeof(U));
     const unsigned hist_grid = static_cast<unsigned>(current_device_info().cus * kHistBlocksPerCU);
     constexpr int kField17Shift = field17_shift<U>();
-    // 32-bit keys: keys-only sorts (the two LDS passes under a 16/17-bit
-    // prefix then sort the whole key; no odd-even rounds needed)
-    int mode = (n >= kHybridMin && (sizeof(U) == 8 || !HAS_VAL)) ? hybrid_mode() : 0;
+    // 32-bit keys: the two LDS passes under a 16/17-bit prefix sort a single
+    // bucket's whole key (no odd-even rounds)
+    int mode = n >= kHybridMin ? hybrid_mode() : 0;
     if (HAS_VAL && mode > 16) mode = 16;  // no 9-bit pass with values
 
     auto* bits = reinterpret_cast<unsigned long long*>(base + L.bits);

@@ -205,3 +205,35 @@ def test_sort_by_key_signed_and_double_keys(pol, gpu_target, kdt):
     v = np.arange(n, dtype=np.uint64)
     check_kv(pol, gpu_target, k, v)
     check_kv(pol, gpu_target, k, v, True)
+
+
+# ---- sort_by_key with 32-bit keys: the 16-bit form on the two top bytes; a
+# single-bucket segment is finished by the two LDS passes, a packed run of
+# small buckets by the odd-even rounds, stable throughout.
+@pytest.mark.parametrize("kdt", [np.uint32, np.int32, np.float32])
+@pytest.mark.parametrize("vdt", [np.uint64, np.uint32])
+def test_sort_by_key_32bit_keys(pol, gpu_target, kdt, vdt):
+    rng = np.random.default_rng(31)
+    n = (1 << 24) + 9
+    if kdt is np.float32:
+        k = (rng.standard_normal(n) * np.exp2(rng.integers(-30, 30, n))).astype(np.float32)
+        k[:4] = [0.0, -0.0, np.inf, -np.inf]
+    else:
+        info = np.iinfo(kdt)
+        k = rng.integers(info.min, info.max, n, dtype=kdt, endpoint=True)
+    v = np.arange(n, dtype=vdt)
+    check_kv(pol, gpu_target, k, v)
+    check_kv(pol, gpu_target, k, v, True)
+
+
+def test_sort_by_key_32bit_duplicates_and_oversized(pol, gpu_target):
+    rng = np.random.default_rng(32)
+    n = 1 << 22
+    v = np.arange(n, dtype=np.uint64)
+    # keys below 2^20: many equal keys, packed multi-bucket segments
+    check_kv(pol, gpu_target, rng.integers(0, 1 << 20, n, dtype=np.uint32), v)
+    # one 16-bit prefix holds 20000 extra pairs: per-bucket LSD with its values
+    k = rng.integers(0, 2**32 - 1, n, dtype=np.uint32, endpoint=True)
+    k[:20000] = np.uint32(0xABCD0000) | rng.integers(0, 1 << 16, 20000, dtype=np.uint32)
+    k[20000:20050] = np.uint32(0xABCD0000)
+    check_kv(pol, gpu_target, k, v)
