@@ -138,6 +138,13 @@ int hybrid_mode() {
     return std::atoi(e);
 }
 
+// HPXHIP_SORT_DIRECT=<d>: take the per-bucket segment sort when the average
+// bucket holds at least 1/d of a segment (default 2; ablations).
+double direct_divisor() {
+    const char* e = std::getenv("HPXHIP_SORT_DIRECT");
+    return e ? std::atof(e) : 2.0;
+}
+
 inline int top_bit(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
 
 template <typename T, bool DESC, typename VAL, bool HAS_VAL>
@@ -317,17 +324,47 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         HPXHIP_CHECK(hipStreamSynchronize(s));
         return 0;
     };
-    // Buckets of at least half a segment on average (random keys from about
-    // 2^29.2 up with the 17-bit prefix): one workgroup per bucket straight
-    // from the bounds, so no read-back and host packing (1.2 ms of idle GPU
-    // at 2^30, profiles/r02_sort_direct_buckets.log) sits between the prefix
-    // passes and the segment sort; only an oversized bucket brings the
-    // bounds to the host.
-    if (!HAS_VAL && variant == 17 && top_single > 0 && 2.0 * static_cast<double>(n) >= static_cast<double>(nb) * cap) {
+    // oversized buckets: LSD over the live bytes under the prefix, with the
+    // bucket's own histogram (the byte that holds bit 47 under a 17-bit
+    // prefix is included: its prefix bit is constant inside the bucket)
+    auto finish_big = [&](const std::vector<std::pair<uint64_t, uint64_t>>& big) -> int {
+        for (const auto& [bs, len] : big) {
+            if ((rc = histogram(kc + bs, len, 0, false))) return rc;
+            U* a = kc + bs;
+            U* b = ka + bs;
+            VAL* av = HAS_VAL ? vc + bs : nullptr;
+            VAL* bv = HAS_VAL ? va + bs : nullptr;
+            for (size_t i = live.size(); i-- > 0;) {
+                if (8 * live[i] >= s2) continue;
+                if ((rc = pass8(a, b, av, bv, len, live[i]))) return rc;
+                std::swap(a, b);
+                std::swap(av, bv);
+            }
+            if (a != kc + bs) {
+                HPXHIP_CHECK(hipMemcpyAsync(kc + bs, a, len * sizeof(U), hipMemcpyDeviceToDevice, s));
+                if constexpr (HAS_VAL)
+                    HPXHIP_CHECK(hipMemcpyAsync(vc + bs, av, len * sizeof(VAL), hipMemcpyDeviceToDevice, s));
+            }
+        }
+        return 0;
+    };
+    // Buckets of at least DIRECT_DIV-th of a segment on average (random keys
+    // from about 2^29.2 up with the 17-bit prefix): one workgroup per bucket
+    // straight from the bounds, so no read-back and host packing (1.2 ms of
+    // idle GPU at 2^30, profiles/r02_sort_direct_buckets.log) sits between
+    // the prefix passes and the segment sort; only an oversized bucket brings
+    // the bounds to the host.
+    const double direct_div = direct_divisor();
+    if (top_single > 0 && (HAS_VAL || variant == 17) &&
+        direct_div * static_cast<double>(n) >= static_cast<double>(nb) * cap) {
         auto* oversized = reinterpret_cast<uint32_t*>(bits + 2);
         HPXHIP_CHECK(hipMemsetAsync(oversized, 0, 4, s));
-        hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true>), dim3(nb),
-                           dim3(kSegThreads17), 0, s, kc, bounds, top_single, X{}, nullptr, oversized);
+        if constexpr (HAS_VAL)
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true, true>), dim3(nb),
+                               dim3(kSegThreads16), 0, s, kc, bounds, top_single, X{}, vc, oversized);
+        else
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true>), dim3(nb),
+                               dim3(kSegThreads17), 0, s, kc, bounds, top_single, X{}, nullptr, oversized);
         HPXHIP_CHECK_LAUNCH();
         uint32_t big_flag = 0;
         HPXHIP_CHECK(hipMemcpyAsync(&big_flag, oversized, 4, hipMemcpyDeviceToHost, s));
@@ -338,18 +375,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         for (uint32_t v = 0; v < nb; ++v)
             if (off[v + 1] - off[v] > cap) big.emplace_back(off[v], off[v + 1] - off[v]);
         if (big.size() > kMaxBigBuckets) return lsd(0);
-        for (const auto& [bs, len] : big) {
-            if ((rc = histogram(kc + bs, len, 0, false))) return rc;
-            U* a = kc + bs;
-            U* b = ka + bs;
-            for (size_t i = live.size(); i-- > 0;) {
-                if (8 * live[i] >= s2) continue;
-                if ((rc = pass8(a, b, nullptr, nullptr, len, live[i]))) return rc;
-                std::swap(a, b);
-            }
-            if (a != kc + bs) HPXHIP_CHECK(hipMemcpyAsync(kc + bs, a, len * sizeof(U), hipMemcpyDeviceToDevice, s));
-        }
-        return 0;
+        return finish_big(big);
     }
     if ((rc = read_bounds())) return rc;
 
@@ -398,28 +424,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                                segd, top_single, X{});
         HPXHIP_CHECK_LAUNCH();
     }
-    // oversized buckets: LSD over the live bytes under the prefix, with the
-    // bucket's own histogram (the byte that holds bit 47 under a 17-bit
-    // prefix is included: its prefix bit is constant inside the bucket)
-    for (const auto& [bs, len] : big) {
-        if ((rc = histogram(kc + bs, len, 0, false))) return rc;
-        U* a = kc + bs;
-        U* b = ka + bs;
-        VAL* av = HAS_VAL ? vc + bs : nullptr;
-        VAL* bv = HAS_VAL ? va + bs : nullptr;
-        for (size_t i = live.size(); i-- > 0;) {
-            if (8 * live[i] >= s2) continue;
-            if ((rc = pass8(a, b, av, bv, len, live[i]))) return rc;
-            std::swap(a, b);
-            std::swap(av, bv);
-        }
-        if (a != kc + bs) {
-            HPXHIP_CHECK(hipMemcpyAsync(kc + bs, a, len * sizeof(U), hipMemcpyDeviceToDevice, s));
-            if constexpr (HAS_VAL)
-                HPXHIP_CHECK(hipMemcpyAsync(vc + bs, av, len * sizeof(VAL), hipMemcpyDeviceToDevice, s));
-        }
-    }
-    return 0;
+    return finish_big(big);
 }
 
 template <typename T, typename VAL, bool HAS_VAL>
