@@ -237,3 +237,23 @@ def test_sort_by_key_32bit_duplicates_and_oversized(pol, gpu_target):
     k[:20000] = np.uint32(0xABCD0000) | rng.integers(0, 1 << 16, 20000, dtype=np.uint32)
     k[20000:20050] = np.uint32(0xABCD0000)
     check_kv(pol, gpu_target, k, v)
+
+
+# ---- the direct per-bucket path (one workgroup per bucket, bounds read on
+# the device, oversized buckets flagged) forced at test sizes: normally it
+# starts where buckets average half a segment (~2^29 random keys).
+@pytest.mark.parametrize("kdt", [np.uint64, np.uint32])
+def test_direct_path_forced(pol, gpu_target, monkeypatch, kdt):
+    monkeypatch.setenv("HPXHIP_SORT_DIRECT", "100000")
+    rng = np.random.default_rng(41)
+    n = 1 << 22
+    bits = np.dtype(kdt).itemsize * 8
+    k = rng.integers(0, 2**bits - 1, n, dtype=kdt, endpoint=True)
+    check(pol, gpu_target, k)
+    # one oversized bucket (flagged by the kernel, finished by per-bucket LSD)
+    k[:30000] = kdt(0xABCD) << kdt(bits - 16) | rng.integers(0, 1 << (bits - 16), 30000, dtype=kdt)
+    k[30000:30050] = kdt(0xABCD) << kdt(bits - 16)
+    check(pol, gpu_target, k, True)
+    v = np.arange(n, dtype=np.uint64)
+    check_kv(pol, gpu_target, k, v)
+    check_kv(pol, gpu_target, k, v, True)
