@@ -561,9 +561,16 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
         __syncthreads();
         reload();
     }
-    for (uint32_t i = t; i < m; i += THREADS) {
-        st_stream(&gkeys[i], s_keys[i]);
-        if constexpr (HAS_VAL) st_stream(&gvals[i], s_vals[i]);
+    // Write-back with the lanes aligned to 64-B lines of the output (a
+    // bucket starts anywhere): each wave store then covers whole lines, not
+    // 9 part-lines per 512 B (WRITE_SIZE 1.067x the keys before).
+    const uint32_t klead = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(gkeys) % 64) / sizeof(U);
+    for (uint32_t i = t; i < m + klead; i += THREADS)
+        if (i >= klead) st_stream(&gkeys[i - klead], s_keys[i - klead]);
+    if constexpr (HAS_VAL) {
+        const uint32_t vlead = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(gvals) % 64) / sizeof(VAL);
+        for (uint32_t i = t; i < m + vlead; i += THREADS)
+            if (i >= vlead) st_stream(&gvals[i - vlead], s_vals[i - vlead]);
     }
 }
 
