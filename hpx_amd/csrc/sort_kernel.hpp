@@ -563,8 +563,12 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     }
     // Write-back with the lanes aligned to 64-B lines of the output (a
     // bucket starts anywhere): each wave store then covers whole lines, not
-    // 9 part-lines per 512 B (WRITE_SIZE 1.067x the keys before).
-    const uint32_t klead = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(gkeys) % 64) / sizeof(U);
+    // 9 part-lines per 512 B (WRITE_SIZE 1.067x -> 1.053x the keys).  Same-box
+    // A/B (profiles/r02_sort_writeback_ab.log): sort_by_key u64/u64 2^28
+    // 8.80 -> 8.56-8.67 ms; keys-only sorts neutral to 0.5 % slower, so they
+    // keep the plain loop.
+    const uint32_t klead =
+        HAS_VAL ? static_cast<uint32_t>(reinterpret_cast<uintptr_t>(gkeys) % 64) / sizeof(U) : 0u;
     for (uint32_t i = t; i < m + klead; i += THREADS)
         if (i >= klead) st_stream(&gkeys[i - klead], s_keys[i - klead]);
     if constexpr (HAS_VAL) {
