@@ -371,17 +371,33 @@ def seg_reduce_row(S, F, comm, tgt, pol, x, reps=5):
             "pct_peak_per_rank": pct(per_rank), "value": int(r)}
 
 
+STENCIL_SEED = 0xC0FFEE
+
+
+def stencil_windows(nx, nt):
+    """Checked ranges [lo, lo + count) of the stencil row: the periodic seam
+    (0 and nx - 1), 2^31 +- nt points, 2^28 / 2^29 points (2^31 / 2^32 bytes),
+    2^32 - 1 and seeded random positions (tests/test_gpu_stencil_fullsize.py)."""
+    w = [(0, 64), (nx - 64, 64), ((1 << 31) - nt - 32, 2 * nt + 64), ((1 << 28) - 32, 64), ((1 << 29) - 32, 64),
+         (nx // 2 + 1000, 64), (nx - 1, 1)]
+    w += [(int(s), 96) for s in np.random.default_rng(7).integers(0, max(1, nx - 96), 4)]
+    return [(lo, c) for lo, c in w if 0 <= lo and lo + c <= nx]
+
+
 def stencil_row(S, comm, tgt, nx, nt):
     """examples/1d_stencil heat over the ranks (strong scaling: nx points in
     total), partitioned solver with temporal blocking and the halo ring;
-    max-over-ranks wall time of nt steps.  Check: the linear ramp U0[i] = i
-    is a steady state away from the periodic wrap, so after nt steps every
-    point at distance > nt from the wrap still equals its global index
-    (sampled windows, exact)."""
+    max-over-ranks wall time of nt steps (after nt untimed warm-up steps).  Initial state: U0[i] =
+    splitmix64(seed ^ i) in [0, 1), generated on the device (no steady
+    state: every wrong neighbour, skipped step or index wrap shows).  Check:
+    sampled windows bit for bit against the serial oracle run on +-nt
+    points around each window (after nt steps point i depends only on
+    U0[i-nt .. i+nt]); each rank checks the windows inside its partition."""
     import time
     from hpx_amd import _lib as L
-    hs = S.heat_solver(nx, comm, tgt)
-    hs.do_work(1)
+    from oracle import oracle as O  # checker only, after the timed region
+    hs = S.heat_solver(nx, comm, tgt, init=("unit", STENCIL_SEED))
+    hs.do_work(nt)   # warm-up: first launches, first touch of the second buffer
     hs.synchronize()
     comm.barrier()
     t0 = time.perf_counter()
@@ -390,22 +406,23 @@ def stencil_row(S, comm, tgt, nx, nt):
     comm.barrier()
     el = max_over_ranks(comm, time.perf_counter() - t0)
     cur = hs.current
-    m = len(cur)
-    ok = True
-    for w0 in (0, m // 2, max(0, m - 4096)):
-        win = np.empty(min(4096, m - w0), np.float64)
-        L.call("hpxhip_memcpy_async", win.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(cur.data() + 8 * w0),
-               8 * win.size, L.D2H, tgt.stream)
+    ok, checked = True, 0
+    for lo, c in stencil_windows(nx, 2 * nt):
+        if lo < hs.lo or lo + c > hs.hi:
+            continue
+        win = np.empty(c, np.float64)
+        L.call("hpxhip_memcpy_async", win.ctypes.data_as(ctypes.c_void_p),
+               ctypes.c_void_p(cur.data() + 8 * (lo - hs.lo)), 8 * c, L.D2H, tgt.stream)
         tgt.synchronize()
-        g = hs.lo + w0 + np.arange(win.size)
-        far = (g > nt + 2) & (g < nx - nt - 3)  # nt + 1 steps ran (one warm-up)
-        ok = ok and bool(np.all(win[far] == g[far].astype(np.float64)))
+        ok = ok and bool(np.array_equal(win, O.stencil_window(nx, 2 * nt, STENCIL_SEED, lo, c)))
+        checked += c
     ok = bool(max_over_ranks(comm, 0.0 if ok else 1.0) == 0.0)
-    for v in hs.U:
+    for v in hs.U + [hs.H]:
         v.free()
     return {"points": nx, "ranks": comm.size, "steps": nt, "ms": round(1e3 * el, 3),
             "gpoint_steps_per_s": round(nx * nt / el / 1e9, 2), "gbs_model_16B": round(16 * nx * nt / el / 1e9, 1),
-            "ramp_check": ok, "halo_width": hs.W}
+            "init": "splitmix64(seed ^ i) in [0, 1)", "window_check_bit_exact": ok, "steps_checked": 2 * nt,
+            "points_checked_rank0": checked, "halo_width": hs.W}
 
 
 def dist_extras(S, F, comm, tgt, pol, x, n_local, world, args):

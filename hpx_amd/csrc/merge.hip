@@ -224,11 +224,25 @@ namespace hpxhip {
 size_t merge_scratch_bytes(uint64_t n) { return ((n + kTile - 1) / kTile + 1) * 8; }
 }  // namespace hpxhip
 
-// Adjacent pairs (i, i+1) with key[i] ordered after key[i+1]; thread t
-// handles the pairs starting in its 16-byte vector (the neighbour of the
-// vector's last element is the next vector's first, re-read through the cache).
+// is_sorted.hpp:40-120 counts a pair (i, i+1) as out of order iff
+// pred(key[i+1], key[i]) with pred = std::less (std::greater when
+// descending), on the VALUES: for floats -0.0 and +0.0 compare equal and a
+// NaN is never out of order (every comparison with it is false), unlike the
+// radix key order the sort uses.
+template <typename T, bool DESC>
+struct value_out_of_order {
+    using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
+    __device__ __forceinline__ bool operator()(U cur, U next) const {
+        const T a = __builtin_bit_cast(T, cur), b = __builtin_bit_cast(T, next);
+        return DESC ? (a < b) : (b < a);
+    }
+};
+
+// Adjacent pairs out of order; thread t handles the pairs starting in its
+// 16-byte vector (the neighbour of the vector's last element is the next
+// vector's first, re-read through the cache).
 template <typename U, typename X>
-__global__ __launch_bounds__(256) void k_unsorted_pairs(const U* __restrict__ keys, uint64_t n, X xf,
+__global__ __launch_bounds__(256) void k_unsorted_pairs(const U* __restrict__ keys, uint64_t n, X after,
                                                         unsigned long long* __restrict__ count) {
     constexpr int V = 16 / sizeof(U);
     using VT = vec<U, V>;
@@ -242,13 +256,13 @@ __global__ __launch_bounds__(256) void k_unsorted_pairs(const U* __restrict__ ke
         for (uint64_t v = tid; v < nvec; v += stride) {
             const VT x = ld_stream(&vk[v]);
 #pragma unroll
-            for (int e = 0; e + 1 < V; ++e) c += xf(x.v[e]) > xf(x.v[e + 1]);
+            for (int e = 0; e + 1 < V; ++e) c += after(x.v[e], x.v[e + 1]);
             const uint64_t nx = (v + 1) * V;
-            if (nx < n) c += xf(x.v[V - 1]) > xf(keys[nx]);
+            if (nx < n) c += after(x.v[V - 1], keys[nx]);
         }
-        for (uint64_t i = nvec * V + tid; i + 1 < n; i += stride) c += xf(keys[i]) > xf(keys[i + 1]);
+        for (uint64_t i = nvec * V + tid; i + 1 < n; i += stride) c += after(keys[i], keys[i + 1]);
     } else {
-        for (uint64_t i = tid; i + 1 < n; i += stride) c += xf(keys[i]) > xf(keys[i + 1]);
+        for (uint64_t i = tid; i + 1 < n; i += stride) c += after(keys[i], keys[i + 1]);
     }
     const uint64_t w = wave_reduce(c, op_plus{});
     if (lane_id() == 0 && w) atomicAdd(count, static_cast<unsigned long long>(w));
@@ -297,7 +311,7 @@ int hpxhip_sorted_bounds(int dtype, const void* sorted, uint64_t n, const void* 
 }
 
 // is_sorted.hpp:40-120 (hpx::parallel::is_sorted / is_sorted_until): the
-// number of adjacent pairs out of order under the sort's key order, counted
+// number of adjacent pairs out of order (value comparison, see above), counted
 // on the device (grid-stride, 16-B loads, wave reduction, one 64-bit atomic
 // add per wave); 0 <=> sorted.  *count_dev is overwritten.
 int hpxhip_unsorted_pairs(int dtype, const void* keys, uint64_t n, int descending, uint64_t* count_dev,
@@ -314,12 +328,12 @@ int hpxhip_unsorted_pairs(int dtype, const void* keys, uint64_t n, int descendin
         using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
         const unsigned grid = static_cast<unsigned>(std::min<uint64_t>((n + 1023) / 1024, 8192));
         if (descending)
-            hipLaunchKernelGGL((k_unsorted_pairs<U, ordered_bits<T, true>>), dim3(grid), dim3(256), 0, s,
-                               static_cast<const U*>(keys), n, ordered_bits<T, true>{},
+            hipLaunchKernelGGL((k_unsorted_pairs<U, value_out_of_order<T, true>>), dim3(grid), dim3(256), 0, s,
+                               static_cast<const U*>(keys), n, value_out_of_order<T, true>{},
                                reinterpret_cast<unsigned long long*>(count_dev));
         else
-            hipLaunchKernelGGL((k_unsorted_pairs<U, ordered_bits<T, false>>), dim3(grid), dim3(256), 0, s,
-                               static_cast<const U*>(keys), n, ordered_bits<T, false>{},
+            hipLaunchKernelGGL((k_unsorted_pairs<U, value_out_of_order<T, false>>), dim3(grid), dim3(256), 0, s,
+                               static_cast<const U*>(keys), n, value_out_of_order<T, false>{},
                                reinterpret_cast<unsigned long long*>(count_dev));
         HPXHIP_CHECK_LAUNCH();
         return 0;

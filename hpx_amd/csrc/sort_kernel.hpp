@@ -71,10 +71,16 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
     constexpr int V = 16 / sizeof(U);
     using VT = vec<U, V>;
     const uint32_t copy = threadIdx.x % COPIES;
-    const uint64_t nvec = n / V;
+    // a range starting inside a 16-B vector (a bucket of the hybrid sort's
+    // oversized-bucket finish starts anywhere): its head is counted by
+    // scalar loads and the 16-B loads start at the first aligned key
+    const uint64_t mis = (reinterpret_cast<uintptr_t>(keys) % 16) / sizeof(U);
+    const uint64_t head = mis ? (n < V - mis ? n : V - mis) : 0;
+    const U* akeys = keys + head;
+    const uint64_t nvec = (n - head) / V;
     const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * THREADS + threadIdx.x;
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * THREADS;
-    const VT* vk = reinterpret_cast<const VT*>(keys);
+    const VT* vk = reinterpret_cast<const VT*>(akeys);
     U any = 0, all = static_cast<U>(~U(0));
     auto count = [&](U b) {
         any |= b;
@@ -96,7 +102,8 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
                 for (int e = 0; e < V; ++e) count(xf(x[u].v[e]));
             }
     }
-    if (tid < n - nvec * V) count(xf(keys[nvec * V + tid]));
+    if (tid < n - head - nvec * V) count(xf(akeys[nvec * V + tid]));
+    if (tid < head) count(xf(keys[tid]));
     any = wave_reduce(any, op_bit_or{});
     all = wave_reduce(all, op_bit_and{});
     if (lane_id() == 0) {

@@ -30,6 +30,7 @@ is :class:`HipEngine` (the C ABI); there is no host fallback.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -179,10 +180,23 @@ class _DeviceMemory:
         self.torch = torch
         self.device = torch.device("cuda", tgt.device)
 
+    @contextlib.contextmanager
     def ctx(self, stream):
-        s = self.torch.cuda.ExternalStream(stream.value if hasattr(stream, "value") else int(stream),
-                                           device=self.device)
-        return self.torch.cuda.stream(s)
+        """Every RCCL call of TorchComm runs inside this: torch's current
+        stream IS the library stream, so the collective is ordered after the
+        kernels that filled its buffers (checked, not assumed)."""
+        sv = stream.value if hasattr(stream, "value") else int(stream)
+        s = self.torch.cuda.ExternalStream(sv, device=self.device)
+        with self.torch.cuda.stream(s):
+            cur = self.torch.cuda.current_stream(self.device).cuda_stream
+            if cur != sv:
+                raise RuntimeError(f"TorchComm: collective on stream {cur:#x}, not the library stream {sv:#x}")
+            yield
+
+    def retire(self):
+        """Before dropping exchange tensors that collectives or kernels on
+        the library stream may still use: wait for the device."""
+        self.torch.cuda.synchronize(self.device)
 
     def handle(self, t):
         return t.data_ptr()
@@ -213,8 +227,10 @@ class _HostMemory:
         self.device = torch.device("cpu")
 
     def ctx(self, stream):
-        import contextlib
         return contextlib.nullcontext()
+
+    def retire(self):
+        pass
 
     def handle(self, t):
         return t.numpy()
@@ -255,6 +271,7 @@ class TorchComm:
     def slots(self, nbytes: int):
         words = max(1, -(-int(nbytes) // 8))
         if self._send.numel() < words:
+            self.mem.retire()  # the old tensors may still be read by stream-ordered work
             self._send = self.torch.zeros(words, dtype=self.torch.int64, device=self.device)
             self._recv = self.torch.zeros(words * self.size, dtype=self.torch.int64, device=self.device)
         return self.mem.handle(self._send), self.mem.handle(self._recv)
@@ -396,8 +413,18 @@ class HipEngine:
 
     # --- 1d_stencil primitives
     def heat_buffers(self, n, offset, init=None):
-        """U[0] = global index (1d_stencil_4.cpp:64-66) or `init`; U[1] scratch."""
-        if init is not None:
+        """U[0] = global index (1d_stencil_4.cpp:64-66), the host array `init`,
+        or a device-generated state `init = (kind, seed)` of the global
+        sequence (hpxhip_generate_at, e.g. ("unit", s): splitmix64(s ^ i) in
+        [0, 1)); U[1] scratch."""
+        if isinstance(init, tuple):
+            kind, seed = init
+            kinds = {"unit": L.GEN_UNIT, "iota": L.GEN_IOTA}
+            u0 = vector(max(1, n), dtype=np.float64, tgt=self.tgt)
+            if n:
+                L.call("hpxhip_generate_at", L.F64, kinds[kind], int(seed), int(offset), 0, 0,
+                       ctypes.c_void_p(u0.data()), n, self.stream)
+        elif init is not None:
             u0 = vector.from_host(np.ascontiguousarray(init, np.float64), self.tgt)
         else:
             u0 = vector(max(1, n), dtype=np.float64, tgt=self.tgt)
@@ -956,7 +983,9 @@ class heat_solver:
         w = min(HALO_MAX if fuse is None else int(fuse), min(sizes))
         self.W = w if w <= 1 else w - (w % 2)
         self.k, self.dt, self.dx = k, dt, dx
-        self.U = self.eng.heat_buffers(self.n, self.lo, None if init is None else init[self.lo:self.hi])
+        if init is not None and not isinstance(init, tuple):
+            init = init[self.lo:self.hi]
+        self.U = self.eng.heat_buffers(self.n, self.lo, init)
         self.H = self.eng.halo_buffer()   # 2 slots x [left block | right block], HALO_MAX points each
         self.t = 0
         self._cur = 0    # buffer holding step t

@@ -326,9 +326,10 @@ int hpxhip_sorted_bounds(int dtype, const void* sorted, uint64_t n, const void* 
                          int upper, int descending, uint64_t* out_dev, hpxhip_stream stream);
 
 /* is_sorted.hpp:40-120: *count_dev (uint64, device; overwritten) = the
-   number of adjacent pairs (keys[i], keys[i+1]) ordered after one another
-   under the sort's key order (0 <=> sorted); full-size sort verification
-   without a host copy. */
+   number of adjacent pairs with pred(keys[i+1], keys[i]), pred = std::less
+   (std::greater if descending) on the values -- so -0.0/+0.0 are equal and
+   NaN is never out of order, as in the reference (0 <=> sorted); full-size
+   sort verification without a host copy. */
 int hpxhip_unsorted_pairs(int dtype, const void* keys, uint64_t n, int descending, uint64_t* count_dev,
                           hpxhip_stream stream);
 

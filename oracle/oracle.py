@@ -168,6 +168,29 @@ def stencil_heat(u, nt, k=0.5, dt=1.0, dx=1.0):
     return out
 
 
+def unit_at(idx, seed):
+    """generate("unit") at arbitrary global indices (hpxhip_generate_at GEN_UNIT):
+    (splitmix64(seed ^ i) >> 11) * 2^-53."""
+    z = splitmix64(np.uint64(seed) ^ np.asarray(idx, np.uint64))
+    return (z >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+
+
+def stencil_window(nx, nt, seed, lo, count, k=0.5, dt=1.0, dx=1.0):
+    """Points [lo, lo + count) of the periodic nx-point heat ring after nt
+    steps of 1d_stencil_1.cpp:41-72 from U0[i] = unit_at(i, seed).  After nt
+    steps point i depends only on U0[i - nt .. i + nt], so the serial stepper
+    runs on that window only (each step drops one point per side); the
+    window wraps around the ring.  Needs count + 2 nt <= nx."""
+    if count + 2 * nt > nx:
+        u = stencil_heat(unit_at(np.arange(nx, dtype=np.uint64), seed), nt, k, dt, dx)
+        return u[(lo + np.arange(count)) % nx]
+    g = (np.int64(lo) - nt + np.arange(count + 2 * nt, dtype=np.int64)) % np.int64(nx)
+    w = unit_at(g.astype(np.uint64), seed)
+    for _ in range(nt):
+        w = stencil_heat_step(w[1:-1], w[0], w[-1], k, dt, dx)
+    return w
+
+
 def stencil_heat_step(cur, left, right, k=0.5, dt=1.0, dx=1.0):
     cur = np.ascontiguousarray(cur, np.float64)
     out = np.empty_like(cur)

@@ -63,6 +63,6 @@ def test_bench_two_ranks_one_json_line(gpu_target):
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["global_elements"] == 2 * (1 << 22)
     x = d["extras"]
     assert x["segmented_sort_uint64"]["sorted_and_ordered"] is True
-    assert x["stencil_heat_dist"]["ramp_check"] is True and x["stencil_heat_dist"]["points"] == 1 << 22
+    assert x["stencil_heat_dist"]["window_check_bit_exact"] is True and x["stencil_heat_dist"]["points"] == 1 << 22
     r = x["segmented_reduce_int64"]
     assert r["ranks"] == 2 and r["gbs_per_rank"] > 0

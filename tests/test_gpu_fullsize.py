@@ -161,6 +161,32 @@ def test_is_sorted_small(pol, gpu_target, n):
             assert P.is_sorted(pol, v.begin() + 1, v.end())
 
 
+def _host_is_sorted(h, desc=False):
+    """is_sorted.hpp:40-120: no i with pred(h[i+1], h[i]) (pred = less / greater)."""
+    return not any((h[i] < h[i + 1]) if desc else (h[i + 1] < h[i]) for i in range(len(h) - 1))
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_is_sorted_signed_zero_and_nan(pol, gpu_target, dt):
+    """Values, not the sort's radix key order, decide: [0.0, -0.0] is sorted
+    (they compare equal), and a NaN is never out of order."""
+    nan = np.nan
+    cases = [[0.0, -0.0], [-0.0, 0.0], [1.0, -0.0, 0.0, 2.0], [1.0, nan, 0.5], [nan, nan], [nan, -1.0, 3.0],
+             [2.0, 1.0, nan], [-np.inf, -0.0, 0.0, np.inf], [3.0, 2.0, -0.0, 0.0, nan, -5.0]]
+    for c in cases:
+        for pad in (0, 1, 6):  # the pair inside a 16-B vector, across vectors, unaligned start
+            h = np.array([-1e30] * pad + c, dt)
+            v = hpx.vector.from_host(h, gpu_target)
+            for desc, comp in ((False, F.less), (True, F.greater)):
+                hh = h if not desc else np.array([1e30] * pad + c, dt)
+                if desc:
+                    v = hpx.vector.from_host(hh, gpu_target)
+                exp = _host_is_sorted(hh, desc)
+                assert P.is_sorted(pol, v.begin(), v.end(), comp) == exp, (c, pad, desc)
+                if len(hh) > 2:
+                    assert P.is_sorted(pol, v.begin() + 1, v.end(), comp) == _host_is_sorted(hh[1:], desc)
+
+
 def test_sort_2p30_oversized_bucket(pol, gpu_target):
     # 2^30 keys: the hybrid sorts one bucket per workgroup straight from the
     # bucket bounds; 30000 extra keys in one 17-bit prefix make that bucket

@@ -132,3 +132,19 @@ def test_generate_restatement_is_deterministic():
     assert r.min() >= -(1 << 20) and r.max() <= (1 << 20)
     u = O.generate(np.float64, "unit", 10000, seed=3)
     assert u.min() >= 0.0 and u.max() < 1.0
+
+
+def test_stencil_window_equals_full_ring():
+    """oracle.stencil_window (the +-nt window restatement the 2^32-point GPU
+    check uses) against the full periodic-ring oracle, at the seam, inside,
+    wrapping both ends, and in the small-ring fallback."""
+    nx, seed = 4099, 0xC0FFEE
+    for nt in (1, 2, 17, 100):
+        full = O.stencil_heat(O.unit_at(np.arange(nx, dtype=np.uint64), seed), nt)
+        for lo, c in [(0, 64), (nx - 64, 64), (nx - 1, 1), (1000, 333), (2048 - nt, 2 * nt + 1)]:
+            np.testing.assert_array_equal(O.stencil_window(nx, nt, seed, lo, c), full[lo:lo + c])
+    small = O.stencil_heat(O.unit_at(np.arange(50, dtype=np.uint64), 3), 40)
+    np.testing.assert_array_equal(O.stencil_window(50, 40, 3, 10, 20), small[10:30])
+    # unit_at is generate("unit") at arbitrary indices
+    np.testing.assert_array_equal(O.unit_at(np.arange(7, 20, dtype=np.uint64), 9),
+                                  O.generate(np.float64, "unit", 13, 9, offset=7))

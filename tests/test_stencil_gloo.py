@@ -34,7 +34,10 @@ class HeatEngine:
     stream = None
 
     def heat_buffers(self, n, offset, init=None):
-        u0 = np.arange(offset, offset + n, dtype=np.float64) if init is None else np.array(init, np.float64)
+        if isinstance(init, tuple):  # device-generated state (kind, seed) of the global sequence
+            u0 = O.unit_at(np.arange(offset, offset + n, dtype=np.uint64), init[1])
+        else:
+            u0 = np.arange(offset, offset + n, dtype=np.float64) if init is None else np.array(init, np.float64)
         return [u0, np.zeros(n)]
 
     def halo_buffer(self):
@@ -73,7 +76,16 @@ class HeatEngine:
 # (nx, nt, initial state, halo width cap: None = HALO_MAX fused steps per pass,
 # 1 = one step per exchange as in 1d_stencil_8, 4 = four)
 CASES = [(1001, 25, "ramp", None), (1001, 25, "random", None), (9, 7, "random", None), (64, 40, "random", None),
-         (1001, 11, "random", 1), (1001, 13, "random", 4), (37, 9, "random", None)]
+         (1001, 11, "random", 1), (1001, 13, "random", 4), (37, 9, "random", None), (1001, 30, "gen", None)]
+GEN = ("unit", 0xC0FFEE)  # device-generated state: splitmix64(seed ^ global i) in [0, 1)
+
+
+def _u0(nx, kind):
+    if kind == "ramp":
+        return np.arange(nx, dtype=np.float64)
+    if kind == "gen":
+        return O.unit_at(np.arange(nx, dtype=np.uint64), GEN[1])
+    return np.random.default_rng(nx).standard_normal(nx)
 
 
 def _worker(rank, size, port, q, ckdir):
@@ -84,7 +96,7 @@ def _worker(rank, size, port, q, ckdir):
         comm = S.TorchComm(None, memory="host") if size > 1 else OneRankComm()
         res = {}
         for nx, nt, kind, fuse in CASES:
-            init = None if kind == "ramp" else np.random.default_rng(nx).standard_normal(nx)
+            init = {"ramp": None, "gen": GEN}[kind] if kind in ("ramp", "gen") else _u0(nx, kind)
             try:
                 hs = S.heat_solver(nx, comm, engine=HeatEngine(), init=init, fuse=fuse)
             except ValueError:
@@ -133,8 +145,7 @@ def test_heat_solver_ring_gloo(size, tmp_path):
         assert not isinstance(results[r], Exception), results[r]
     for case in CASES:
         nx, nt, kind, fuse = case
-        u0 = np.arange(nx, dtype=np.float64) if kind == "ramp" else np.random.default_rng(nx).standard_normal(nx)
-        exp = O.stencil_heat(u0, nt)
+        exp = O.stencil_heat(_u0(nx, kind), nt)
         if results[0][case] is None:
             assert -(-nx // size) * (size - 1) >= nx
             continue
