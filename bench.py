@@ -248,6 +248,7 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
                             "pct_peak": pct(12 * n / ms / 1e6)}
     res["segmented_reduce_int64"] = seg_reduce_row(S, F, comm, tgt, pol, x)
     res["double_reduce_scan"] = double_row(hpx, L, P, F, tgt, pol, n)
+    res["stream_2p30"] = stream_row(hpx, L, P, F, tgt, pol, n)
     # sort of 2^30 uint64 keys (8 GiB + 8 GiB workspace)
     keys = hpx.vector(n, dtype=np.uint64, tgt=tgt)
     regen = lambda: P.generate(pol, keys.begin(), keys.end(), "bits", 7)  # noqa: E731
@@ -311,6 +312,52 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
     dbuf.free()
     res["host_device_copy_1GiB"] = xfer
     return res
+
+
+def stream_row(hpx, L, P, F, tgt, pol, n, iterations=10, scalar=3.0):
+    """BASELINE configs[0]: the whole STREAM benchmark (stream.cpp:294-375)
+    through the hip executor at 2^30 doubles per array: fill, a *= 2, then
+    `iterations` rounds of copy / scale / add / triad, each bracketed by HIP
+    events on the target's stream; best and average of iterations 1.. (the
+    first is skipped, :485-495), rates on the reference's byte model (:478-483:
+    2, 2, 3, 3 x 8 B per element).  check_results (:82-133) on the device:
+    min == max == the closed-form aj, bj, cj for each array."""
+    a = hpx.vector(n, dtype=np.float64, value=1.0, tgt=tgt)
+    b = hpx.vector(n, dtype=np.float64, value=2.0, tgt=tgt)
+    c = hpx.vector(n, dtype=np.float64, value=0.0, tgt=tgt)
+    P.transform(pol, a.begin(), a.end(), a.begin(), F.multiply_step(2.0))
+    kernels = (("copy", 16, lambda: P.copy(pol, a.begin(), a.end(), c.begin())),
+               ("scale", 16, lambda: P.transform(pol, c.begin(), c.end(), b.begin(), F.multiply_step(scalar))),
+               ("add", 24, lambda: P.transform(pol, a.begin(), a.end(), b.begin(), b.end(), c.begin(), F.add_step())),
+               ("triad", 24, lambda: P.transform(pol, b.begin(), b.end(), c.begin(), c.end(), a.begin(),
+                                                 F.triad_step(scalar))))
+    ev = Events(L, 8 * iterations + 2)
+    marks = []
+    for _ in range(iterations):
+        row = []
+        for _name, _b, fn in kernels:
+            e0 = ev.record(tgt.stream)
+            fn()
+            row.append((e0, ev.record(tgt.stream)))
+        marks.append(row)
+    tgt.synchronize()
+    from oracle import oracle as O  # checker only, after the timed kernels
+    aj, bj, cj = O.stream_expected(iterations, scalar)
+    ok = True
+    for v, exp in ((a, aj), (b, bj), (c, cj)):
+        lo = P.reduce(pol, v.begin(), v.end(), float("inf"), F.minimum)
+        hi = P.reduce(pol, v.begin(), v.end(), float("-inf"), F.maximum)
+        ok = ok and lo == exp and hi == exp
+    for v in (a, b, c):
+        v.free()
+    out = {"elements": n, "iterations": iterations, "check_results": bool(ok)}
+    for k, (name, nbytes, _fn) in enumerate(kernels):
+        t = [ev.ms(*marks[i][k]) for i in range(1, iterations)]
+        best = min(t)
+        out[name] = {"best_gbs": round(nbytes * n / best / 1e6, 1), "pct_peak": pct(nbytes * n / best / 1e6),
+                     "min_ms": round(best, 4), "avg_ms": round(sum(t) / len(t), 4), "max_ms": round(max(t), 4),
+                     "bytes_per_elem": nbytes}
+    return out
 
 
 def double_row(hpx, L, P, F, tgt, pol, n):
@@ -551,6 +598,14 @@ def cpu_baseline(logn):
     del keys
     nx, nt = 1 << max(10, logn - 3), 20
     t_st, _ = O.par_stencil(np.arange(nx, dtype=np.float64), nt, threads)
+    # configs[0] itself: the STREAM benchmark at 2^27 doubles on host par
+    st, abc = O.par_stream(n, threads, 3.0, 10)
+    stream = {"elements": n, "iterations": 10,
+              "check_results": bool(tuple(abc) == tuple(O.stream_expected(10, 3.0)))}
+    for name, nbytes in (("copy", 16), ("scale", 16), ("add", 24), ("triad", 24)):
+        best, avg = st[name]
+        stream[name] = {"best_gbs": round(nbytes * n / best / 1e9, 2), "min_ms": round(1e3 * best, 3),
+                        "avg_ms": round(1e3 * avg, 3)}
     return {"value": round(gbs, 2), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"2^{logn} elements: triad f64 + reduce int64 + inclusive_scan int64, best of 3, "
                       f"HPX par chunking (4*cores chunks) on {threads} std::threads",
@@ -563,7 +618,8 @@ def cpu_baseline(logn):
                                        "gbs_model_136B": round(136 * ns / t_sort / 1e9, 2)},
                        "stencil_heat": {"points": nx, "steps": nt, "ms": round(1e3 * t_st, 2),
                                         "gpoint_steps_per_s": round(nx * nt / t_st / 1e9, 3),
-                                        "gbs_model_16B": round(16 * nx * nt / t_st / 1e9, 2)}}}
+                                        "gbs_model_16B": round(16 * nx * nt / t_st / 1e9, 2)},
+                       "stream": stream}}
 
 
 if __name__ == "__main__":

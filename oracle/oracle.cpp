@@ -604,6 +604,46 @@ void* oracle_par_alloc(uint64_t bytes, int threads) {
 
 void oracle_par_free(void* p, uint64_t) { ::operator delete(p); }
 
+// stream.cpp:294-375 on the host `par` policy: fill a = 1, b = 2, c = 0,
+// a = 2a, then `iterations` rounds of copy (c = a), scale (b = s c), add
+// (c = a + b) and triad (a = b + s c), each timed; best[k] / avg[k] = min /
+// mean seconds over iterations 1.. (the first is skipped, :485-495);
+// abc[0..2] = a[0], b[0], c[0] for check_results (:82-133).  Arrays are
+// first-touched by the thread that processes them (block_allocator.hpp).
+int oracle_par_stream(uint64_t n, double s, int iterations, int threads, double* best, double* avg, double* abc) {
+    if (iterations < 2 || n == 0) return 1;
+    double* a = static_cast<double*>(oracle_par_alloc(n * 8, threads));
+    double* b = static_cast<double*>(oracle_par_alloc(n * 8, threads));
+    double* c = static_cast<double*>(oracle_par_alloc(n * 8, threads));
+    auto loop = [&](auto&& f) {
+        const double t0 = now();
+        run_par(n, threads, [&](size_t, uint64_t beg, uint64_t len) {
+            for (uint64_t i = beg; i < beg + len; ++i) f(i);
+        });
+        return now() - t0;
+    };
+    loop([&](uint64_t i) { a[i] = 1.0; b[i] = 2.0; c[i] = 0.0; });
+    loop([&](uint64_t i) { a[i] = a[i] * 2.0; });  // multiply_step(2.0), stream.cpp:303-305
+    for (int k = 0; k < 4; ++k) best[k] = 1e300, avg[k] = 0.0;
+    for (int it = 0; it < iterations; ++it) {
+        double t[4];
+        t[0] = loop([&](uint64_t i) { c[i] = a[i]; });
+        t[1] = loop([&](uint64_t i) { b[i] = c[i] * s; });  // multiply_step: val * factor_ (:234-237)
+        t[2] = loop([&](uint64_t i) { c[i] = a[i] + b[i]; });
+        t[3] = loop([&](uint64_t i) { a[i] = b[i] + c[i] * s; });  // triad_step: val1 + val2 * factor_ (:266-269)
+        if (it == 0) continue;
+        for (int k = 0; k < 4; ++k) {
+            best[k] = std::min(best[k], t[k]);
+            avg[k] += t[k] / (iterations - 1);
+        }
+    }
+    abc[0] = a[0], abc[1] = b[0], abc[2] = c[0];
+    oracle_par_free(a, n * 8);
+    oracle_par_free(b, n * 8);
+    oracle_par_free(c, n * 8);
+    return 0;
+}
+
 double oracle_par_triad(double* a, const double* b, const double* c, uint64_t n, double s, int threads) {
     const double t0 = now();
     run_par(n, threads, [&](size_t, uint64_t beg, uint64_t len) {

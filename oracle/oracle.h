@@ -100,6 +100,10 @@ void oracle_par_free(void* p, uint64_t bytes);
 /* a[i] = b[i] + s*c[i] over `threads` threads; returns seconds. */
 double oracle_par_triad(double* a, const double* b, const double* c, uint64_t n, double s,
                         int threads);
+/* stream.cpp:294-375 (copy, scale, add, triad; `iterations` rounds, the
+   first skipped): best/avg seconds per kernel, abc = a[0], b[0], c[0]. */
+int oracle_par_stream(uint64_t n, double s, int iterations, int threads, double* best, double* avg,
+                      double* abc);
 /* sum of int64 with init; returns seconds, result in *out. */
 double oracle_par_reduce_i64(const int64_t* in, uint64_t n, int64_t init, int64_t* out,
                              int threads);

@@ -264,6 +264,18 @@ def generate(dtype, kind, n, seed=0x5EED, lo=0, hi=0, offset=0):
 
 
 # ------------------------------------------------------------- host baseline
+def par_stream(n, threads, scalar=3.0, iterations=10):
+    """HPX-par restatement of the whole STREAM benchmark (stream.cpp:294-375):
+    returns ({kernel: (best s, avg s)}, (a0, b0, c0))."""
+    lib = load()
+    best, avg, abc = (ctypes.c_double * 4)(), (ctypes.c_double * 4)(), (ctypes.c_double * 3)()
+    lib.oracle_par_stream.argtypes = [ctypes.c_uint64, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    _check(lib.oracle_par_stream(n, scalar, iterations, threads, best, avg, abc), "par_stream")
+    names = ("copy", "scale", "add", "triad")
+    return {k: (best[i], avg[i]) for i, k in enumerate(names)}, tuple(abc)
+
+
 def par_triad(n, threads, scalar=3.0, reps=3):
     """HPX-par restatement of STREAM triad on `threads` host threads; returns
     best seconds."""

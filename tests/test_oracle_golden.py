@@ -148,3 +148,12 @@ def test_stencil_window_equals_full_ring():
     # unit_at is generate("unit") at arbitrary indices
     np.testing.assert_array_equal(O.unit_at(np.arange(7, 20, dtype=np.uint64), 9),
                                   O.generate(np.float64, "unit", 13, 9, offset=7))
+
+
+@pytest.mark.parametrize("iters", [2, 10])
+def test_par_stream_check_results(iters):
+    """The host-par STREAM (cpu_baseline's configs[0] leg) ends on
+    check_results' closed form (stream.cpp:82-133), as the golden fixture."""
+    times, abc = O.par_stream(100003, 3, 3.0, iters)
+    assert abc == tuple(O.stream_expected(iters, 3.0))
+    assert set(times) == {"copy", "scale", "add", "triad"} and all(b > 0 and a > 0 for b, a in times.values())
