@@ -13,7 +13,7 @@ HIPFLAGS := -O3 --offload-arch=$(ARCH) -fPIC -std=c++17 -ffp-contract=off \
 LIB      := hpx_amd/libhpxhip.so
 KSRC     := runtime elementwise reduce scan copy_if sort merge stencil
 KOBJ     := $(KSRC:%=$(BUILD)/csrc/%.o)
-KHDR     := $(wildcard hpx_amd/csrc/*.hpp) include/hpxhip.h
+KHDR     := $(wildcard hpx_amd/csrc/*.hpp) $(wildcard include/hpxhip/kernels/*.hpp) include/hpxhip.h
 
 ORACLE   := oracle/_build/liboracle.so
 OFLAGS   := -O2 -fPIC -std=c++17 -ffp-contract=off -Wall -pthread
@@ -52,7 +52,7 @@ tests/cxx/bin/oracle_sanitize: tests/cxx/oracle_sanitize.cpp oracle/oracle.cpp o
 	$(CXX) $(SANFLAGS) tests/cxx/oracle_sanitize.cpp oracle/oracle.cpp -o $@
 
 # ... and the hipcc-compiled ones (device closures, HPX_HOST_DEVICE lambdas)
-HIPT     := device_closures partitioned_vector
+HIPT     := device_closures partitioned_vector closure_algorithms
 HIPTBIN  := $(HIPT:%=tests/cxx/bin/%)
 HTFLAGS  := -O2 -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-parameter -Iinclude
 

@@ -113,6 +113,8 @@ SIGNATURES = {
     "hpxhip_memcpy_peer_async": [_vp, _i, _vp, _i, _sz, _vp],
     "hpxhip_memset_async": [_vp, _i, _sz, _vp],
     "hpxhip_scratch_bytes": [_i, _i, _i, _u64, ctypes.POINTER(_sz)],
+    "hpxhip_stream_scratch": [_vp, _sz, ctypes.POINTER(_vp)],
+    "hpxhip_device_error_word": [_vp, ctypes.POINTER(_vp)],
     "hpxhip_generate": [_i, _i, _u64, ctypes.c_int64, ctypes.c_int64, _vp, _u64, _vp],
     "hpxhip_generate_at": [_i, _i, _u64, _u64, ctypes.c_int64, ctypes.c_int64, _vp, _u64, _vp],
     "hpxhip_fill": [_i, _vp, _vp, _u64, _vp],

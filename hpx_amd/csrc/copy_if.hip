@@ -13,7 +13,7 @@
 #include <cstdlib>
 
 #include "internal.hpp"
-#include "copy_if_kernel.hpp"
+#include <hpxhip/kernels/copy_if_kernel.hpp>
 
 using namespace hpxhip;
 

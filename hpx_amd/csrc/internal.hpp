@@ -3,7 +3,7 @@
 // cache and the device error word.
 #pragma once
 
-#include "common.hpp"
+#include <hpxhip/kernels/common.hpp>
 #include "../../include/hpxhip.h"
 
 #include <cmath>

@@ -19,158 +19,13 @@
 // sort + merge agree on every dtype.  Traffic: 16 B/key (u64): each input
 // read once, the output written once.
 #include "internal.hpp"
+#include <hpxhip/kernels/merge_kernel.hpp>
 
 using namespace hpxhip;
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kItems = 8;
-constexpr int kTile = kThreads * kItems;
-
-// Number of a-elements among the first d outputs of the stable merge.
-template <typename U, typename X>
-__device__ __forceinline__ uint64_t path_split(const U* a, uint64_t na, const U* b, uint64_t nb, uint64_t d, X xf) {
-    uint64_t lo = d > nb ? d - nb : 0;
-    uint64_t hi = d < na ? d : na;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (xf(a[mid]) <= xf(b[d - mid - 1])) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-
-template <typename U, typename X>
-__global__ __launch_bounds__(256) void k_merge_partition(const U* __restrict__ a, uint64_t na, const U* __restrict__ b,
-                                                          uint64_t nb, uint64_t ntiles, X xf,
-                                                          uint64_t* __restrict__ splits) {
-    const uint64_t t = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
-    if (t > ntiles) return;
-    const uint64_t total = na + nb;
-    const uint64_t d = t * kTile < total ? t * kTile : total;
-    splits[t] = path_split(a, na, b, nb, d, xf);
-}
-
-// Stage src[lo, hi) into dst[0, hi - lo) with aligned 16-B loads.
-template <typename U>
-__device__ __forceinline__ void stage(const U* __restrict__ src, uint64_t lo, uint64_t hi, U* dst) {
-    constexpr int V = 16 / sizeof(U);
-    using VT = vec<U, V>;
-    if (hi <= lo) return;
-    const uint64_t v0 = lo / V, v1 = (hi + V - 1) / V;
-    const VT* vs = reinterpret_cast<const VT*>(src);
-    for (uint64_t v = v0 + threadIdx.x; v < v1; v += kThreads) {
-        const VT x = ld_stream(&vs[v]);
-#pragma unroll
-        for (int e = 0; e < V; ++e) {
-            const uint64_t i = v * V + e;
-            if (i >= lo && i < hi) dst[i - lo] = x.v[e];
-        }
-    }
-}
-
-template <typename U, typename X>
-__global__ __launch_bounds__(kThreads) void k_merge(const U* __restrict__ a, uint64_t na, const U* __restrict__ b,
-                                                     uint64_t nb, const uint64_t* __restrict__ splits, X xf,
-                                                     U* __restrict__ out) {
-    __shared__ U s[kTile];
-    const uint64_t t = blockIdx.x;
-    const uint64_t total = na + nb;
-    const uint64_t d0 = t * kTile;
-    const uint64_t d1 = d0 + kTile < total ? d0 + kTile : total;
-    const uint64_t a0 = splits[t], a1 = splits[t + 1];
-    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
-    const int la = static_cast<int>(a1 - a0), lb = static_cast<int>(b1 - b0);
-    const int len = la + lb;
-    // a and b are 16-B aligned by the host (else the V = 1 instantiation)
-    stage(a, a0, a1, s);
-    stage(b, b0, b1, s + la);
-    __syncthreads();
-
-    const int dk = min(static_cast<int>(threadIdx.x) * kItems, len);
-    int lo = dk > lb ? dk - lb : 0, hi = dk < la ? dk : la;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (xf(s[mid]) <= xf(s[la + dk - mid - 1])) lo = mid + 1;
-        else hi = mid;
-    }
-    int ia = lo, ib = dk - lo;
-    U r[kItems];
-    U va = ia < la ? s[ia] : U(0);
-    U vb = ib < lb ? s[la + ib] : U(0);
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-        const bool takeb = ia >= la || (ib < lb && xf(vb) < xf(va));
-        if (takeb) {
-            r[k] = vb;
-            ++ib;
-            vb = ib < lb ? s[la + ib] : U(0);
-        } else {
-            r[k] = va;
-            ++ia;
-            va = ia < la ? s[ia] : U(0);
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kItems; ++k)
-        if (dk + k < len) s[dk + k] = r[k];
-    __syncthreads();
-
-    constexpr int V = 16 / sizeof(U);
-    using VT = vec<U, V>;
-    if (len == kTile) {
-        VT* vo = reinterpret_cast<VT*>(out + d0);
-        const VT* vsrc = reinterpret_cast<const VT*>(s);
-        for (int v = threadIdx.x; v < kTile / V; v += kThreads) st_stream(&vo[v], vsrc[v]);
-    } else {
-        for (int i = threadIdx.x; i < len; i += kThreads) out[d0 + i] = s[i];
-    }
-}
-
-// Scalar fallback for ranges that are not 16-B aligned: same algorithm,
-// element loads.
-template <typename U, typename X>
-__global__ __launch_bounds__(kThreads) void k_merge_unaligned(const U* __restrict__ a, uint64_t na,
-                                                               const U* __restrict__ b, uint64_t nb,
-                                                               const uint64_t* __restrict__ splits, X xf,
-                                                               U* __restrict__ out) {
-    __shared__ U s[kTile];
-    const uint64_t t = blockIdx.x;
-    const uint64_t total = na + nb;
-    const uint64_t d0 = t * kTile;
-    const uint64_t d1 = d0 + kTile < total ? d0 + kTile : total;
-    const uint64_t a0 = splits[t], a1 = splits[t + 1];
-    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
-    const int la = static_cast<int>(a1 - a0), lb = static_cast<int>(b1 - b0);
-    const int len = la + lb;
-    for (int i = threadIdx.x; i < la; i += kThreads) s[i] = a[a0 + i];
-    for (int i = threadIdx.x; i < lb; i += kThreads) s[la + i] = b[b0 + i];
-    __syncthreads();
-    const int dk = min(static_cast<int>(threadIdx.x) * kItems, len);
-    int lo = dk > lb ? dk - lb : 0, hi = dk < la ? dk : la;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (xf(s[mid]) <= xf(s[la + dk - mid - 1])) lo = mid + 1;
-        else hi = mid;
-    }
-    int ia = lo, ib = dk - lo;
-    U r[kItems];
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-        const bool takeb = ia >= la || (ib < lb && xf(s[la + ib]) < xf(s[ia]));
-        r[k] = takeb ? s[la + (ib < lb ? ib : 0)] : s[ia < la ? ia : 0];
-        if (takeb) ++ib;
-        else ++ia;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kItems; ++k)
-        if (dk + k < len) s[dk + k] = r[k];
-    __syncthreads();
-    for (int i = threadIdx.x; i < len; i += kThreads) out[d0 + i] = s[i];
-}
+using namespace hpxhip::merge_detail;
 
 // out[i] = number of sorted[] elements ordered before values[i]
 // (lower_bound; upper: also those equal to it).
@@ -203,17 +58,18 @@ int run_merge(const void* a, uint64_t na, const void* b, uint64_t nb, void* out,
     uint64_t* splits = static_cast<uint64_t*>(ws);
     const U* ua = static_cast<const U*>(a);
     const U* ub = static_cast<const U*>(b);
-    hipLaunchKernelGGL((k_merge_partition<U, X>), dim3(static_cast<unsigned>((ntiles + 1 + 255) / 256)), dim3(256), 0,
-                       s, ua, na, ub, nb, ntiles, X{}, splits);
+    using C = key_less<X>;
+    hipLaunchKernelGGL((k_merge_partition<U, C>), dim3(static_cast<unsigned>((ntiles + 1 + 255) / 256)), dim3(256), 0,
+                       s, ua, na, ub, nb, ntiles, C{}, splits);
     HPXHIP_CHECK_LAUNCH();
     const bool aligned = (reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
                           reinterpret_cast<uintptr_t>(out)) % 16 == 0;
     if (aligned)
-        hipLaunchKernelGGL((k_merge<U, X>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads), 0, s, ua, na, ub, nb,
-                           splits, X{}, static_cast<U*>(out));
+        hipLaunchKernelGGL((k_merge<U, C, true>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads), 0, s, ua, na, ub,
+                           nb, splits, C{}, static_cast<U*>(out));
     else
-        hipLaunchKernelGGL((k_merge_unaligned<U, X>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads), 0, s, ua, na,
-                           ub, nb, splits, X{}, static_cast<U*>(out));
+        hipLaunchKernelGGL((k_merge<U, C, false>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads), 0, s, ua, na,
+                           ub, nb, splits, C{}, static_cast<U*>(out));
     HPXHIP_CHECK_LAUNCH();
     return 0;
 }

@@ -417,6 +417,20 @@ int hpxhip_memset_async(void* dst, int value, size_t bytes, hpxhip_stream stream
     return static_cast<int>(hipMemsetAsync(dst, value, bytes, reinterpret_cast<hipStream_t>(stream)));
 }
 
+int hpxhip_stream_scratch(hpxhip_stream stream, size_t bytes, void** ptr) {
+    if (!ptr) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    return scratch_get(s, bytes ? bytes : 1, ptr);
+}
+
+int hpxhip_device_error_word(hpxhip_stream stream, uint32_t** word) {
+    if (!word) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    *word = device_error_word(reinterpret_cast<hipStream_t>(stream));
+    return *word ? 0 : HPXHIP_ERROR_OUT_OF_MEMORY;
+}
+
 int hpxhip_scratch_bytes(int algo, int dtype, int aux_dtype, uint64_t n, size_t* bytes) {
     if (!bytes) return HPXHIP_ERROR_INVALID_ARGUMENT;
     if (dtype_size(dtype) == 0) return HPXHIP_ERROR_INVALID_ARGUMENT;

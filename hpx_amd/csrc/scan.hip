@@ -17,8 +17,8 @@
 // Integer results are exact; FP results follow a tree order that can differ
 // from the sequential left fold (tolerance in DESIGN.md).
 #include "internal.hpp"
-#include "lookback.hpp"
-#include "scan_kernel.hpp"
+#include <hpxhip/kernels/lookback.hpp>
+#include <hpxhip/kernels/scan_kernel.hpp>
 
 using namespace hpxhip;
 

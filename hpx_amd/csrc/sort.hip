@@ -40,7 +40,7 @@
 // LDS beside their keys (9216-pair segments): 2^28 u64/u64 pairs 20.7 ->
 // 9.2 ms, 104 instead of 264 B/pair (profiles/r02_sort_by_key_hybrid.log).
 #include "internal.hpp"
-#include "sort_kernel.hpp"
+#include <hpxhip/kernels/sort_kernel.hpp>
 
 #include <algorithm>
 #include <cstdlib>

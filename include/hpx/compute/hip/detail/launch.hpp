@@ -8,8 +8,7 @@
 // <hpx/compute/hip/functional.hpp>); asking it to launch a closure is a
 // compile-time error, never a silent host fallback.
 //
-// HPX_HOST_DEVICE / HPX_DEVICE mirror libs/config/include/hpx/config/
-// compiler_specific.hpp:95-126.
+// HPX_HOST_DEVICE / HPX_DEVICE: <hpx/config/compiler_specific.hpp>.
 #pragma once
 
 #include <hpx/compute/hip.hpp>
@@ -20,24 +19,7 @@
 #include <type_traits>
 #include <utility>
 
-#if defined(__HIPCC__)
-#include <hip/hip_runtime.h>
-#ifndef HPX_HOST_DEVICE
-#define HPX_HOST_DEVICE __host__ __device__
-#endif
-#ifndef HPX_DEVICE
-#define HPX_DEVICE __device__
-#endif
-#define HPX_HAVE_HIP_DEVICE_CLOSURES 1
-#else
-#ifndef HPX_HOST_DEVICE
-#define HPX_HOST_DEVICE
-#endif
-#ifndef HPX_DEVICE
-#define HPX_DEVICE
-#endif
-#define HPX_HAVE_HIP_DEVICE_CLOSURES 0
-#endif
+#include <hpx/config/compiler_specific.hpp>
 
 namespace hpx { namespace compute { namespace hip { namespace detail {
 

@@ -28,6 +28,7 @@
 // the trait to specialise -- never a silent host fallback.
 #pragma once
 
+#include <hpx/config/compiler_specific.hpp>
 #include <hpxhip.h>
 
 #include <functional>
@@ -39,57 +40,57 @@ namespace hpx { namespace compute { namespace hip {
 namespace functional {
 // ---- unary element functors (also callable on the host) -----------------
 struct identity {
-    template <typename T> T operator()(T x) const { return x; }
+    template <typename T> HPX_HOST_DEVICE T operator()(T x) const { return x; }
 };
 template <typename T>
 struct multiply_step {  // stream.cpp:224-237
     using compute_type = T;
     T factor;
-    T operator()(T x) const { return x * factor; }
+    HPX_HOST_DEVICE T operator()(T x) const { return x * factor; }
 };
 template <typename T>
 struct add_value {  // for_each_compute.cu:40 `i += 5`
     using compute_type = T;
     T value;
-    T operator()(T x) const { return x + value; }
+    HPX_HOST_DEVICE T operator()(T x) const { return x + value; }
 };
 template <typename T>
 struct affine {
     using compute_type = T;
     T a, b;
-    T operator()(T x) const { return x * a + b; }
+    HPX_HOST_DEVICE T operator()(T x) const { return x * a + b; }
 };
 struct negate {
-    template <typename T> T operator()(T x) const { return -x; }
+    template <typename T> HPX_HOST_DEVICE T operator()(T x) const { return -x; }
 };
 struct absolute {
-    template <typename T> T operator()(T x) const { return x < T(0) ? -x : x; }
+    template <typename T> HPX_HOST_DEVICE T operator()(T x) const { return x < T(0) ? -x : x; }
 };
 struct square {
-    template <typename T> T operator()(T x) const { return x * x; }
+    template <typename T> HPX_HOST_DEVICE T operator()(T x) const { return x * x; }
 };
 
 // ---- binary element functors ---------------------------------------------
 struct add_step {  // stream.cpp:240-253
-    template <typename T> T operator()(T x, T y) const { return x + y; }
+    template <typename T> HPX_HOST_DEVICE T operator()(T x, T y) const { return x + y; }
 };
 template <typename T>
 struct triad_step {  // stream.cpp:256-271, transform_compute.cu:36
     using compute_type = T;
     T factor;
-    T operator()(T x, T y) const { return x + y * factor; }
+    HPX_HOST_DEVICE T operator()(T x, T y) const { return x + y * factor; }
 };
 struct subtract {
-    template <typename T> T operator()(T x, T y) const { return x - y; }
+    template <typename T> HPX_HOST_DEVICE T operator()(T x, T y) const { return x - y; }
 };
 struct multiply {
-    template <typename T> T operator()(T x, T y) const { return x * y; }
+    template <typename T> HPX_HOST_DEVICE T operator()(T x, T y) const { return x * y; }
 };
 template <typename T>
 struct axpy {
     using compute_type = T;
     T a;
-    T operator()(T x, T y) const { return x * a + y; }
+    HPX_HOST_DEVICE T operator()(T x, T y) const { return x * a + y; }
 };
 
 // ---- for_loop bodies ----------------------------------------------------------
@@ -121,10 +122,10 @@ struct loop_accumulate {
 
 // ---- reduction operators not in <functional> ------------------------------
 struct minimum {
-    template <typename T> T operator()(T x, T y) const { return y < x ? y : x; }
+    template <typename T> HPX_HOST_DEVICE T operator()(T x, T y) const { return y < x ? y : x; }
 };
 struct maximum {
-    template <typename T> T operator()(T x, T y) const { return x < y ? y : x; }
+    template <typename T> HPX_HOST_DEVICE T operator()(T x, T y) const { return x < y ? y : x; }
 };
 
 // ---- predicates -------------------------------------------------------------
@@ -132,7 +133,7 @@ struct maximum {
     template <typename T>                                             \
     struct NAME {                                                     \
         T value;                                                      \
-        bool operator()(T x) const { return EXPR; }                   \
+        HPX_HOST_DEVICE bool operator()(T x) const { return EXPR; }   \
     };
 HPXHIP_PREDICATE(less_than, x < value)
 HPXHIP_PREDICATE(less_equal, x <= value)

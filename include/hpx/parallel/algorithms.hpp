@@ -33,6 +33,7 @@
 #include <hpx/compute/hip/concurrent_executor.hpp>
 #include <hpx/compute/hip/default_executor.hpp>
 #include <hpx/compute/hip/functional.hpp>
+#include <hpx/parallel/detail/device_algorithms.hpp>
 #include <hpx/parallel/detail/device_closures.hpp>
 #include <hpx/parallel/execution.hpp>
 #include <hpx/parallel/segmented_fwd.hpp>
@@ -77,6 +78,24 @@ hip::target const& target_of(P const& p, It const& it) {
 
 template <typename F>
 constexpr bool is_complete_binary = tr::detail::is_complete<tr::binary_t<F>>::value;
+template <typename F>
+constexpr bool is_complete_pred = tr::detail::is_complete<tr::pred_t<F>>::value;
+template <typename F>
+constexpr bool is_complete_compare = tr::detail::is_complete<tr::compare_t<F>>::value;
+// A scan's operator argument: a mapped operator, or any callable op(V, V)
+// (an init value is not callable), inclusive_scan.hpp:288 vs :320.
+template <typename A, typename V>
+constexpr bool is_scan_op = tr::is_binop<A> || std::is_invocable<std::decay_t<A> const&, V const&, V const&>::value;
+
+// Function objects with no mapping to a library operator kind run on kernels
+// instantiated for them (device_algorithms.hpp) -- only in a translation
+// unit compiled by hipcc.
+template <typename F>
+void no_device_mapping(char const*) {
+    static_assert(compute::hip::detail::dependent_false<F>,
+                  "this function object has no mapping to a library operator (traits::unary/binop/pred/compare) "
+                  "-- compile the translation unit with hipcc to run it as a device closure");
+}
 
 template <typename P>
 constexpr bool is_concurrent =
@@ -318,15 +337,24 @@ template <typename P, typename In, typename Out, typename F>
 detail::result_t<P, util::tagged_pair<In, Out>> copy_if(P&& p, In first, In last, Out dest, F&& f) {
     static_assert(detail::is_dev<In> && detail::is_dev<Out>, "copy_if: device iterators required");
     using T = detail::value_t<In>;
-    using Tr = detail::tr::pred_t<F>;
     using R = util::tagged_pair<In, Out>;
     auto const& t = detail::target_of(p, first);
     uint64_t n = detail::distance(first, last);
-    T arg = static_cast<T>(Tr::arg(f));
     auto slot = t.make_result_slot();
-    detail::check(hpxhip_copy_if(detail::dt<T>, Tr::kind, &arg, first.device_ptr(), dest.device_ptr(), n,
-                                 static_cast<uint64_t*>(slot.device()), t.stream(), nullptr, 0),
-                  "copy_if");
+    if constexpr (detail::is_complete_pred<F>) {
+        using Tr = detail::tr::pred_t<F>;
+        T arg = static_cast<T>(Tr::arg(f));
+        detail::check(hpxhip_copy_if(detail::dt<T>, Tr::kind, &arg, first.device_ptr(), dest.device_ptr(), n,
+                                     static_cast<uint64_t*>(slot.device()), t.stream(), nullptr, 0),
+                      "copy_if");
+    } else {
+#if HPX_HAVE_HIP_DEVICE_CLOSURES
+        detail::dev::copy_if(t, static_cast<T const*>(first.device_ptr()), dest.device_ptr(), n, f,
+                             static_cast<uint64_t*>(slot.device()));
+#else
+        detail::no_device_mapping<F>("copy_if");
+#endif
+    }
     detail::fetch_slot(t, slot, 8, "copy_if count");
     return detail::finish_slot<R>(p, t, std::move(slot), [last, dest](unsigned char const* b) {
         uint64_t c;
@@ -434,12 +462,22 @@ result_t<P, T> reduce_impl(P&& p, It first, It last, T init, Op&& op, Conv&& con
     static_assert(is_dev<It>, "reduce: device iterators required");
     using TI = value_t<It>;
     auto const& t = target_of(p, first);
-    T s[2] = {};
-    tr::unary_t<Conv>::scalars(conv, s);
     auto slot = t.make_result_slot();
-    check(hpxhip_transform_reduce(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::unary_t<Conv>::kind, s, &init,
-                                  first.device_ptr(), distance(first, last), slot.device(), t.stream(), nullptr, 0),
-          "transform_reduce");
+    if constexpr (tr::is_binop<Op> && tr::is_unary<Conv>) {
+        T s[2] = {};
+        tr::unary_t<Conv>::scalars(conv, s);
+        check(hpxhip_transform_reduce(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::unary_t<Conv>::kind, s, &init,
+                                      first.device_ptr(), distance(first, last), slot.device(), t.stream(), nullptr,
+                                      0),
+              "transform_reduce");
+    } else {
+#if HPX_HAVE_HIP_DEVICE_CLOSURES
+        dev::reduce<T, false>(t, static_cast<TI const*>(first.device_ptr()), static_cast<TI const*>(nullptr),
+                              distance(first, last), init, op, conv, slot.device());
+#else
+        no_device_mapping<Op>("transform_reduce");
+#endif
+    }
     fetch_slot(t, slot, sizeof(T), "reduce result");
     return finish_slot<T>(p, t, std::move(slot), load_value<T>{});
     }
@@ -462,7 +500,7 @@ detail::result_t<P, detail::value_t<It>> reduce(P&& p, It first, It last) {
 }
 
 template <typename P, typename It, typename T, typename Red, typename Conv,
-          typename = typename std::enable_if<(detail::is_dev<It> || detail::is_seg<It>) && detail::tr::is_unary<Conv>>::type>
+          typename = typename std::enable_if<detail::is_dev<It> || detail::is_seg<It>>::type>
 detail::result_t<P, T> transform_reduce(P&& p, It first, It last, T init, Red&& red, Conv&& conv) {
     return detail::reduce_impl<T>(std::forward<P>(p), first, last, init, std::forward<Red>(red),
                                   std::forward<Conv>(conv));
@@ -475,13 +513,22 @@ result_t<P, T> reduce_binary_impl(P&& p, It1 first1, It1 last1, It2 first2, T in
     using TI = value_t<It1>;
     static_assert(std::is_same<TI, value_t<It2>>::value, "transform_reduce: input element types must match");
     auto const& t = target_of(p, first1);
-    T s[2] = {};
-    tr::binary_t<Comb>::scalars(comb, s);
     auto slot = t.make_result_slot();
-    check(hpxhip_transform_reduce_binary(dt<TI>, dt<T>, tr::binop_t<Red>::kind, tr::binary_t<Comb>::kind, s, &init,
-                                         first1.device_ptr(), first2.device_ptr(), distance(first1, last1),
-                                         slot.device(), t.stream(), nullptr, 0),
-          "transform_reduce");
+    if constexpr (tr::is_binop<Red> && is_complete_binary<Comb>) {
+        T s[2] = {};
+        tr::binary_t<Comb>::scalars(comb, s);
+        check(hpxhip_transform_reduce_binary(dt<TI>, dt<T>, tr::binop_t<Red>::kind, tr::binary_t<Comb>::kind, s,
+                                             &init, first1.device_ptr(), first2.device_ptr(), distance(first1, last1),
+                                             slot.device(), t.stream(), nullptr, 0),
+              "transform_reduce");
+    } else {
+#if HPX_HAVE_HIP_DEVICE_CLOSURES
+        dev::reduce<T, true>(t, static_cast<TI const*>(first1.device_ptr()), static_cast<TI const*>(first2.device_ptr()),
+                             distance(first1, last1), init, red, comb, slot.device());
+#else
+        no_device_mapping<Comb>("transform_reduce");
+#endif
+    }
     fetch_slot(t, slot, sizeof(T), "reduce result");
     return finish_slot<T>(p, t, std::move(slot), load_value<T>{});
 }
@@ -515,12 +562,20 @@ result_t<P, Out> scan_impl(P&& p, In first, In last, Out dest, Op&& op, Conv&& c
     static_assert(std::is_same<V, value_t<Out>>::value, "scan: input and output element types must match");
     auto const& t = target_of(p, first);
     uint64_t n = distance(first, last);
-    V s[2] = {};
-    tr::unary_t<Conv>::scalars(conv, s);
-    V iv = static_cast<V>(init);
-    check(hpxhip_scan(dt<V>, tr::binop_t<Op>::kind, inclusive ? 1 : 0, tr::unary_t<Conv>::kind, s, &iv, nullptr,
-                      first.device_ptr(), dest.device_ptr(), n, t.stream(), nullptr, 0),
-          inclusive ? "inclusive_scan" : "exclusive_scan");
+    if constexpr (tr::is_binop<Op> && tr::is_unary<Conv>) {
+        V s[2] = {};
+        tr::unary_t<Conv>::scalars(conv, s);
+        V iv = static_cast<V>(init);
+        check(hpxhip_scan(dt<V>, tr::binop_t<Op>::kind, inclusive ? 1 : 0, tr::unary_t<Conv>::kind, s, &iv, nullptr,
+                          first.device_ptr(), dest.device_ptr(), n, t.stream(), nullptr, 0),
+              inclusive ? "inclusive_scan" : "exclusive_scan");
+    } else {
+#if HPX_HAVE_HIP_DEVICE_CLOSURES
+        dev::scan(t, static_cast<V const*>(first.device_ptr()), dest.device_ptr(), n, op, conv, init, inclusive);
+#else
+        no_device_mapping<Op>(inclusive ? "inclusive_scan" : "exclusive_scan");
+#endif
+    }
     Out end = dest + static_cast<std::ptrdiff_t>(n);
     return finish<Out>(p, t, [end] { return end; });
     }
@@ -531,7 +586,7 @@ using ident = hpx::compute::hip::functional::identity;
 // inclusive_scan.hpp:288 (op, init) and :320 (init, op)
 template <typename P, typename In, typename Out, typename A, typename B>
 detail::result_t<P, Out> inclusive_scan(P&& p, In first, In last, Out dest, A&& a, B&& b) {
-    if constexpr (detail::tr::is_binop<A>)
+    if constexpr (detail::is_scan_op<A, detail::value_t<In>>)
         return detail::scan_impl(std::forward<P>(p), first, last, dest, std::forward<A>(a), detail::ident{}, b, true);
     else
         return detail::scan_impl(std::forward<P>(p), first, last, dest, std::forward<B>(b), detail::ident{}, a, true);
@@ -540,7 +595,7 @@ detail::result_t<P, Out> inclusive_scan(P&& p, In first, In last, Out dest, A&& 
 template <typename P, typename In, typename Out, typename A>
 detail::result_t<P, Out> inclusive_scan(P&& p, In first, In last, Out dest, A&& a) {
     using V = detail::value_t<In>;
-    if constexpr (detail::tr::is_binop<A>)
+    if constexpr (detail::is_scan_op<A, V>)
         return detail::scan_impl(std::forward<P>(p), first, last, dest, std::forward<A>(a), detail::ident{}, V(), true);
     else
         return detail::scan_impl(std::forward<P>(p), first, last, dest, std::plus<V>(), detail::ident{}, a, true);
@@ -583,24 +638,37 @@ detail::result_t<P, Out> transform_exclusive_scan(P&& p, In first, In last, Out 
 }
 
 // ------------------------------------------------------------------- sort
-template <typename P, typename It, typename Comp = std::less<>>
-detail::result_t<P, It> sort(P&& p, It first, It last, Comp&& = Comp()) {
-    static_assert(detail::is_dev<It>, "sort: device iterators required");
+// sort.hpp:364 sort(policy, first, last, comp = less, proj = identity):
+// std::less / std::greater on the elements themselves take the radix sort
+// (hpxhip_sort); any other comparator or projection a comparison merge sort
+// instantiated for it (hipcc translation units, device_algorithms.hpp).
+template <typename P, typename It, typename Comp = std::less<>, typename Proj = util::projection_identity,
+          typename = std::enable_if_t<detail::is_dev<It>>>
+detail::result_t<P, It> sort(P&& p, It first, It last, Comp&& comp = Comp(), Proj&& proj = Proj()) {
     using T = detail::value_t<It>;
     auto const& t = detail::target_of(p, first);
-    detail::check(hpxhip_sort(detail::dt<T>, first.device_ptr(), detail::distance(first, last),
-                              detail::tr::compare_t<Comp>::descending ? 1 : 0, t.stream(), nullptr, 0),
-                  "sort");
+    uint64_t n = detail::distance(first, last);
+    if constexpr (detail::is_complete_compare<Comp> &&
+                  std::is_same<std::decay_t<Proj>, util::projection_identity>::value) {
+        detail::check(hpxhip_sort(detail::dt<T>, first.device_ptr(), n,
+                                  detail::tr::compare_t<Comp>::descending ? 1 : 0, t.stream(), nullptr, 0),
+                      "sort");
+    } else {
+#if HPX_HAVE_HIP_DEVICE_CLOSURES
+        detail::dev::merge_sort(t, first.device_ptr(), n, comp, proj);
+#else
+        detail::no_device_mapping<Comp>("sort");
+#endif
+    }
     return detail::finish<It>(p, t, [last] { return last; });
 }
 
-// container_algorithms/sort.hpp:102: sort(policy, rng[, comp]) over
-// begin(rng), end(rng) (projections: the identity only -- the radix sort
-// orders by the keys' own bits).
-template <typename P, typename Rng, typename Comp = std::less<>,
+// container_algorithms/sort.hpp:102: sort(policy, rng[, comp[, proj]]) over
+// begin(rng), end(rng).
+template <typename P, typename Rng, typename Comp = std::less<>, typename Proj = util::projection_identity,
           typename = std::enable_if_t<detail::is_dev<decltype(std::declval<Rng&>().begin())>>>
-auto sort(P&& p, Rng&& rng, Comp&& comp = Comp()) {
-    return sort(std::forward<P>(p), rng.begin(), rng.end(), std::forward<Comp>(comp));
+auto sort(P&& p, Rng&& rng, Comp&& comp = Comp(), Proj&& proj = Proj()) {
+    return sort(std::forward<P>(p), rng.begin(), rng.end(), std::forward<Comp>(comp), std::forward<Proj>(proj));
 }
 
 // is_sorted.hpp:40-120: no adjacent pair ordered after one another under

@@ -13,6 +13,7 @@
 #pragma once
 
 #include <hpx/compute/hip.hpp>
+#include <hpx/config/compiler_specific.hpp>
 
 #include <cstddef>
 #include <type_traits>
@@ -145,6 +146,15 @@ struct algorithm_result {
 // hpx::util::tagged_pair / tagged_tuple results of copy, transform, copy_if,
 // sort_by_key (hpx/util/tagged_pair.hpp); accessors named by the tags.
 namespace util {
+// hpx/parallel/util/projection_identity.hpp: the default projection of the
+// algorithms that take one (sort.hpp:364).
+struct projection_identity {
+    template <typename T>
+    HPX_HOST_DEVICE constexpr T operator()(T v) const {
+        return v;
+    }
+};
+
 template <typename A, typename B>
 struct tagged_pair {
     A first;

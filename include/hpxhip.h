@@ -202,6 +202,17 @@ int hpxhip_memset_async(void* dst, int value, size_t bytes, hpxhip_stream stream
    value dtype is passed in `aux_dtype`, else ignored). */
 int hpxhip_scratch_bytes(int algo, int dtype, int aux_dtype, uint64_t n, size_t* bytes);
 
+/* The per-stream scratch cache itself (>= bytes of device memory, reused by
+   later calls on the same stream, so valid for stream-ordered work queued
+   before the next call that takes scratch on that stream), and the device
+   error word the look-back kernels raise a bounded-spin timeout in.  For
+   kernels instantiated outside the library -- the C++ layer's device
+   closures (hpx/parallel/detail/device_algorithms.hpp), which run the same
+   kernel bodies (include/hpxhip/kernels/) with user callables.  No reference
+   counterpart: cuda::target's per-target scratch lives in the CUDA runtime. */
+int hpxhip_stream_scratch(hpxhip_stream stream, size_t bytes, void** ptr);
+int hpxhip_device_error_word(hpxhip_stream stream, uint32_t** word);
+
 /* Scratch convention for every algorithm below: pass (NULL, 0) to let the
    library use a per-stream cached buffer (grown with hipMalloc, so not
    graph-capturable); or pass a caller-owned device buffer of at least

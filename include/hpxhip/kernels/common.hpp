@@ -91,6 +91,35 @@ struct op_bit_xor {
 };
 
 // ---------------------------------------------------------------------------
+// opt<T>: a value or "no value".  A user operator (a device closure of the
+// C++ layer) has no known identity, but every GPU tree and scan pads
+// inactive lanes with one: lifted_op makes "no value" that identity, so the
+// kernels run any associative operator unchanged (reduce_kernel.hpp,
+// scan_kernel.hpp; hpx/parallel/detail/device_algorithms.hpp).
+template <typename T>
+struct opt {
+    T v;
+    uint32_t ok;
+};
+template <typename T>
+__host__ __device__ __forceinline__ T unwrap_value(T x) { return x; }
+template <typename T>
+__host__ __device__ __forceinline__ T unwrap_value(opt<T> x) { return x.v; }
+
+template <typename F>
+struct lifted_op {
+    F f;
+    template <typename X>
+    __device__ __forceinline__ X operator()(X a, X b) const {
+        if (!a.ok) return b;
+        if (!b.ok) return a;
+        return X{f(a.v, b.v), 1u};
+    }
+    template <typename X>
+    __host__ __device__ static constexpr X identity() { return X{}; }
+};
+
+// ---------------------------------------------------------------------------
 // 16-byte vector of T (one `global_load_dwordx4` per lane).
 template <typename T, int N>
 struct alignas(sizeof(T) * N) vec {
@@ -188,7 +217,7 @@ struct ordered_bits {
 // Bit casts between T and 32-bit lanes (DPP moves 32 bits per lane).
 template <typename T>
 __device__ __forceinline__ void to_words(T x, uint32_t (&w)[(sizeof(T) + 3) / 4]) {
-    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4/8-byte types only");
+    static_assert(sizeof(T) % 4 == 0 && sizeof(T) <= 32, "whole 32-bit words only");
     __builtin_memcpy(w, &x, sizeof(T));
 }
 template <typename T>

@@ -3,8 +3,8 @@
 // instantiates exactly the shipped kernel with other tile shapes.
 #pragma once
 
-#include "common.hpp"
-#include "lookback.hpp"
+#include <hpxhip/kernels/common.hpp>
+#include <hpxhip/kernels/lookback.hpp>
 
 namespace hpxhip {
 namespace copy_if_detail {

@@ -38,7 +38,7 @@
 // bounded (kSpinLimit) and raises the device error word.
 #pragma once
 
-#include "common.hpp"
+#include <hpxhip/kernels/common.hpp>
 
 namespace hpxhip {
 
@@ -46,8 +46,8 @@ enum : uint32_t { TILE_INVALID = 0, TILE_AGGREGATE = 1, TILE_INCLUSIVE = 2 };
 
 template <typename T>
 struct tile_state {
-    static constexpr int G = sizeof(T) / 4;  // granules per value (1 or 2)
-    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4/8-byte tile values only");
+    static constexpr int G = sizeof(T) / 4;  // granules per value (1 or 2; up to 8 for opt<T> values)
+    static_assert(sizeof(T) % 4 == 0 && sizeof(T) <= 32, "tile values of whole 32-bit words");
 
     uint64_t* slots;  // [ntiles][2 (aggregate, inclusive)][G]
     uint32_t* err;    // device error word (may be null)

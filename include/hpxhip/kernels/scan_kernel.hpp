@@ -3,8 +3,8 @@
 // instantiate exactly the shipped kernel with other tile shapes.
 #pragma once
 
-#include "common.hpp"
-#include "lookback.hpp"
+#include <hpxhip/kernels/common.hpp>
+#include <hpxhip/kernels/lookback.hpp>
 
 namespace hpxhip {
 namespace scan_detail {
@@ -73,11 +73,14 @@ __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& 
     if (lane < WAVES) s_wave_total[lane] = op(p, wex);
 }
 
+// T: element type of in/out; X: the scanned value type (T for the built-in
+// operators; opt<T> for a user operator without an identity, the C++
+// layer's device closures): conv maps T -> X, unwrap_value X -> T.
 template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED, int ROUNDS = kRounds,
           int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false, int LBK = 1,
-          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = true>
-__global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init,
-                                                   const T* prefix_dev, uint32_t* counter, tile_state<T> st) {
+          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = true, typename X = T>
+__global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, X init,
+                                                   const X* prefix_dev, uint32_t* counter, tile_state<X> st) {
     constexpr int V = 16 / sizeof(T);
     constexpr int WAVES = THREADS / kWave;
     constexpr uint64_t TILE = tile_elems<T, ROUNDS, THREADS>();
@@ -85,7 +88,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
     using VT = vec<T, V>;
 
     __shared__ uint32_t s_tile;
-    __shared__ T s_wave_total[WAVES];
+    __shared__ X s_wave_total[WAVES];
 
     if constexpr (DYN_ID) {
         if (threadIdx.x == 0)
@@ -95,29 +98,30 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
     const uint64_t tile = DYN_ID ? s_tile : blockIdx.x;
     const int wave = threadIdx.x / kWave;
     const int lane = lane_id();
-    const T id = Op::template identity<T>();
+    const X id = Op::template identity<X>();
 
     const uint64_t tile_base = tile * TILE;
     const uint64_t wbase = tile_base + wave * WAVE_ELEMS;
     const bool full = tile_base + TILE <= n;
 
     // ---- load (all rounds in flight) and convert
-    VT x[ROUNDS];
+    X x[ROUNDS][V];
     if (ALIGNED && full) {
         const VT* src = reinterpret_cast<const VT*>(in + wbase);
+        VT raw[ROUNDS];
 #pragma unroll
-        for (int r = 0; r < ROUNDS; ++r) x[r] = ld_stream(&src[r * kWave + lane]);
+        for (int r = 0; r < ROUNDS; ++r) raw[r] = ld_stream(&src[r * kWave + lane]);
 #pragma unroll
         for (int r = 0; r < ROUNDS; ++r)
 #pragma unroll
-            for (int e = 0; e < V; ++e) x[r].v[e] = conv(x[r].v[e]);
+            for (int e = 0; e < V; ++e) x[r][e] = conv(raw[r].v[e]);
     } else {
 #pragma unroll
         for (int r = 0; r < ROUNDS; ++r)
 #pragma unroll
             for (int e = 0; e < V; ++e) {
                 const uint64_t i = wbase + (static_cast<uint64_t>(r) * kWave + lane) * V + e;
-                x[r].v[e] = i < n ? conv(in[i]) : id;
+                x[r][e] = i < n ? conv(in[i]) : id;
             }
     }
 
@@ -127,43 +131,43 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
     // rounds.  Measured slower at every tile shape (2.91-2.95 ms vs 2.82-2.84
     // for 2^30 int64, profiles/r01_ubench_scan_early_agg.log): not shipped.
     if constexpr (EARLY) {
-        T lt = id;
+        X lt = id;
 #pragma unroll
         for (int r = 0; r < ROUNDS; ++r)
 #pragma unroll
-            for (int e = 0; e < V; ++e) lt = op(lt, x[r].v[e]);
-        const T wt = wave_reduce(lt, op);
+            for (int e = 0; e < V; ++e) lt = op(lt, x[r][e]);
+        const X wt = wave_reduce(lt, op);
         if (lane == 0) s_wave_total[wave] = wt;
         __syncthreads();
-        if (wave == 0) tile_prefix<T, Op, WAVES, LOOKBACK, LBK>(tile, st, op, prefix_dev, init, s_wave_total);
+        if (wave == 0) tile_prefix<X, Op, WAVES, LOOKBACK, LBK>(tile, st, op, prefix_dev, init, s_wave_total);
     }
 
     // ---- per-round lane scan + wave scan; x becomes the wave-local result
-    T carry = id;
+    X carry = id;
 #pragma unroll
     for (int r = 0; r < ROUNDS; ++r) {
-        T local[V];
-        T run = id;
+        X local[V];
+        X run = id;
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-            const T nxt = op(run, x[r].v[e]);
+            const X nxt = op(run, x[r][e]);
             local[e] = INCL ? nxt : run;
             run = nxt;
         }
-        const T incl = wave_inclusive_scan(run, op);
-        const T excl = wave_shift_right<T, Op>(incl);
-        const T pre = op(carry, excl);
+        const X incl = wave_inclusive_scan(run, op);
+        const X excl = wave_shift_right<X, Op>(incl);
+        const X pre = op(carry, excl);
 #pragma unroll
-        for (int e = 0; e < V; ++e) x[r].v[e] = op(pre, local[e]);
+        for (int e = 0; e < V; ++e) x[r][e] = op(pre, local[e]);
         carry = op(carry, readlane(incl, kWave - 1));
     }
     if constexpr (!EARLY) {
         if (lane == 0) s_wave_total[wave] = carry;
         __syncthreads();
-        if (wave == 0) tile_prefix<T, Op, WAVES, LOOKBACK, LBK>(tile, st, op, prefix_dev, init, s_wave_total);
+        if (wave == 0) tile_prefix<X, Op, WAVES, LOOKBACK, LBK>(tile, st, op, prefix_dev, init, s_wave_total);
     }
     __syncthreads();
-    const T pre = s_wave_total[wave];
+    const X pre = s_wave_total[wave];
 
     // ---- store
     if (ALIGNED && full) {
@@ -172,7 +176,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
         for (int r = 0; r < ROUNDS; ++r) {
             VT y;
 #pragma unroll
-            for (int e = 0; e < V; ++e) y.v[e] = op(pre, x[r].v[e]);
+            for (int e = 0; e < V; ++e) y.v[e] = unwrap_value(op(pre, x[r][e]));
             if constexpr (NT_STORE) st_stream(&dst[r * kWave + lane], y);
             else dst[r * kWave + lane] = y;
         }
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
 #pragma unroll
             for (int e = 0; e < V; ++e) {
                 const uint64_t i = wbase + (static_cast<uint64_t>(r) * kWave + lane) * V + e;
-                if (i < n) out[i] = op(pre, x[r].v[e]);
+                if (i < n) out[i] = unwrap_value(op(pre, x[r][e]));
             }
     }
 }

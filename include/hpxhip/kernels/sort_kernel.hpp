@@ -3,7 +3,7 @@
 // shipped kernels with other tile shapes.
 #pragma once
 
-#include "common.hpp"
+#include <hpxhip/kernels/common.hpp>
 
 namespace hpxhip {
 namespace sort_detail {

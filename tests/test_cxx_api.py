@@ -50,6 +50,26 @@ void f(hpx::compute::vector<double>& a, hpx::compute::vector<double>& b) {
     assert r.returncode == 0, r.stderr
 
 
+def test_closure_algorithms_need_hipcc():
+    """A lambda conv / op / pred / comp in a host-compiled TU is rejected at
+    compile time with the way out named (no host fallback)."""
+    for call in ("hpx::parallel::transform_reduce(p, a.begin(), a.end(), 0, std::plus<>(), [](int x) { return x * 2; });",
+                 "hpx::parallel::reduce(p, a.begin(), a.end(), 0, [](int x, int y) { return x + y; });",
+                 "hpx::parallel::inclusive_scan(p, a.begin(), a.end(), a.begin(), [](int x, int y) { return x + y; });",
+                 "hpx::parallel::copy_if(p, a.begin(), a.end(), a.begin(), [](int x) { return x > 0; });",
+                 "hpx::parallel::sort(p, a.begin(), a.end(), [](int x, int y) { return x > y; });"):
+        r = _compile(f"""
+#include <hpx/hpx.hpp>
+void f(hpx::compute::vector<int>& a) {{
+    hpx::compute::hip::default_executor exec;
+    auto p = hpx::parallel::execution::par.on(exec);
+    {call}
+}}
+""")
+        assert r.returncode != 0, call
+        assert "compile the translation unit with hipcc" in r.stderr, (call, r.stderr[-2000:])
+
+
 def test_unmapped_functor_is_a_compile_error():
     r = _compile("""
 #include <hpx/hpx.hpp>
@@ -68,6 +88,8 @@ void f(hpx::compute::vector<int>& a) {
     ("stream_hip", ["--vector_size", str(1 << 26), "--iterations", "10"]),
     ("for_loop_merge", []),
     ("device_closures", ["4242"]),
+    ("closure_algorithms", ["777"]),
+    ("closure_algorithms", ["778", "--big"]),
     ("partitioned_vector", []),
     ("stencil_partitioned", []),
     ("call_overhead", []),
