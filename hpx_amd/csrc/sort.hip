@@ -71,7 +71,7 @@ struct tile_shape {
 
 struct sort_layout {
     uint64_t ntiles;
-    size_t alt_keys, alt_vals, hist, xhist, bits, start, xstart, bounds, segs, counter, lb, lb_bytes, total;
+    size_t alt_keys, alt_vals, hist, xhist, bits, start, xstart, bounds, ctl, counter, lb, lb_bytes, total;
     bool wide;  // 64-bit granules
 };
 
@@ -94,11 +94,11 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     off += 8 * kRadix * 8;
     L.xstart = off;
     off += kXBins * 8;
-    L.bounds = off;  // hybrid: bucket bounds (up to 2^17 + 1) and segment (begin, end) pairs
+    L.bounds = off;  // hybrid: bucket bounds (up to 2^17 + 1)
     off = align_up(off + 8 * (kMaxBuckets + 1), 256);
-    L.segs = off;
-    off = align_up(off + 16 * kMaxBuckets, 256);
-    L.counter = off;  // counter (16 B) immediately followed by lb: one memset
+    L.ctl = off;  // the device-side plan (ctl words below)
+    off += 256;
+    L.counter = off;  // counter (16 B) immediately followed by lb: one zero fill per pass
     off += 256;
     L.lb = off;
     L.lb_bytes = L.ntiles * kXBins * (L.wide ? 8 : 4);  // room for a 9-bit pass
@@ -107,30 +107,29 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     return L;
 }
 
-// Hybrid tail (keys-only sorts of at least 2^22 keys whose bucket
-// sizes, estimated from the prefix fields' histograms, fit the LDS):
+// Hybrid tail (keys-only sorts and pairs of at least 2^22 elements whose
+// bucket sizes, estimated from the prefix fields' histograms, fit the LDS):
 //   17-bit prefix (top byte + the 9 bits under it): segments of <= 9216 keys
 //     sorted by 512-thread workgroups, two per CU, so one workgroup's loads
 //     and stores overlap the other's LDS passes (7.2 vs 9.7 ms for the
 //     segment sort at 2^30, profiles/r02_ubench_segment_sort.log);
-//   16-bit prefix (the two top live bytes): segments of <= 18432 keys, one
-//     1024-thread workgroup per CU -- for buckets too large for the first
-//     form (more than ~2^30.1 random keys) or top bytes that are constant.
+//   16-bit prefix (the two top live bytes): the same 512-thread segments, or
+//     1024-thread segments of <= 18432 keys (one workgroup per CU) for
+//     buckets too large for both -- e.g. top bytes that are constant.
 // HPXHIP_SORT_HYBRID=0 / 16 turns the hybrid / its 17-bit form off (tests,
 // ablations).
 constexpr int kSegThreads16 = 1024, kSegThreads17 = 512, kSegItems = 18;
 constexpr uint64_t kCap16 = static_cast<uint64_t>(kSegThreads16) * kSegItems;
 constexpr uint64_t kCap17 = static_cast<uint64_t>(kSegThreads17) * kSegItems;
-// sort_by_key (64-bit keys): the 16-bit form with the values staged beside
-// the keys, segments of <= 1024 x 9 pairs (144 KiB of LDS with 8-B values,
-// one workgroup per CU); buckets fit up to about 2^29 random pairs.
+// sort_by_key: the 16-bit form with the values staged beside the keys,
+// segments of <= 1024 x 9 pairs (144 KiB of LDS with 8-B values, one
+// workgroup per CU).
 constexpr int kSegItemsKV = 9;
 constexpr uint64_t kCapKV = static_cast<uint64_t>(kSegThreads16) * kSegItemsKV;
 // the 9-bit field under the top byte: bits [47, 56) of a 64-bit key, [15, 24) of a 32-bit one
 template <typename U>
 constexpr int field17_shift() { return static_cast<int>(8 * sizeof(U)) - 17; }
 constexpr uint64_t kHybridMin = 1ull << 22;
-constexpr size_t kMaxBigBuckets = 64;  // more oversized buckets than this -> finish as plain LSD
 
 int hybrid_mode() {
     const char* e = std::getenv("HPXHIP_SORT_HYBRID");
@@ -138,14 +137,165 @@ int hybrid_mode() {
     return std::atoi(e);
 }
 
-// HPXHIP_SORT_DIRECT=<d>: take the per-bucket segment sort when the average
-// bucket holds at least 1/d of a segment (default 2; ablations).
-double direct_divisor() {
-    const char* e = std::getenv("HPXHIP_SORT_DIRECT");
-    return e ? std::atof(e) : 2.0;
+// ---------------------------------------------------------------- the plan
+// The sort is planned ON THE DEVICE: the host enqueues one fixed sequence of
+// kernels for (dtype, n, keys / pairs) and every kernel reads its part of
+// the plan from these words and returns at once when the plan does not take
+// it.  So no histogram, bucket bound or oversized flag travels to the host,
+// the call returns as soon as the work is enqueued (sort.hpp:251-276 returns
+// a future under task policies), and a sort can be captured in a graph.
+enum : int {
+    C_A9 = 0,          // shift of the 9-bit prefix pass (17-bit form), -1 = not run
+    C_A8 = 1,          // shift of the second-byte prefix pass (16-bit form), -1
+    C_B = 2,           // shift of the top-byte prefix pass, -1
+    C_LSD = 3,         // [3, 11): LSD pass shifts, least significant first, -1
+    C_BOUNDS = 11,     // {on, nb, s1, s2, b2} of k_bucket_bounds
+    C_SEGA = 16,       // {on, nb, top_single}: 512-thread segment sort (keys) / the pairs kernel
+    C_SEGB = 19,       // {on, nb, top_single}: 1024-thread segment sort (keys, buckets over 9216)
+    C_OVERSIZED = 22,  // raised by a segment sort: a bucket over its LDS capacity
+    C_HIST_A = 23,     // count digits [0, first) before the prefix passes
+    C_HIST_B = 24,     // ... after a hybrid that fell back to the LSD
+    C_COPY = 25,       // the LSD ended in the alternate buffer: copy back
+    C_PENDING = 26,    // stage 0 needs the second live byte's histogram to decide
+    C_NLSD = 27,       // live digits
+    C_DIGITS = 28,     // [28, 36): live digits, least significant first
+    C_FIRST = 36,      // the first histogram counted digits [first, passes)
+    C_WORDS = 40
+};
+static_assert(C_WORDS * 4 <= 256, "plan words fit their slot");
+
+// A bucket whose estimated size exceeds this fraction of its segment's LDS
+// capacity is not planned (a bucket over the capacity sends the whole sort to
+// the LSD); the estimate is (largest top-byte bin) x (largest field bin) / n.
+constexpr double kFit = 0.8;
+
+__device__ inline int top_bit_d(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
+// Planner, one thread.  stage 0 runs on the first histogram (the two top
+// digits and the 9-bit field under the top byte; every digit for small
+// sorts); stage 1 (after the gated count of the remaining digits) decides a
+// plan stage 0 left pending.
+//   17-bit form: the top two digits live, the 9-bit field's histogram known:
+//     prefix passes on the 9-bit field then the top byte, buckets = top byte +
+//     the top b2 <= 9 bits of the field, b2 the smallest whose estimated
+//     largest bucket fits a 512-thread segment (two workgroups per CU);
+//   16-bit form (pairs, or keys the 17-bit form does not fit): prefix passes
+//     on the two top live bytes, b2 <= 8, a 512-thread (keys) / pairs
+//     segment, or the 1024-thread keys segment for b2 = 8 buckets over 9216;
+//   otherwise the LSD over the live digits.
+__global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const unsigned long long* __restrict__ xhist,
+                            const unsigned long long* __restrict__ bits, uint64_t n, int passes, int first, int mode,
+                            int has_val, int stage, int32_t* __restrict__ ctl) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (stage == 1) {
+        if (!ctl[C_PENDING]) return;
+        first = 0;  // every digit is counted now
+    } else {
+        for (int i = 0; i < C_WORDS; ++i) ctl[i] = 0;
+        for (int i = 0; i < 11; ++i) ctl[i] = -1;
+        ctl[C_FIRST] = first;
+    }
+    ctl[C_PENDING] = 0;
+    const uint64_t diff = bits[0] ^ bits[1];
+    int live[8], nl = 0;
+    for (int p = passes - 1; p >= 0; --p)
+        if ((diff >> (8 * p)) & 0xffu) live[nl++] = p;
+    ctl[C_NLSD] = nl;
+    for (int i = 0; i < nl; ++i) ctl[C_DIGITS + i] = live[nl - 1 - i];
+    auto lsd = [&] {
+        for (int i = 0; i < nl; ++i) ctl[C_LSD + i] = 8 * live[nl - 1 - i];
+        ctl[C_COPY] = nl & 1;
+        if (stage == 0) ctl[C_HIST_A] = first > 0;
+    };
+    if (mode == 0 || nl < 3) return lsd();
+    const double dn = static_cast<double>(n);
+    auto bin_max = [](const unsigned long long* c, int bins, int group) {
+        unsigned long long m = 0;
+        for (int g = 0; g < bins; g += group) {
+            unsigned long long sum = 0;
+            for (int j = 0; j < group; ++j) sum += c[g + j];
+            m = sum > m ? sum : m;
+        }
+        return static_cast<double>(m);
+    };
+    auto plan = [&](int s1, int s2, int b2, int seg) {
+        const uint32_t nb = 256u << b2;
+        ctl[C_BOUNDS + 0] = 1;
+        ctl[C_BOUNDS + 1] = static_cast<int32_t>(nb);
+        ctl[C_BOUNDS + 2] = s1;
+        ctl[C_BOUNDS + 3] = s2;
+        ctl[C_BOUNDS + 4] = b2;
+        ctl[seg + 0] = 1;
+        ctl[seg + 1] = static_cast<int32_t>(nb);
+        ctl[seg + 2] = top_bit_d(diff & ((uint64_t(1) << s2) - 1));
+    };
+    const bool top_two = live[0] == passes - 1 && live[1] == passes - 2;
+    if (mode == 17 && !has_val && first > 0 && top_two) {
+        const double m_top = bin_max(hist + live[0] * kRadix, kRadix, 1);
+        const int fs = 8 * passes - 17;
+        for (int b2 = 1; b2 <= 9; ++b2)
+            if (m_top * bin_max(xhist, kXBins, 1 << (9 - b2)) / dn <= kFit * kCap17) {
+                ctl[C_A9] = fs;
+                ctl[C_B] = 8 * live[0];
+                return plan(8 * live[0], fs + 9 - b2, b2, C_SEGA);
+            }
+    }
+    if (mode >= 16) {
+        if (live[1] < first) {  // the second live byte was not counted: decide after the full count
+            ctl[C_PENDING] = 1;
+            ctl[C_HIST_A] = 1;
+            return;
+        }
+        const double m_top = bin_max(hist + live[0] * kRadix, kRadix, 1);
+        const unsigned long long* h2 = hist + live[1] * kRadix;
+        for (int b2 = 1; b2 <= 8; ++b2)
+            if (m_top * bin_max(h2, kRadix, 1 << (8 - b2)) / dn <= kFit * (has_val ? kCapKV : kCap17)) {
+                ctl[C_A8] = 8 * live[1];
+                ctl[C_B] = 8 * live[0];
+                return plan(8 * live[0], 8 * live[1] + 8 - b2, b2, C_SEGA);
+            }
+        if (!has_val && m_top * bin_max(h2, kRadix, 1) / dn <= kFit * kCap16) {
+            ctl[C_A8] = 8 * live[1];
+            ctl[C_B] = 8 * live[0];
+            return plan(8 * live[0], 8 * live[1], 8, C_SEGB);
+        }
+    }
+    lsd();
 }
 
-inline int top_bit(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
+// After the segment sorts: a bucket over its LDS capacity (skewed keys) left
+// its keys unsorted -- the plan switches to the LSD over every live digit,
+// which sorts the prefix-ordered array from where it is (a permutation of
+// the input: same digit counts).
+__global__ void k_sort_fallback(int32_t* __restrict__ ctl) {
+    if (threadIdx.x != 0 || blockIdx.x != 0 || ctl[C_OVERSIZED] == 0) return;
+    const int nl = ctl[C_NLSD];
+    for (int i = 0; i < nl; ++i) ctl[C_LSD + i] = 8 * ctl[C_DIGITS + i];
+    ctl[C_COPY] = nl & 1;
+    ctl[C_HIST_B] = ctl[C_FIRST] > 0 && !ctl[C_HIST_A];
+}
+
+// Zero fill of a pass's look-back state, run iff *gate >= 0 (the pass runs).
+__global__ __launch_bounds__(256) void k_zero_gated(uint4* __restrict__ p, uint64_t n16, const int32_t* __restrict__ gate) {
+    if (*gate < 0) return;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n16; i += stride)
+        p[i] = make_uint4(0, 0, 0, 0);
+}
+
+// dst[0, n) = src[0, n), run iff *gate != 0.
+template <typename E>
+__global__ __launch_bounds__(256) void k_copy_gated(const E* __restrict__ src, E* __restrict__ dst, uint64_t n,
+                                                     const int32_t* __restrict__ gate) {
+    if (*gate == 0) return;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+
+inline unsigned grid_for(uint64_t items, uint64_t cap = 8192) {
+    const uint64_t g = (items + 255) / 256;
+    return static_cast<unsigned>(g < 1 ? 1 : (g > cap ? cap : g));
+}
 
 template <typename T, bool DESC, typename VAL, bool HAS_VAL>
 int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, size_t scratch_bytes) {
@@ -161,40 +311,46 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     auto* xhist = reinterpret_cast<unsigned long long*>(base + L.xhist);
     auto* start = reinterpret_cast<unsigned long long*>(base + L.start);
     auto* xstart = reinterpret_cast<unsigned long long*>(base + L.xstart);
+    auto* bits = reinterpret_cast<unsigned long long*>(base + L.bits);
+    auto* bounds = reinterpret_cast<uint64_t*>(base + L.bounds);
+    auto* ctl = reinterpret_cast<int32_t*>(base + L.ctl);
     uint32_t* counter = reinterpret_cast<uint32_t*>(base + L.counter);
     uint32_t* err = device_error_word(s);
     const int passes = static_cast<int>(sizeof(U));
     const unsigned hist_grid = static_cast<unsigned>(current_device_info().cus * kHistBlocksPerCU);
     constexpr int kField17Shift = field17_shift<U>();
-    // 32-bit keys: the two LDS passes under a 16/17-bit prefix sort a single
-    // bucket's whole key (no odd-even rounds)
     int mode = n >= kHybridMin ? hybrid_mode() : 0;
     if (HAS_VAL && mode > 16) mode = 16;  // no 9-bit pass with values
+    // a sort that may take the hybrid counts only the two top digits (and the
+    // 9-bit field under the top byte) first -- the LDS atomics, not the read,
+    // bound k_hist -- and the rest only when the plan needs them
+    const int first = mode ? passes - 2 : 0;
+    const bool xfield = mode == 17;
 
-    auto* bits = reinterpret_cast<unsigned long long*>(base + L.bits);
-    // histograms of digits [first, passes) of keys[0, cnt) -> hist, their
-    // exclusive bin starts -> start, OR / AND of the keys -> bits; with
-    // xfield, also the 9-bit field under the top byte -> xhist / xstart
-    auto histogram = [&](const U* k, uint64_t cnt, int first, bool xfield) -> int {
-        HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8 + kXBins * 8, s));  // hist and xhist
-        HPXHIP_CHECK(hipMemsetAsync(bits, 0, 8, s));
-        HPXHIP_CHECK(hipMemsetAsync(bits + 1, 0xff, 8, s));
-        hipLaunchKernelGGL((k_hist<U, X, kHistThreads>), dim3(hist_grid), dim3(kHistThreads), 0, s, k, cnt, first, passes,
-                           X{}, hist, bits, xfield ? kField17Shift : -1, xhist);
-        HPXHIP_CHECK_LAUNCH();
+    U* kc = static_cast<U*>(keys);
+    U* ka = reinterpret_cast<U*>(base + L.alt_keys);
+    VAL* vc = static_cast<VAL*>(vals);
+    VAL* va = reinterpret_cast<VAL*>(base + L.alt_vals);
+
+    auto offsets = [&]() -> int {
         hipLaunchKernelGGL(k_bin_offsets<kRadix>, dim3(passes), dim3(kRadix), 0, s, hist, start);
         HPXHIP_CHECK_LAUNCH();
-        if (xfield) {
-            hipLaunchKernelGGL(k_bin_offsets<kXBins>, dim3(1), dim3(kXBins), 0, s, xhist, xstart);
-            HPXHIP_CHECK_LAUNCH();
-        }
         return 0;
     };
-    // one stable onesweep pass of the rb-bit digit at `shift` over cnt keys
-    auto pass = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, uint64_t cnt, int shift, int rb,
-                    const unsigned long long* bstart) -> int {
-        const uint64_t nt = (cnt + TS::tile - 1) / TS::tile;
-        HPXHIP_CHECK(hipMemsetAsync(counter, 0, 256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), s));
+    // the remaining digits [0, first), iff *gate
+    auto count_rest = [&](const int32_t* gate) -> int {
+        hipLaunchKernelGGL((k_hist<U, X, kHistThreads>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n, 0, first,
+                           X{}, hist, bits, -1, xhist, gate);
+        HPXHIP_CHECK_LAUNCH();
+        return offsets();
+    };
+    // one stable onesweep pass; ctl word: its digit shift or -1 (not run)
+    auto pass = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, int rb, const int32_t* word) -> int {
+        const uint64_t nt = L.ntiles;
+        const uint64_t zbytes = align_up(256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), 16);
+        hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
+                           reinterpret_cast<uint4*>(counter), zbytes / 16, word);
+        HPXHIP_CHECK_LAUNCH();
         const dim3 grid(static_cast<unsigned>(nt)), block(TS::threads);
         auto launch = [&](auto gtag, auto rbtag) {
             using G = decltype(gtag);
@@ -205,9 +361,8 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             // profiles/r02_ubench_tile_order_ab.log).
             constexpr bool DYN = sizeof(U) == 8;
             hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB, true, DYN>),
-                               grid, block, 0,
-                               s, kin, kout, vin, vout, cnt, shift, bstart, reinterpret_cast<G*>(base + L.lb), counter,
-                               err, X{});
+                               grid, block, 0, s, kin, kout, vin, vout, n, 0, RB == 9 ? xstart : start,
+                               reinterpret_cast<G*>(base + L.lb), counter, err, X{}, word);
         };
         using R8 = std::integral_constant<int, 8>;
         using R9 = std::integral_constant<int, 9>;
@@ -215,8 +370,6 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             if constexpr (!HAS_VAL) {
                 if (L.wide) launch((unsigned long long)0, R9{});
                 else launch(uint32_t(0), R9{});
-            } else {
-                return HPXHIP_ERROR_INVALID_ARGUMENT;
             }
         } else {
             if (L.wide) launch((unsigned long long)0, R8{});
@@ -225,206 +378,69 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         HPXHIP_CHECK_LAUNCH();
         return 0;
     };
-    auto pass8 = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, uint64_t cnt, int p) -> int {
-        return pass(kin, kout, vin, vout, cnt, 8 * p, 8, start + p * kRadix);
-    };
 
-    // Pass skipping needs the live digits on the host (a digit is live iff
-    // OR and AND of the keys differ on it).  A sort that may take the hybrid
-    // path counts only the two top digits (and the 9-bit field under the top
-    // byte) first -- the LDS atomics, not the read, bound k_hist -- and counts
-    // the rest only when it needs them.
-    std::vector<unsigned long long> h(static_cast<size_t>(passes) * kRadix);
-    std::vector<unsigned long long> hx(kXBins);
-    std::vector<int> live;  // non-constant digits, most significant first
-    uint64_t diff = 0;      // bits in which the keys differ (ordered form)
-    // 17-bit form: the top byte and the 9-bit field; 16-bit form: the two top bytes
-    int counted = mode ? passes - (mode == 17 ? 1 : 2) : 0;
-    auto count_digits = [&](int first) -> int {
-        const bool xf17 = mode == 17 && first > 0;
-        if ((rc = histogram(static_cast<const U*>(keys), n, first, xf17))) return rc;
-        unsigned long long ob[2];
-        HPXHIP_CHECK(hipMemcpyAsync(h.data(), hist, h.size() * 8, hipMemcpyDeviceToHost, s));
-        if (xf17) HPXHIP_CHECK(hipMemcpyAsync(hx.data(), xhist, hx.size() * 8, hipMemcpyDeviceToHost, s));
-        HPXHIP_CHECK(hipMemcpyAsync(ob, bits, 16, hipMemcpyDeviceToHost, s));
-        HPXHIP_CHECK(hipStreamSynchronize(s));
-        diff = ob[0] ^ ob[1];
-        live.clear();
-        for (int p = passes - 1; p >= 0; --p)
-            if ((diff >> (8 * p)) & 0xffu) live.push_back(p);
-        counted = first;
-        return 0;
-    };
-    if ((rc = count_digits(counted))) return rc;
-    const bool top_two = live.size() >= 3 && live[0] == passes - 1 && live[1] == passes - 2;
-    if (counted > 0 && !top_two)
-        if ((rc = count_digits(0))) return rc;
-    const int counted_first = counted;  // the digits [counted_first, passes) have histograms
-
-    U* kc = static_cast<U*>(keys);
-    U* ka = reinterpret_cast<U*>(base + L.alt_keys);
-    VAL* vc = static_cast<VAL*>(vals);
-    VAL* va = reinterpret_cast<VAL*>(base + L.alt_vals);
-    // LSD over live[from..] (least significant first), whole array, result in keys
-    auto lsd = [&](size_t from) -> int {
-        if (counted > 0 && (rc = histogram(kc, n, 0, false))) return rc;  // a permutation: same counts
-        int executed = 0;
-        for (size_t i = live.size(); i-- > from;) {
-            if ((rc = pass8(kc, ka, vc, va, n, live[i]))) return rc;
-            std::swap(kc, ka);
-            std::swap(vc, va);
-            ++executed;
-        }
-        if (executed & 1) {
-            HPXHIP_CHECK(hipMemcpyAsync(keys, kc, n * sizeof(U), hipMemcpyDeviceToDevice, s));
-            if constexpr (HAS_VAL) HPXHIP_CHECK(hipMemcpyAsync(vals, vc, n * sizeof(VAL), hipMemcpyDeviceToDevice, s));
-        }
-        return 0;
-    };
-
-    if (!mode || live.size() < 3) return lsd(0);
-    auto max_of = [](const unsigned long long* c, int bins) {
-        unsigned long long m = 0;
-        for (int d = 0; d < bins; ++d) m = std::max(m, c[d]);
-        return static_cast<double>(m);
-    };
-    const double dn = static_cast<double>(n);
-    const double m_top = max_of(&h[live[0] * kRadix], kRadix);
-    int variant = 0;  // 17 or 16 (prefix bits), 0 = plain LSD
-    if (mode == 17 && counted_first > 0 && top_two && m_top * max_of(hx.data(), kXBins) / dn <= 0.95 * kCap17) {
-        variant = 17;
-    } else if (mode >= 16) {
-        if (live[1] < counted_first && (rc = count_digits(0))) return rc;  // the second byte was not counted
-        if (m_top * max_of(&h[live[1] * kRadix], kRadix) / dn <= 0.95 * (HAS_VAL ? kCapKV : kCap16)) variant = 16;
-    }
-    if (!variant) return lsd(0);
-
-    // ---- prefix passes (low field, then the top live byte: keys -> alt -> keys)
-    const int p1 = live[0];
-    const int s2 = variant == 17 ? kField17Shift : 8 * live[1];
-    const int b2 = variant == 17 ? 9 : 8;
-    if (variant == 17) {
-        if ((rc = pass(kc, ka, nullptr, nullptr, n, s2, 9, xstart))) return rc;
-    } else {
-        if ((rc = pass8(kc, ka, vc, va, n, live[1]))) return rc;
-    }
-    if ((rc = pass8(ka, kc, va, vc, n, p1))) return rc;
-    const uint32_t nb = 256u << b2;
-    auto* bounds = reinterpret_cast<uint64_t*>(base + L.bounds);
-    hipLaunchKernelGGL((k_bucket_bounds<U, X>), dim3((nb + 1 + 255) / 256), dim3(256), 0, s, kc, n, 8 * p1, s2, b2, nb,
-                       X{}, bounds);
+    // ---- first histogram (+ OR / AND of the keys) and the plan
+    HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8 + kXBins * 8, s));  // hist and xhist
+    HPXHIP_CHECK(hipMemsetAsync(bits, 0, 8, s));
+    HPXHIP_CHECK(hipMemsetAsync(bits + 1, 0xff, 8, s));
+    hipLaunchKernelGGL((k_hist<U, X, kHistThreads>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n, first, passes,
+                       X{}, hist, bits, xfield ? kField17Shift : -1, xhist, static_cast<const int32_t*>(nullptr));
     HPXHIP_CHECK_LAUNCH();
-    // the highest bit in which keys of one bucket can differ
-    const int top_single = top_bit(diff & ((uint64_t(1) << s2) - 1));
-    const uint64_t cap = HAS_VAL ? kCapKV : variant == 17 ? kCap17 : kCap16;
-    std::vector<uint64_t> off;
-    auto read_bounds = [&]() -> int {
-        off.resize(nb + 1);
-        HPXHIP_CHECK(hipMemcpyAsync(off.data(), bounds, off.size() * 8, hipMemcpyDeviceToHost, s));
-        HPXHIP_CHECK(hipStreamSynchronize(s));
-        return 0;
-    };
-    // oversized buckets: LSD over the live bytes under the prefix, with the
-    // bucket's own histogram (the byte that holds bit 47 under a 17-bit
-    // prefix is included: its prefix bit is constant inside the bucket)
-    auto finish_big = [&](const std::vector<std::pair<uint64_t, uint64_t>>& big) -> int {
-        for (const auto& [bs, len] : big) {
-            if ((rc = histogram(kc + bs, len, 0, false))) return rc;
-            U* a = kc + bs;
-            U* b = ka + bs;
-            VAL* av = HAS_VAL ? vc + bs : nullptr;
-            VAL* bv = HAS_VAL ? va + bs : nullptr;
-            for (size_t i = live.size(); i-- > 0;) {
-                if (8 * live[i] >= s2) continue;
-                if ((rc = pass8(a, b, av, bv, len, live[i]))) return rc;
-                std::swap(a, b);
-                std::swap(av, bv);
-            }
-            if (a != kc + bs) {
-                HPXHIP_CHECK(hipMemcpyAsync(kc + bs, a, len * sizeof(U), hipMemcpyDeviceToDevice, s));
-                if constexpr (HAS_VAL)
-                    HPXHIP_CHECK(hipMemcpyAsync(vc + bs, av, len * sizeof(VAL), hipMemcpyDeviceToDevice, s));
-            }
-        }
-        return 0;
-    };
-    // Buckets of at least DIRECT_DIV-th of a segment on average (random keys
-    // from about 2^29.2 up with the 17-bit prefix): one workgroup per bucket
-    // straight from the bounds, so no read-back and host packing (1.2 ms of
-    // idle GPU at 2^30, profiles/r02_sort_direct_buckets.log) sits between
-    // the prefix passes and the segment sort; only an oversized bucket brings
-    // the bounds to the host.
-    const double direct_div = direct_divisor();
-    if (top_single > 0 && (HAS_VAL || variant == 17) &&
-        direct_div * static_cast<double>(n) >= static_cast<double>(nb) * cap) {
-        auto* oversized = reinterpret_cast<uint32_t*>(bits + 2);
-        HPXHIP_CHECK(hipMemsetAsync(oversized, 0, 4, s));
-        if constexpr (HAS_VAL)
-            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true, true>), dim3(nb),
-                               dim3(kSegThreads16), 0, s, kc, bounds, top_single, X{}, vc, oversized);
-        else
-            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true>), dim3(nb),
-                               dim3(kSegThreads17), 0, s, kc, bounds, top_single, X{}, nullptr, oversized);
-        HPXHIP_CHECK_LAUNCH();
-        uint32_t big_flag = 0;
-        HPXHIP_CHECK(hipMemcpyAsync(&big_flag, oversized, 4, hipMemcpyDeviceToHost, s));
-        HPXHIP_CHECK(hipStreamSynchronize(s));
-        if (!big_flag) return 0;
-        if ((rc = read_bounds())) return rc;
-        std::vector<std::pair<uint64_t, uint64_t>> big;
-        for (uint32_t v = 0; v < nb; ++v)
-            if (off[v + 1] - off[v] > cap) big.emplace_back(off[v], off[v + 1] - off[v]);
-        if (big.size() > kMaxBigBuckets) return lsd(0);
-        return finish_big(big);
-    }
-    if ((rc = read_bounds())) return rc;
-
-    // segments: runs of whole buckets of at most `cap` keys; larger buckets
-    // are finished separately
-    std::vector<uint64_t> segs;
-    std::vector<std::pair<uint64_t, uint64_t>> big;
-    uint64_t sb = 0, se = 0;
-    auto close = [&] {
-        if (se > sb) {
-            segs.push_back(sb);
-            segs.push_back(se);
-        }
-    };
-    for (uint32_t v = 0; v < nb; ++v) {
-        const uint64_t bs = off[v], be = off[v + 1];
-        if (be == bs) continue;
-        if (be - bs > cap) {
-            close();
-            big.emplace_back(bs, be - bs);
-            sb = se = be;
-            continue;
-        }
-        if (be - sb > cap) {
-            close();
-            sb = bs;
-        }
-        se = be;
-    }
-    close();
-    if (big.size() > kMaxBigBuckets) return lsd(0);  // plain LSD from here (the prefix passes are wasted)
-
-    if (!segs.empty() && top_single > 0) {
-        auto* segd = reinterpret_cast<uint64_t*>(base + L.segs);
-        HPXHIP_CHECK(hipMemcpyAsync(segd, segs.data(), segs.size() * 8, hipMemcpyHostToDevice, s));
-        HPXHIP_CHECK(hipStreamSynchronize(s));  // `segs` is pageable and local
-        const dim3 grid(static_cast<unsigned>(segs.size() / 2));
-        if constexpr (HAS_VAL)
-            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true>), grid,
-                               dim3(kSegThreads16), 0, s, kc, segd, top_single, X{}, vc);
-        else if (variant == 17)
-            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems>), grid, dim3(kSegThreads17), 0, s, kc,
-                               segd, top_single, X{});
-        else
-            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItems>), grid, dim3(kSegThreads16), 0, s, kc,
-                               segd, top_single, X{});
+    if ((rc = offsets())) return rc;
+    if (xfield) {
+        hipLaunchKernelGGL(k_bin_offsets<kXBins>, dim3(1), dim3(kXBins), 0, s, xhist, xstart);
         HPXHIP_CHECK_LAUNCH();
     }
-    return finish_big(big);
+    hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, bits, n, passes, first, mode, HAS_VAL ? 1 : 0,
+                       0, ctl);
+    HPXHIP_CHECK_LAUNCH();
+    if (first > 0) {
+        if ((rc = count_rest(ctl + C_HIST_A))) return rc;
+        hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, bits, n, passes, first, mode,
+                           HAS_VAL ? 1 : 0, 1, ctl);
+        HPXHIP_CHECK_LAUNCH();
+    }
+
+    // ---- hybrid: prefix passes (keys -> alt -> keys), bucket bounds, per-bucket LDS sort
+    if (mode) {
+        if (!HAS_VAL && mode == 17 && (rc = pass(kc, ka, nullptr, nullptr, 9, ctl + C_A9))) return rc;
+        if ((rc = pass(kc, ka, vc, va, 8, ctl + C_A8))) return rc;
+        if ((rc = pass(ka, kc, va, vc, 8, ctl + C_B))) return rc;
+        hipLaunchKernelGGL((k_bucket_bounds<U, X>), dim3((kMaxBuckets + 1 + 255) / 256), dim3(256), 0, s, kc, n, 0, 0,
+                           0, 0u, X{}, bounds, ctl + C_BOUNDS);
+        HPXHIP_CHECK_LAUNCH();
+        auto* oversized = reinterpret_cast<uint32_t*>(ctl + C_OVERSIZED);
+        if constexpr (HAS_VAL) {
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true, true>),
+                               dim3(kMaxBuckets / 2), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, vc, oversized,
+                               ctl + C_SEGA);
+        } else {
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true>),
+                               dim3(kMaxBuckets), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
+                               ctl + C_SEGA);
+            HPXHIP_CHECK_LAUNCH();
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItems, 16, uint32_t, false, true>),
+                               dim3(kMaxBuckets / 2), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, nullptr,
+                               oversized, ctl + C_SEGB);
+        }
+        HPXHIP_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_sort_fallback, dim3(1), dim3(64), 0, s, ctl);
+        HPXHIP_CHECK_LAUNCH();
+        if (first > 0 && (rc = count_rest(ctl + C_HIST_B))) return rc;
+    }
+
+    // ---- LSD over the live digits (keys <-> alt), when planned
+    for (int i = 0; i < passes; ++i) {
+        const bool even = (i & 1) == 0;
+        if ((rc = pass(even ? kc : ka, even ? ka : kc, even ? vc : va, even ? va : vc, 8, ctl + C_LSD + i))) return rc;
+    }
+    hipLaunchKernelGGL((k_copy_gated<U>), dim3(grid_for(n)), dim3(256), 0, s, ka, kc, n, ctl + C_COPY);
+    HPXHIP_CHECK_LAUNCH();
+    if constexpr (HAS_VAL) {
+        hipLaunchKernelGGL((k_copy_gated<VAL>), dim3(grid_for(n)), dim3(256), 0, s, va, vc, n, ctl + C_COPY);
+        HPXHIP_CHECK_LAUNCH();
+    }
+    return 0;
 }
 
 template <typename T, typename VAL, bool HAS_VAL>

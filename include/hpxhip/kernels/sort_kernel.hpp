@@ -61,7 +61,9 @@ template <typename U, typename X, int THREADS = 256, int COPIES = 4>
 __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, uint64_t n, int first, int passes, X xf,
                                                    unsigned long long* __restrict__ hist,
                                                    unsigned long long* __restrict__ bits, int xshift,
-                                                   unsigned long long* __restrict__ xhist) {
+                                                   unsigned long long* __restrict__ xhist,
+                                                   const int32_t* __restrict__ gate = nullptr) {
+    if (gate && *gate == 0) return;  // device-planned sort: this count is not needed
     constexpr int P = static_cast<int>(sizeof(U));
     __shared__ uint32_t h[P * kRadix * COPIES];
     __shared__ uint32_t hx[kXBins * COPIES];
@@ -166,7 +168,16 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
                                                        uint64_t n, int shift,
                                                        const unsigned long long* __restrict__ bin_start,
                                                        G* __restrict__ lb, uint32_t* __restrict__ counter,
-                                                       uint32_t* __restrict__ err, X xf) {
+                                                       uint32_t* __restrict__ err, X xf,
+                                                       const int32_t* __restrict__ ctl = nullptr) {
+    // device-planned sort (sort.hip): *ctl = this launch's digit shift, or
+    // -1 when the plan does not take this pass (every block returns at once)
+    if (ctl) {
+        const int32_t sh = *ctl;
+        if (sh < 0) return;
+        shift = sh;
+        if constexpr (RB == 8) bin_start += static_cast<uint32_t>(sh >> 3) * kRadix;
+    }
     constexpr int R = 1 << RB;
     constexpr uint32_t DMASK = R - 1;
     using CT = std::conditional_t<(RB > 8), uint16_t, uint32_t>;
@@ -352,9 +363,18 @@ __device__ __forceinline__ uint32_t bucket_of(U k, int s1, int s2, int b2, X xf)
 
 // off[v] = first index whose prefix is >= v (v = 0..nb): a lower_bound per
 // bucket over the prefix-ordered keys instead of a pass over all of them.
+// ctl (device-planned sort): {on, nb, s1, s2, b2} read on the device.
 template <typename U, typename X>
 __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ keys, uint64_t n, int s1, int s2, int b2,
-                                                        uint32_t nb, X xf, uint64_t* __restrict__ off) {
+                                                        uint32_t nb, X xf, uint64_t* __restrict__ off,
+                                                        const int32_t* __restrict__ ctl = nullptr) {
+    if (ctl) {
+        if (!ctl[0]) return;
+        nb = static_cast<uint32_t>(ctl[1]);
+        s1 = ctl[2];
+        s2 = ctl[3];
+        b2 = ctl[4];
+    }
     const uint32_t v = blockIdx.x * 256 + threadIdx.x;
     if (v > nb) return;
     uint64_t lo = 0, hi = n;
@@ -395,7 +415,14 @@ template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX
           bool HAS_VAL = false, bool BOUNDS = false>
 __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
     void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf,
-                       VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr) {
+                       VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr,
+                       const int32_t* __restrict__ ctl = nullptr) {
+    // device-planned sort: ctl = {on, buckets, top_single}; the grid covers
+    // the largest bucket count, blocks past the planned one return
+    if (ctl) {
+        if (!ctl[0] || blockIdx.x >= static_cast<uint32_t>(ctl[1])) return;
+        top_single = ctl[2];
+    }
     constexpr int WAVES = THREADS / kWave;
     constexpr int CHUNK = ITEMS * kWave;
     constexpr int BITS = static_cast<int>(sizeof(U) * 8);

@@ -1,14 +1,75 @@
-"""Sort-only run for rocprof breakdown: 2^30 keys (KEY=u64 | u32), sorted twice."""
-import ctypes, os, sys
+"""Sort size sweep on one GPU: hpxhip_sort / hpxhip_sort_by_key over random
+keys at 2^20..2^30, device time from HIP events (best of 3, generation
+subtracted), host time of the call itself, and an is_sorted + checksum
+check of every result.  usage: python scripts/sort_probe.py [maxlog]"""
+import ctypes
+import os
+import sys
+import time
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from hpx_amd import _lib as L
-lib = L.load(); vp = ctypes.c_void_p
-st = vp(); L.check(lib.hpxhip_stream_create(0, ctypes.byref(st)))
-N = 1 << int(os.environ.get("LOGN", "30"))
-KT, KB = (L.U32, 4) if os.environ.get("KEY") == "u32" else (L.U64, 8)
-k = vp(); L.check(lib.hpxhip_malloc(0, ctypes.byref(k), KB * N))
-for r in range(2):
-    L.check(lib.hpxhip_generate(KT, L.GEN_BITS, 7 + r, 0, 0, k, N, st))
-    L.check(lib.hpxhip_sort(KT, k, N, 0, st, None, 0))
-L.check(lib.hpxhip_stream_synchronize(st))
-print("done")
+import numpy as np  # noqa: E402
+
+import hpx_amd as hpx  # noqa: E402
+from hpx_amd import _lib as L  # noqa: E402
+from hpx_amd import execution as ex, functional as F, parallel as P  # noqa: E402
+from hpx_amd.compute import dtype_code  # noqa: E402
+
+t = hpx.target(0)
+pol = ex.par.on(hpx.default_executor(t))
+S = t.stream
+
+
+def ev():
+    h = ctypes.c_void_p()
+    L.call("hpxhip_event_create", ctypes.byref(h))
+    return h
+
+
+e0, e1, e2 = ev(), ev(), ev()
+
+
+def ms(a, b):
+    f = ctypes.c_float()
+    L.call("hpxhip_event_elapsed_ms", a, b, ctypes.byref(f))
+    return f.value
+
+
+def run(dt, logn, kv=False, reps=3):
+    n = 1 << logn
+    k = hpx.vector(n, dtype=dt, tgt=t)
+    v = hpx.vector(n, dtype=np.uint64, tgt=t) if kv else None
+    best, host = 1e30, 1e30
+    for r in range(reps):
+        P.generate(pol, k.begin(), k.end(), "bits", 7 + r)
+        if kv:
+            P.generate(pol, v.begin(), v.end(), "iota", 0, 0, 0)
+        t.synchronize()
+        L.call("hpxhip_event_record", e0, S)
+        h0 = time.perf_counter()
+        if kv:
+            L.call("hpxhip_sort_by_key", dtype_code(dt), L.U64, ctypes.c_void_p(k.data()), ctypes.c_void_p(v.data()),
+                   n, 0, S, None, 0)
+        else:
+            L.call("hpxhip_sort", dtype_code(dt), ctypes.c_void_p(k.data()), n, 0, S, None, 0)
+        h1 = time.perf_counter()
+        L.call("hpxhip_event_record", e1, S)
+        t.synchronize()
+        best = min(best, ms(e0, e1))
+        host = min(host, 1e3 * (h1 - h0))
+    ok = bool(P.is_sorted(pol, k.begin(), k.end()))
+    if kv:  # values are a permutation of iota: sum check
+        ok = ok and P.reduce(pol, v.begin(), v.end(), 0, F.plus) == n * (n - 1) // 2
+        v.free()
+    k.free()
+    return best, host, ok
+
+
+maxlog = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+print(f"{'case':28s} {'ms':>9s} {'Gkeys/s':>8s} {'host_ms':>8s} ok", flush=True)
+for logn in range(20, maxlog + 1, 2):
+    for dt, kv, name in ((np.uint64, False, "u64"), (np.uint32, False, "u32"), (np.uint64, True, "u64/u64 pairs")):
+        if kv and logn > 28:
+            continue
+        d, h, ok = run(dt, logn, kv)
+        print(f"{name + ' 2^' + str(logn):28s} {d:9.3f} {(1 << logn) / d / 1e6:8.2f} {h:8.3f} {ok}", flush=True)

@@ -18,6 +18,7 @@
 #include <hpx/hpx_init.hpp>
 #include <hpx/util/lightweight_test.hpp>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <vector>
@@ -81,6 +82,31 @@ int hpx_main(int, char**) {
     exec.target().synchronize();
     HPX_TEST_EQ(double(a[n - 1]), 2.0);  // a = b + 3 c with b = 2, c = 0
 
+    // sort(par(task)) returns once the device-planned sort is enqueued
+    // (sort.hpp:251-276); a reduce queued behind it on the same stream sees
+    // the sorted keys.  2^27 u64 keys: the device takes milliseconds, the
+    // call must return in far less.
+    using ualloc_t = hpx::compute::hip::allocator<uint64_t>;
+    const std::size_t nk = std::size_t(1) << 27;
+    hpx::compute::vector<uint64_t, ualloc_t> keys(nk, ualloc_t(t));
+    double sort_call_us = 1e30, sort_total_us = 1e30;
+    for (int rep = 0; rep < 3; ++rep) {
+        hpxhip_generate(HPXHIP_U64, HPXHIP_GEN_BITS, 77 + rep, 0, 0, keys.data(), nk, stream);
+        const uint64_t sum0 = hpx::parallel::reduce(ex::par.on(exec), keys.begin(), keys.end(), uint64_t(0));
+        const auto t0 = std::chrono::steady_clock::now();
+        auto fs = hpx::parallel::sort(ex::par(ex::task).on(exec), keys.begin(), keys.end());
+        const auto t1 = std::chrono::steady_clock::now();
+        auto fr = hpx::parallel::reduce(ex::par(ex::task).on(exec), keys.begin(), keys.end(), uint64_t(0));
+        auto fo = hpx::parallel::is_sorted(ex::par(ex::task).on(exec), keys.begin(), keys.end());
+        HPX_TEST(fs.get() == keys.end());
+        HPX_TEST_EQ(fr.get(), sum0);
+        HPX_TEST(fo.get());
+        const auto t2 = std::chrono::steady_clock::now();
+        sort_call_us = std::min(sort_call_us, std::chrono::duration<double, std::micro>(t1 - t0).count());
+        sort_total_us = std::min(sort_total_us, std::chrono::duration<double, std::micro>(t2 - t0).count());
+    }
+    HPX_TEST(sort_call_us < 0.25 * sort_total_us);  // the call did not wait for the device
+
     std::printf("C++ layer host time per call, %zu doubles (us):\n", n);
     std::printf("  transform par.on(exec)                 %8.2f\n", sync_tr);
     std::printf("  transform par(task).on(exec) + get     %8.2f\n", task_tr);
@@ -88,6 +114,9 @@ int hpx_main(int, char**) {
     std::printf("  reduce par(task).on(inline exec) + get %8.2f\n", task_red);
     std::printf("  reduce x64 futures + when_all, per call %7.2f\n", many);
     std::printf("  raw C ABI enqueue (transform_binary)   %8.2f\n", raw);
+    std::printf("sort(par(task)) of 2^27 u64 keys: call returns after %.1f us, sort + reduce + is_sorted done "
+                "after %.1f us\n",
+                sort_call_us, sort_total_us);
     return hpx::finalize();
 }
 

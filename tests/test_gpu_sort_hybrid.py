@@ -1,11 +1,13 @@
-"""The hybrid tail of the keys-only sort (64- and 32-bit keys) (sort.hip: two onesweep passes
-on the prefix -- the top byte and the 9 bits under it (17-bit form, 9216-key
-segments) or the two top live bytes (16-bit form, 18432-key segments) --,
-bucket bounds by lower_bound, one LDS-resident sort per segment of whole
-buckets; oversized buckets finished by per-bucket LSD, many of them by plain
-LSD), checked element for element against numpy's sort on the distributions
-that steer it down each branch, in both forms (HPXHIP_SORT_HYBRID=17 / 16).
-Sizes start at the hybrid's 2^22-key threshold.
+"""The hybrid tail of the sort (64- and 32-bit keys, and sort_by_key), planned
+on the device (sort.hip k_sort_plan): two onesweep passes on the prefix --
+the top byte and the 9 bits under it (17-bit form) or the two top live bytes
+(16-bit form) --, bucket bounds by lower_bound over buckets of the top byte
+plus b2 bits, b2 chosen from the histograms, one LDS-resident sort per
+bucket (512- or 1024-thread segments); a bucket over its segment's capacity
+sends the whole sort to the LSD over the live digits.  Checked element for
+element against numpy's sort on the distributions that steer it down each
+branch, in both forms (HPXHIP_SORT_HYBRID=17 / 16).  Sizes start at the
+hybrid's 2^22-key threshold.
 
 Parity: std::sort's order for integer keys (sort.hpp:78-229 via the oracle's
 O.sort, itself numpy's stable sort) and the IEEE total order for doubles."""
@@ -239,12 +241,11 @@ def test_sort_by_key_32bit_duplicates_and_oversized(pol, gpu_target):
     check_kv(pol, gpu_target, k, v)
 
 
-# ---- the direct per-bucket path (one workgroup per bucket, bounds read on
-# the device, oversized buckets flagged) forced at test sizes: normally it
-# starts where buckets average half a segment (~2^29 random keys).
+# ---- one workgroup per bucket straight from the bounds (the device plan
+# picks the bucket width from the histograms), with an oversized bucket
+# flagged by the segment kernel and the whole sort finished by the LSD.
 @pytest.mark.parametrize("kdt", [np.uint64, np.uint32])
-def test_direct_path_forced(pol, gpu_target, monkeypatch, kdt):
-    monkeypatch.setenv("HPXHIP_SORT_DIRECT", "100000")
+def test_direct_path_and_fallback(pol, gpu_target, kdt):
     rng = np.random.default_rng(41)
     n = 1 << 22
     bits = np.dtype(kdt).itemsize * 8
