@@ -128,6 +128,7 @@ SIGNATURES = {
     "hpxhip_transform_reduce": [_i, _i, _i, _i, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _sz],
     "hpxhip_transform_reduce_binary": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _sz],
     "hpxhip_fold": [_i, _i, _vp, _vp, _u64, _vp, _vp],
+    "hpxhip_fold_exclusive": [_i, _i, _vp, _vp, _u64, _vp, _vp],
     "hpxhip_scan": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _sz],
     "hpxhip_copy_if": [_i, _i, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _sz],
     "hpxhip_sort": [_i, _vp, _u64, _i, _vp, _vp, _sz],

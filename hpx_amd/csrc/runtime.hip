@@ -175,6 +175,17 @@ __global__ void k_fold(T init, const T* __restrict__ v, uint64_t count, T* __res
         *out = acc;
     }
 }
+// The carries of a segmented scan (detail/scan.hpp:646-677): out[0] = init,
+// out[j + 1] = out[j] (op) v[j] -- the same segment-order left fold as k_fold,
+// every prefix kept.
+template <typename T, typename Op>
+__global__ void k_fold_exclusive(T init, const T* __restrict__ v, uint64_t count, T* __restrict__ out, Op op) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        T acc = init;
+        out[0] = acc;
+        for (uint64_t i = 0; i < count; ++i) out[i + 1] = acc = op(acc, v[i]);
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -453,12 +464,34 @@ int hpxhip_fold(int dtype, int op, const void* init, const void* values_dev, uin
     HPXHIP_ANNOTATE("hpxhip_fold");
     if (!init || !out_dev || (count && !values_dev)) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
     return with_dtype(dtype, [&](auto t) -> int {
         using T = typename decltype(t)::type;
         return with_binop<T>(op, [&](auto o) -> int {
             T iv;
             std::memcpy(&iv, init, sizeof(T));
             hipLaunchKernelGGL((k_fold<T, decltype(o)>), dim3(1), dim3(64), 0, s, iv,
+                               static_cast<const T*>(values_dev), count, static_cast<T*>(out_dev), o);
+            HPXHIP_CHECK_LAUNCH();
+            return 0;
+        });
+    });
+}
+
+int hpxhip_fold_exclusive(int dtype, int op, const void* init, const void* values_dev, uint64_t count,
+                          void* out_dev, hpxhip_stream stream) {
+    HPXHIP_ANNOTATE("hpxhip_fold_exclusive");
+    if (!init || !out_dev || (count && !values_dev)) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    return with_dtype(dtype, [&](auto t) -> int {
+        using T = typename decltype(t)::type;
+        return with_binop<T>(op, [&](auto o) -> int {
+            T iv;
+            std::memcpy(&iv, init, sizeof(T));
+            hipLaunchKernelGGL((k_fold_exclusive<T, decltype(o)>), dim3(1), dim3(64), 0, s, iv,
                                static_cast<const T*>(values_dev), count, static_cast<T*>(out_dev), o);
             HPXHIP_CHECK_LAUNCH();
             return 0;

@@ -164,10 +164,12 @@ enum : int {
 };
 static_assert(C_WORDS * 4 <= 256, "plan words fit their slot");
 
-// A bucket whose estimated size exceeds this fraction of its segment's LDS
-// capacity is not planned (a bucket over the capacity sends the whole sort to
-// the LSD); the estimate is (largest top-byte bin) x (largest field bin) / n.
-constexpr double kFit = 0.8;
+// A bucket width is planned only if the estimated largest bucket, (largest
+// top-byte bin) x (largest field bin) / n, plus five standard deviations of
+// a Poisson count of that mean fits the segment's LDS capacity (a bucket
+// over the capacity sends the whole sort to the LSD).  2^30 uniform keys:
+// 8192 + 453 <= 9216 for 17-bit buckets.
+__device__ inline bool fits(double est, double cap) { return est + 5.0 * sqrt(est) <= cap; }
 
 __device__ inline int top_bit_d(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
 
@@ -234,7 +236,7 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
         const double m_top = bin_max(hist + live[0] * kRadix, kRadix, 1);
         const int fs = 8 * passes - 17;
         for (int b2 = 1; b2 <= 9; ++b2)
-            if (m_top * bin_max(xhist, kXBins, 1 << (9 - b2)) / dn <= kFit * kCap17) {
+            if (fits(m_top * bin_max(xhist, kXBins, 1 << (9 - b2)) / dn, kCap17)) {
                 ctl[C_A9] = fs;
                 ctl[C_B] = 8 * live[0];
                 return plan(8 * live[0], fs + 9 - b2, b2, C_SEGA);
@@ -249,12 +251,12 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
         const double m_top = bin_max(hist + live[0] * kRadix, kRadix, 1);
         const unsigned long long* h2 = hist + live[1] * kRadix;
         for (int b2 = 1; b2 <= 8; ++b2)
-            if (m_top * bin_max(h2, kRadix, 1 << (8 - b2)) / dn <= kFit * (has_val ? kCapKV : kCap17)) {
+            if (fits(m_top * bin_max(h2, kRadix, 1 << (8 - b2)) / dn, has_val ? kCapKV : kCap17)) {
                 ctl[C_A8] = 8 * live[1];
                 ctl[C_B] = 8 * live[0];
                 return plan(8 * live[0], 8 * live[1] + 8 - b2, b2, C_SEGA);
             }
-        if (!has_val && m_top * bin_max(h2, kRadix, 1) / dn <= kFit * kCap16) {
+        if (!has_val && fits(m_top * bin_max(h2, kRadix, 1) / dn, kCap16)) {
             ctl[C_A8] = 8 * live[1];
             ctl[C_B] = 8 * live[0];
             return plan(8 * live[0], 8 * live[1], 8, C_SEGB);

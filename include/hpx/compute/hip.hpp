@@ -249,6 +249,56 @@ public:
         free_.push_back(id);
     }
 
+    // Device blocks of 2^cls bytes (cls >= 8) for the small per-call arrays of
+    // the segmented algorithms (segment totals and carries), kept per size
+    // class for the process lifetime like the slots.
+    struct block_ref {
+        unsigned cls, idx;
+        void* dev;
+    };
+    block_ref acquire_block(std::size_t bytes) {
+        unsigned cls = 8;
+        while ((std::size_t(1) << cls) < bytes) ++cls;
+        std::lock_guard<std::mutex> lk(mtx_);
+        auto& fl = block_free_[cls];
+        if (fl.empty()) {
+            void* d = nullptr;
+            check(hpxhip_malloc(device_, &d, std::size_t(1) << cls), "device block");
+            blocks_.push_back(d);
+            fl.push_back(static_cast<unsigned>(blocks_.size() - 1));
+        }
+        const unsigned idx = fl.back();
+        fl.pop_back();
+        return {cls, idx, blocks_[idx]};
+    }
+    // No HIP call: safe from a stream callback.
+    void release_block(block_ref const& b) {
+        std::lock_guard<std::mutex> lk(mtx_);
+        block_free_[b.cls].push_back(b.idx);
+    }
+    // The same for pinned host blocks (staging of stream-ordered H2D copies:
+    // the bytes must stay valid until the copy has run, so the block returns
+    // to the pool from the stream, not when the caller's frame ends).
+    block_ref acquire_host_block(std::size_t bytes) {
+        unsigned cls = 8;
+        while ((std::size_t(1) << cls) < bytes) ++cls;
+        std::lock_guard<std::mutex> lk(mtx_);
+        auto& fl = host_free_[cls];
+        if (fl.empty()) {
+            void* h = nullptr;
+            check(hpxhip_malloc_host(&h, std::size_t(1) << cls), "pinned block");
+            host_blocks_.push_back(h);
+            fl.push_back(static_cast<unsigned>(host_blocks_.size() - 1));
+        }
+        const unsigned idx = fl.back();
+        fl.pop_back();
+        return {cls, idx, host_blocks_[idx]};
+    }
+    void release_host_block(block_ref const& b) {
+        std::lock_guard<std::mutex> lk(mtx_);
+        host_free_[b.cls].push_back(b.idx);
+    }
+
     hpxhip_stream take_stream() {
         {
             std::lock_guard<std::mutex> lk(mtx_);
@@ -297,7 +347,38 @@ private:
     std::vector<std::pair<void*, void*>> chunks_;  // (device, pinned host) per chunk
     std::vector<unsigned> free_;
     std::vector<hpxhip_stream> streams_;
+    std::vector<void*> blocks_, host_blocks_;
+    std::vector<unsigned> block_free_[64], host_free_[64];
 };
+
+// Run fn (no HIP calls: it runs on the HIP callback thread) once the work
+// queued on s so far is done.
+inline void on_stream_done(hpxhip_stream s, std::function<void()> fn) {
+    auto* p = new std::function<void()>(std::move(fn));
+    int rc = hpxhip_stream_add_callback(
+        s,
+        [](void* u, int) {
+            auto* f = static_cast<std::function<void()>*>(u);
+            (*f)();
+            delete f;
+        },
+        p);
+    if (rc != HPXHIP_SUCCESS) {
+        delete p;
+        check(rc, "hpxhip_stream_add_callback");
+    }
+}
+
+// `after` waits (on the device) for the work queued on `before` so far.
+inline void stream_after(hpxhip_stream after, hpxhip_stream before) {
+    if (after == before) return;
+    hpxhip_event e = nullptr;
+    check(hpxhip_event_create(&e), "hpxhip_event_create");
+    int rc = hpxhip_event_record(e, before);
+    if (rc == HPXHIP_SUCCESS) rc = hpxhip_stream_wait_event(after, e);
+    hpxhip_event_destroy(e);  // released once the wait no longer needs it
+    check(rc, "stream ordering");
+}
 }  // namespace detail
 
 // One 64-byte (device, pinned host) result slot, returned to its device pool

@@ -21,6 +21,7 @@
 #include <hpx/compute/hip/default_executor.hpp>
 #include <hpx/parallel/execution.hpp>
 
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <cstddef>
@@ -91,15 +92,26 @@ public:
     void sync_execute(F&& f, Ts&&... ts) const {
         next().sync_execute(std::forward<F>(f), std::forward<Ts>(ts)...);
     }
-    // :173-199: each shape element on the next stream (a one-element bulk
-    // launch there), one future per element.
+    // :173-199 with concurrent_executor_parameters (chunk = ceil(n / streams)):
+    // the shape is cut into one chunk per stream, each chunk one bulk launch
+    // on its own stream, one future per chunk; nothing waits for the device.
     template <typename F, typename Shape, typename... Ts>
     std::vector<hpx::future<void>> bulk_async_execute(F&& f, Shape const& shape, Ts&&... ts) const {
+        using V = typename std::decay<decltype(*std::begin(shape))>::type;
+        std::vector<V> all(std::begin(shape), std::end(shape));
         std::vector<hpx::future<void>> result;
-        for (auto const& s : shape) {
+        const std::size_t k = execs_.size();
+        const std::size_t chunk = concurrent_executor_parameters{}.get_chunk_size(*this, f, k, all.size());
+        for (std::size_t off = 0; off < all.size(); off += chunk) {
             auto const& e = next();
-            std::array<typename std::decay<decltype(s)>::type, 1> one{{s}};
-            e.bulk_launch(f, one, ts...);
+            const std::size_t cnt = std::min(chunk, all.size() - off);
+            struct range {
+                V const* b;
+                V const* e;
+                V const* begin() const { return b; }
+                V const* end() const { return e; }
+            };
+            e.bulk_launch(f, range{all.data() + off, all.data() + off + cnt}, ts...);  // staged before it returns
             result.push_back(e.target().get_future());
         }
         return result;

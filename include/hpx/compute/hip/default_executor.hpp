@@ -20,6 +20,7 @@
 #include <hpx/compute/hip/detail/launch.hpp>
 #include <hpx/parallel/execution.hpp>
 
+#include <algorithm>
 #include <cstddef>
 #include <iterator>
 #include <type_traits>
@@ -89,38 +90,44 @@ public:
         target_.synchronize();
     }
 
-    // :194-199 (bulk_launch_helper<Shape>, :42-84)
+    // :194-199 (bulk_launch_helper<Shape>, :42-84): the shape is staged in a
+    // pinned block and copied to a device block, both from this device's
+    // pools and both returned to them from the stream once the launch has
+    // run -- no allocation, free or synchronisation per call.  (Round 2 copied
+    // from the caller's pageable std::vector and freed it when the call
+    // returned; the stream-ordered H2D could then still be reading it, which
+    // is what lost the first shape element.  That version synchronised to
+    // hide it.)
     template <typename F, typename Shape, typename... Ts>
     void bulk_launch(F&& f, Shape const& shape, Ts&&... ts) const {
 #if HPX_HAVE_HIP_DEVICE_CLOSURES
         using V = typename std::decay<decltype(*std::begin(shape))>::type;
         static_assert(std::is_trivially_copyable<V>::value, "bulk shape elements are copied to the device");
-        // As the reference (default_executor.hpp:58-75): the shape goes to a
-        // device buffer owned by this call, freed when the call returns --
-        // hipFree waits for the device, as cudaFree of the reference's
-        // compute::vector does, so a bulk launch is synchronous w.r.t. its
-        // shape.  (A stream-ordered hipMallocAsync/pageable-copy variant lost
-        // the first element of a launch on MI355X; see DESIGN.md.)
-        std::vector<V> host(std::begin(shape), std::end(shape));
-        uint64_t count = host.size();
+        const uint64_t count = static_cast<uint64_t>(std::distance(std::begin(shape), std::end(shape)));
         if (count == 0) return;
+        auto& pool = detail::device_pool::get(target_.device());
+        const std::size_t bytes = count * sizeof(V);
+        auto hb = pool.acquire_host_block(bytes);
+        std::copy(std::begin(shape), std::end(shape), static_cast<V*>(hb.dev));
+        auto db = pool.acquire_block(bytes);
         hpxhip_stream s = target_.stream();
-        void* dev = nullptr;
-        hip::detail::check(hpxhip_malloc(target_.device(), &dev, count * sizeof(V)), "bulk_launch shape");
-        int rc = hpxhip_memcpy_async(dev, host.data(), count * sizeof(V), HPXHIP_H2D, s);
-        if (rc == HPXHIP_SUCCESS) rc = hpxhip_stream_synchronize(s);
+        auto give_back = [&pool, hb, db] {
+            pool.release_host_block(hb);
+            pool.release_block(db);
+        };
+        int rc = hpxhip_memcpy_async(db.dev, hb.dev, bytes, HPXHIP_H2D, s);
         if (rc != HPXHIP_SUCCESS) {
-            hpxhip_free(dev);
+            give_back();
             hip::detail::check(rc, "bulk_launch shape");
         }
         try {
             detail::launch(target_, detail::flat_grid(count), dim3(256), detail::bulk_body<V>{}, std::forward<F>(f),
-                           static_cast<V const*>(dev), count, std::forward<Ts>(ts)...);
+                           static_cast<V const*>(db.dev), count, std::forward<Ts>(ts)...);
         } catch (...) {
-            hpxhip_free(dev);
+            detail::on_stream_done(s, give_back);
             throw;
         }
-        hip::detail::check(hpxhip_free(dev), "bulk_launch shape");
+        detail::on_stream_done(s, give_back);
 #else
         static_assert(detail::dependent_false<F>, "bulk_launch of a device closure needs hipcc");
         (void)f;

@@ -453,6 +453,50 @@ detail::result_t<P, util::tagged_tuple<In1, In2, Out>> transform(P&& p, In1 firs
 
 // ------------------------------------------------------------ reductions
 namespace detail {
+// *out_dev <- init (op) conv(x_0) (op) ... over [first, first + n), queued on
+// t's stream (the library kernel for mapped functors, a kernel instantiated
+// for a device closure otherwise).
+template <typename T, typename TI, typename Op, typename Conv>
+void reduce_into(hip::target const& t, TI const* first, uint64_t n, T init, Op const& op, Conv const& conv,
+                 void* out_dev) {
+    if constexpr (tr::is_binop<Op> && tr::is_unary<Conv>) {
+        T s[2] = {};
+        tr::unary_t<Conv>::scalars(conv, s);
+        check(hpxhip_transform_reduce(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::unary_t<Conv>::kind, s, &init, first, n,
+                                      out_dev, t.stream(), nullptr, 0),
+              "transform_reduce");
+    } else {
+#if HPX_HAVE_HIP_DEVICE_CLOSURES
+        dev::reduce<T, false>(t, first, static_cast<TI const*>(nullptr), n, init, op, conv, out_dev);
+#else
+        no_device_mapping<Op>("transform_reduce");
+#endif
+    }
+}
+
+// [first, first + n) scanned into out, queued on t's stream; prefix_dev (a
+// device value, built-in operators only) replaces init when given.
+template <typename V, typename Op, typename Conv, typename T>
+void scan_into(hip::target const& t, V const* first, V* out, uint64_t n, Op const& op, Conv const& conv, T init,
+               V const* prefix_dev, bool inclusive) {
+    if constexpr (tr::is_binop<Op> && tr::is_unary<Conv>) {
+        V s[2] = {};
+        tr::unary_t<Conv>::scalars(conv, s);
+        V iv = static_cast<V>(init);
+        check(hpxhip_scan(dt<V>, tr::binop_t<Op>::kind, inclusive ? 1 : 0, tr::unary_t<Conv>::kind, s, &iv, prefix_dev,
+                          first, out, n, t.stream(), nullptr, 0),
+              inclusive ? "inclusive_scan" : "exclusive_scan");
+    } else {
+#if HPX_HAVE_HIP_DEVICE_CLOSURES
+        if (prefix_dev)
+            throw hpx::exception(HPXHIP_ERROR_UNSUPPORTED, "scan: a device prefix needs a built-in operator");
+        dev::scan(t, first, out, n, op, conv, init, inclusive);
+#else
+        no_device_mapping<Op>(inclusive ? "inclusive_scan" : "exclusive_scan");
+#endif
+    }
+}
+
 template <typename T, typename P, typename It, typename Op, typename Conv>
 result_t<P, T> reduce_impl(P&& p, It first, It last, T init, Op&& op, Conv&& conv) {
     if constexpr (is_seg<It>) {
@@ -463,21 +507,7 @@ result_t<P, T> reduce_impl(P&& p, It first, It last, T init, Op&& op, Conv&& con
     using TI = value_t<It>;
     auto const& t = target_of(p, first);
     auto slot = t.make_result_slot();
-    if constexpr (tr::is_binop<Op> && tr::is_unary<Conv>) {
-        T s[2] = {};
-        tr::unary_t<Conv>::scalars(conv, s);
-        check(hpxhip_transform_reduce(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::unary_t<Conv>::kind, s, &init,
-                                      first.device_ptr(), distance(first, last), slot.device(), t.stream(), nullptr,
-                                      0),
-              "transform_reduce");
-    } else {
-#if HPX_HAVE_HIP_DEVICE_CLOSURES
-        dev::reduce<T, false>(t, static_cast<TI const*>(first.device_ptr()), static_cast<TI const*>(nullptr),
-                              distance(first, last), init, op, conv, slot.device());
-#else
-        no_device_mapping<Op>("transform_reduce");
-#endif
-    }
+    reduce_into<T>(t, static_cast<TI const*>(first.device_ptr()), distance(first, last), init, op, conv, slot.device());
     fetch_slot(t, slot, sizeof(T), "reduce result");
     return finish_slot<T>(p, t, std::move(slot), load_value<T>{});
     }
@@ -562,20 +592,8 @@ result_t<P, Out> scan_impl(P&& p, In first, In last, Out dest, Op&& op, Conv&& c
     static_assert(std::is_same<V, value_t<Out>>::value, "scan: input and output element types must match");
     auto const& t = target_of(p, first);
     uint64_t n = distance(first, last);
-    if constexpr (tr::is_binop<Op> && tr::is_unary<Conv>) {
-        V s[2] = {};
-        tr::unary_t<Conv>::scalars(conv, s);
-        V iv = static_cast<V>(init);
-        check(hpxhip_scan(dt<V>, tr::binop_t<Op>::kind, inclusive ? 1 : 0, tr::unary_t<Conv>::kind, s, &iv, nullptr,
-                          first.device_ptr(), dest.device_ptr(), n, t.stream(), nullptr, 0),
-              inclusive ? "inclusive_scan" : "exclusive_scan");
-    } else {
-#if HPX_HAVE_HIP_DEVICE_CLOSURES
-        dev::scan(t, static_cast<V const*>(first.device_ptr()), dest.device_ptr(), n, op, conv, init, inclusive);
-#else
-        no_device_mapping<Op>(inclusive ? "inclusive_scan" : "exclusive_scan");
-#endif
-    }
+    scan_into(t, static_cast<V const*>(first.device_ptr()), dest.device_ptr(), n, op, conv, init,
+              static_cast<V const*>(nullptr), inclusive);
     Out end = dest + static_cast<std::ptrdiff_t>(n);
     return finish<Out>(p, t, [end] { return end; });
     }

@@ -15,12 +15,12 @@
 //
 // Every segment's work runs on its partition's target stream as a task
 // (par(task) on the partition's device iterators), so segments on different
-// GPUs run concurrently; the tiny per-segment results (reduce values, scan
-// totals) are combined on the host in segment order, as the reference does
-// with futures on the calling locality.  Under a task policy reduce returns
-// a future composed from the segment futures (when_all + then); the scans
-// need the totals before the second step and return a ready future after
-// the device work is done.
+// GPUs run concurrently.  The per-segment results of reduce and the scans
+// (segment totals, carries) stay on the devices: they are peer-copied to the
+// first segment's target, folded there in segment order (hpxhip_fold /
+// hpxhip_fold_exclusive) and the carries copied back, all stream-ordered with
+// events -- no host round trip, so a task policy returns before the device
+// work is done and its future completes from the streams.
 #pragma once
 
 #include <hpx/parallel/algorithms.hpp>
@@ -176,66 +176,138 @@ typename util::detail::algorithm_result<P, util::tagged_tuple<In1, In2, Out>>::t
     return finish<R, P>(std::move(fs), [e1, e2, eo] { return R{e1, e2, eo}; });
 }
 
+// ------------------------------------------------- segment totals on device
+// Segment j's total S_j = id (op) conv(x) ... is reduced on its partition's
+// target into a result slot there and copied (peer copy across GPUs) into
+// totals[j] of a block on the first segment's target t0, whose stream then
+// waits for every segment -- nothing travels through the host.
+template <typename V, typename PV, typename Op, typename Conv>
+struct segment_totals {
+    std::vector<segment> segs;
+    compute::hip::target const* t0 = nullptr;
+    compute::hip::detail::device_pool* pool0 = nullptr;
+    compute::hip::detail::device_pool::block_ref blk{};
+    std::vector<compute::hip::result_slot> slots;  // per segment: [0] total, [16] carry
+
+    V* totals() const { return static_cast<V*>(blk.dev); }
+    V* carries() const { return reinterpret_cast<V*>(static_cast<char*>(blk.dev) + 16 * ((segs.size() * sizeof(V) + 15) / 16)); }
+
+    segment_totals(PV& pv, std::size_t a, std::size_t b, Op const& op, Conv const& conv) : segs(segments_of(pv, a, b)) {
+        namespace hd = compute::hip::detail;
+        if (segs.empty()) return;
+        t0 = &pv.get_partition(segs[0].part).target;
+        pool0 = &hd::device_pool::get(t0->device());
+        const std::size_t nseg = segs.size();
+        blk = pool0->acquire_block(16 * ((nseg * sizeof(V) + 15) / 16) + (nseg + 1) * sizeof(V));
+        const V id = identity_of<V, typename std::decay<Op>::type>();
+        for (std::size_t j = 0; j < nseg; ++j) {
+            auto const& s = segs[j];
+            auto& part = pv.get_partition(s.part);
+            auto const& tj = part.target;
+            slots.push_back(tj.make_result_slot());
+            detail::reduce_into<V>(tj, part.data->data() + s.lo, s.hi - s.lo, id, op, conv, slots[j].device());
+            copy_value(totals() + j, *t0, slots[j].device(), tj, tj.stream());
+            hd::stream_after(t0->stream(), tj.stream());
+        }
+    }
+    // dst (on `dt`'s device) <- src (on `st`'s device), sizeof(V) bytes on `s`
+    static void copy_value(void* dst, compute::hip::target const& dt, void const* src, compute::hip::target const& st,
+                           hpxhip_stream s) {
+        namespace hd = compute::hip::detail;
+        if (dt.device() == st.device())
+            hd::check(hpxhip_memcpy_async(dst, src, sizeof(V), HPXHIP_D2D, s), "segment value copy");
+        else
+            hd::check(hpxhip_memcpy_peer_async(dst, dt.device(), src, st.device(), sizeof(V), s),
+                      "segment value peer copy");
+    }
+    // the block returns to its pool once `s` has passed the work queued so far
+    void release_block_after(hpxhip_stream s) {
+        auto* pool = pool0;
+        auto b = blk;
+        compute::hip::detail::on_stream_done(s, [pool, b] { pool->release_block(b); });
+    }
+};
+
 // --------------------------------------------------------------- reduce
+// segmented_algorithms/reduce.hpp:112-209: S_j per segment (no init), then
+// init (op) S_0 (op) ... in segment order -- folded on t0's device
+// (hpxhip_fold), the value returned through a result slot.
 template <typename T, typename P, typename It, typename Op, typename Conv>
-typename util::detail::algorithm_result<P, T>::type reduce(P&&, It first, It last, T init, Op&& op, Conv&& conv) {
+typename util::detail::algorithm_result<P, T>::type reduce(P&& p, It first, It last, T init, Op&& op, Conv&& conv) {
     auto& pv = first.container();
-    std::vector<hpx::future<T>> fs;
-    const T id = identity_of<T, typename std::decay<Op>::type>();
-    for (auto const& s : segments_of(pv, index_of(first), index_of(last))) {
-        auto& d = *pv.get_partition(s.part).data;
-        fs.push_back(hpx::parallel::transform_reduce(ex::par(ex::task), d.begin() + s.lo, d.begin() + s.hi, id, op,
-                                                     conv));
+    using PV = typename std::decay<decltype(pv)>::type;
+    static_assert(compute::hip::traits::is_binop<Op>,
+                  "segmented reduce: the segment-order combine runs on the device with a built-in operator");
+    segment_totals<T, PV, Op, Conv> st(pv, index_of(first), index_of(last), op, conv);
+    if (st.segs.empty()) {
+        if constexpr (task_policy<P>) return hpx::make_ready_future(init);
+        else return init;
     }
-    auto fold = [init, op](std::vector<hpx::future<T>>& v) {  // init (op) S_0 (op) ... (reduce.hpp:191-207)
-        T acc = init;
-        for (auto& f : v) acc = op(acc, f.get());
-        return acc;
-    };
-    if constexpr (task_policy<P>) {
-        return hpx::when_all(std::move(fs)).then([fold](auto& all) mutable {
-            auto v = all.get();
-            return fold(v);
-        });
-    } else {
-        return fold(fs);
-    }
+    auto const& t0 = *st.t0;
+    auto slot = t0.make_result_slot();
+    compute::hip::detail::check(hpxhip_fold(detail::dt<T>, compute::hip::traits::binop_t<Op>::kind, &init, st.totals(),
+                                            st.segs.size(), slot.device(), t0.stream()),
+                                "segmented reduce fold");
+    detail::fetch_slot(t0, slot, sizeof(T), "segmented reduce result");
+    st.release_block_after(t0.stream());
+    for (std::size_t j = 0; j < st.segs.size(); ++j)  // each slot returns to its pool on its own stream
+        pv.get_partition(st.segs[j].part).target.template async_result<void>([](unsigned char const*) {},
+                                                                              std::move(st.slots[j]));
+    return detail::finish_slot<T>(p, t0, std::move(slot), detail::load_value<T>{});
 }
 
 // ----------------------------------------------------------------- scans
+// segmented_algorithms/detail/scan.hpp:527-696: 1. segment totals, 2. the
+// carries in segment order (carry_0 = init, carry_{j+1} = carry_j (op) S_j:
+// hpxhip_fold_exclusive on t0), 3. each segment scanned on its own target
+// from its carry, read on the device (hpxhip_scan's prefix).  All of it is
+// queued without a host round trip; under a task policy the future is ready
+// when every segment's scan is.
 template <typename P, typename In, typename Out, typename Op, typename Conv, typename T>
 typename util::detail::algorithm_result<P, Out>::type scan(P&&, In first, In last, Out dest, Op&& op, Conv&& conv,
                                                           T init, bool inclusive) {
+    namespace hd = compute::hip::detail;
     auto& pv = first.container();
     auto& pd = dest.container();
     require_same_layout(pv, index_of(first), pd, index_of(dest), "segmented scan");
-    using V = typename std::decay<decltype(pv)>::type::value_type;
-    const auto segs = segments_of(pv, index_of(first), index_of(last));
-    // 1. segment totals (detail/scan.hpp:64-134), all segments at once
-    std::vector<hpx::future<V>> totals;
-    const V id = identity_of<V, typename std::decay<Op>::type>();
-    for (auto const& s : segs) {
-        auto& d = *pv.get_partition(s.part).data;
-        totals.push_back(
-            hpx::parallel::transform_reduce(ex::par(ex::task), d.begin() + s.lo, d.begin() + s.hi, id, op, conv));
-    }
-    // 2. carries in segment order; 3. each segment scanned from its carry
-    using LO = typename std::decay<decltype(pd.get_partition(0).data->begin())>::type;
-    std::vector<hpx::future<LO>> fs;
-    V carry = static_cast<V>(init);
-    for (std::size_t i = 0; i < segs.size(); ++i) {
-        auto const& s = segs[i];
-        auto& d = *pv.get_partition(s.part).data;
-        auto& o = *pd.get_partition(s.part).data;
-        const V total = totals[i].get();
-        fs.push_back(hpx::parallel::detail::scan_impl(ex::par(ex::task), d.begin() + s.lo, d.begin() + s.hi,
-                                                      o.begin() + s.lo, op, conv, carry, inclusive));
-        carry = op(carry, total);
-    }
-    for (auto& f : fs) f.get();
+    using PV = typename std::decay<decltype(pv)>::type;
+    using V = typename PV::value_type;
+    static_assert(compute::hip::traits::is_binop<Op>,
+                  "segmented scan: the carries are folded on the device with a built-in operator");
     Out end = dest + (last - first);
-    if constexpr (task_policy<P>) return hpx::make_ready_future(end);
-    else return end;
+    segment_totals<V, PV, Op, Conv> st(pv, index_of(first), index_of(last), op, conv);
+    if (st.segs.empty()) {
+        if constexpr (task_policy<P>) return hpx::make_ready_future(end);
+        else return end;
+    }
+    auto const& t0 = *st.t0;
+    const V iv = static_cast<V>(init);
+    hd::check(hpxhip_fold_exclusive(detail::dt<V>, compute::hip::traits::binop_t<Op>::kind, &iv, st.totals(),
+                                    st.segs.size(), st.carries(), t0.stream()),
+              "segmented scan carries");
+    std::vector<hpx::future<void>> fs;
+    for (std::size_t j = 0; j < st.segs.size(); ++j) {
+        auto const& s = st.segs[j];
+        auto& part = pv.get_partition(s.part);
+        auto const& tj = part.target;
+        V* carry = reinterpret_cast<V*>(static_cast<char*>(st.slots[j].device()) + 16);
+        hd::stream_after(tj.stream(), t0.stream());
+        st.copy_value(carry, tj, st.carries() + j, t0, tj.stream());
+        auto& o = *pd.get_partition(s.part).data;
+        detail::scan_into(tj, part.data->data() + s.lo, o.data() + s.lo, s.hi - s.lo, op, conv, iv, carry, inclusive);
+        hd::stream_after(t0.stream(), tj.stream());  // t0 releases the carries block after every copy
+        fs.push_back(tj.template async_result<void>([](unsigned char const*) {}, std::move(st.slots[j])));
+    }
+    st.release_block_after(t0.stream());
+    if constexpr (task_policy<P>) {
+        return hpx::when_all(std::move(fs)).then([end](auto& all) {
+            for (auto& f : all.get()) f.get();  // rethrows a segment's error
+            return end;
+        });
+    } else {
+        for (auto& f : fs) f.get();
+        return end;
+    }
 }
 
 // ------------------------------------------------------------------ copy

@@ -290,6 +290,11 @@ int hpxhip_transform_reduce_binary(int in_dtype, int acc_dtype, int red_op, int 
    (segmented_algorithms/reduce.hpp:191-207, detail/scan.hpp:667-677). */
 int hpxhip_fold(int dtype, int op, const void* init, const void* values_dev, uint64_t count,
                 void* out_dev, hpxhip_stream stream);
+/* Every prefix of the same fold: out_dev[0] = init, out_dev[j + 1] = out_dev[j] (op) v[j]
+   (count + 1 values) -- the carries of a segmented scan in segment order
+   (segmented_algorithms/detail/scan.hpp:646-677), folded on the device. */
+int hpxhip_fold_exclusive(int dtype, int op, const void* init, const void* values_dev, uint64_t count,
+                          void* out_dev, hpxhip_stream stream);
 
 /* -------------------------------------------------------------- scans */
 /* inclusive_scan.hpp:288 / exclusive_scan.hpp:292 (+ transform_*_scan with

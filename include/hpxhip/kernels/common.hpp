@@ -274,21 +274,38 @@ enum : int {
     DPP_ROW_BCAST31 = 0x143,
 };
 
-// Inclusive wave64 scan: lane l receives x_0 (+) ... (+) x_l.
+// Inclusive wave64 scan: lane l receives x_0 (+) ... (+) x_l, the lower
+// lanes always the left operand (a non-commutative associative op -- a user
+// operator of the C++ layer -- scans in lane order).
 // 7 DPP steps: three row_shr from the original value, row_shr:4/8 inside the
 // 16-lane rows, then row_bcast:15/31 across rows.
 template <typename T, typename Op>
 __device__ __forceinline__ T wave_inclusive_scan(T x, Op op) {
     const T id = Op::template identity<T>();
-    T s = op(x, dpp<DPP_ROW_SHR1>(id, x));
-    s = op(s, dpp<DPP_ROW_SHR2>(id, x));
-    s = op(s, dpp<DPP_ROW_SHR3>(id, x));
-    s = op(s, dpp<DPP_ROW_SHR4, 0xf, 0xe>(id, s));
-    s = op(s, dpp<DPP_ROW_SHR8, 0xf, 0xc>(id, s));
-    s = op(s, dpp<DPP_ROW_BCAST15, 0xa, 0xf>(id, s));
-    s = op(s, dpp<DPP_ROW_BCAST31, 0xc, 0xf>(id, s));
+    T s = op(dpp<DPP_ROW_SHR1>(id, x), x);
+    s = op(dpp<DPP_ROW_SHR2>(id, x), s);
+    s = op(dpp<DPP_ROW_SHR3>(id, x), s);
+    s = op(dpp<DPP_ROW_SHR4, 0xf, 0xe>(id, s), s);
+    s = op(dpp<DPP_ROW_SHR8, 0xf, 0xc>(id, s), s);
+    s = op(dpp<DPP_ROW_BCAST15, 0xa, 0xf>(id, s), s);
+    s = op(dpp<DPP_ROW_BCAST31, 0xc, 0xf>(id, s), s);
     return s;
 }
+
+// op with its operands swapped (same identity): a fold over lanes that hold
+// values in DECREASING index order (the look-back window) in index order.
+template <typename Op>
+struct flipped_op {
+    Op op;
+    template <typename T>
+    __device__ __forceinline__ T operator()(T a, T b) const {
+        return op(b, a);
+    }
+    template <typename T>
+    __host__ __device__ static constexpr T identity() {
+        return Op::template identity<T>();
+    }
+};
 
 // Exclusive companion of an inclusive wave scan (lane 0 gets the identity).
 template <typename T, typename Op>

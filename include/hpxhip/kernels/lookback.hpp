@@ -141,8 +141,10 @@ struct tile_state {
                 if (found) break;  // wave-uniform
                 const uint64_t inclusive_lanes = __ballot(f[k] == TILE_INCLUSIVE);
                 const int first = inclusive_lanes ? __builtin_ctzll(inclusive_lanes) : kWave;
+                // lane l holds tile pred - l - 64k: fold the window oldest
+                // first, then put it before the nearer tiles already folded
                 T w = lane > first ? id : v[k];
-                const T s = wave_reduce(w, op);
+                const T s = wave_reduce(w, flipped_op<Op>{op});
                 excl = op(s, excl);
                 found = first < kWave;
             }

@@ -1,25 +1,46 @@
-"""Fused stencil timing through the C ABI: 16 steps per pass over 2^30 points
-(hpxhip_stencil_heat_steps, periodic ring: halos taken from the ring's ends)."""
-import ctypes, os, sys
+"""1d_stencil heat at 2^32 points (one GPU, the partitioned solver): time of
+100 steps after 100 warm-up steps, ramp U0[i] = i vs random U0 = unit(seed),
+and the fused single-GPU run on the same two states.  usage:
+python scripts/stencil_probe.py [logn]"""
+import ctypes
+import os
+import sys
+import time
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from hpx_amd import _lib as L
-lib = L.load(); vp = ctypes.c_void_p
-st = vp(); L.check(lib.hpxhip_stream_create(0, ctypes.byref(st)))
-N = 1 << int(os.environ.get("LOGN", "30"))
-def alloc(b):
-    p = vp(); L.check(lib.hpxhip_malloc(0, ctypes.byref(p), b)); return p
-a, b = alloc(8 * N), alloc(8 * N)
-L.check(lib.hpxhip_generate(L.F64, L.GEN_UNIT, 1, 0, 0, a, N, st))
-e0, e1 = vp(), vp(); lib.hpxhip_event_create(ctypes.byref(e0)); lib.hpxhip_event_create(ctypes.byref(e1))
-for S in (8, 16):
-    lh = vp(a.value + 8 * (N - S))
-    best = 1e9
-    for _ in range(6):
-        lib.hpxhip_event_record(e0, st)
-        L.check(lib.hpxhip_stencil_heat_steps(a, b, ctypes.c_uint64(N), ctypes.c_uint64(0), ctypes.c_uint64(N), lh, a,
-                                              S, ctypes.c_double(0.5), ctypes.c_double(1.0), ctypes.c_double(1.0), st))
-        lib.hpxhip_event_record(e1, st)
-        L.check(lib.hpxhip_event_synchronize(e1))
-        ms = ctypes.c_float(); lib.hpxhip_event_elapsed_ms(e0, e1, ctypes.byref(ms)); best = min(best, ms.value)
-    print(f"fused {S:2d} steps over 2^{N.bit_length()-1} points: {best:.3f} ms = {best / S:.3f} ms/step, "
-          f"{N * S / best / 1e9:.2f} T point-steps/s", flush=True)
+import numpy as np  # noqa: E402
+
+import hpx_amd as hpx  # noqa: E402
+from hpx_amd import _lib as L  # noqa: E402
+from hpx_amd import segmented as S  # noqa: E402
+
+logn = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+nx, nt = 1 << logn, 100
+t = hpx.target(0)
+comm = S.LocalComm(t)
+for init in (None, ("unit", 0xC0FFEE), None, ("unit", 0xC0FFEE)):
+    hs = S.heat_solver(nx, comm, t, init=init)
+    hs.do_work(nt)
+    hs.synchronize()
+    t0 = time.perf_counter()
+    hs.do_work(nt)
+    hs.synchronize()
+    el = time.perf_counter() - t0
+    print(f"heat_solver {'ramp' if init is None else 'random'}: {1e3 * el:.2f} ms for {nt} steps", flush=True)
+    for v in hs.U + [hs.H]:
+        v.free()
+for kind in (L.GEN_IOTA, L.GEN_UNIT, L.GEN_IOTA, L.GEN_UNIT):
+    a = hpx.vector(nx, dtype=np.float64, tgt=t)
+    b = hpx.vector(nx, dtype=np.float64, tgt=t)
+    L.call("hpxhip_generate_at", L.F64, kind, 0xC0FFEE, 0, 0, 0, ctypes.c_void_p(a.data()), nx, t.stream)
+    which = ctypes.c_int()
+    for rep in range(2):
+        t.synchronize()
+        t0 = time.perf_counter()
+        L.call("hpxhip_stencil_heat_run_fused", ctypes.c_void_p(a.data()), ctypes.c_void_p(b.data()), nx, nt,
+               ctypes.c_double(0.5), ctypes.c_double(1.0), ctypes.c_double(1.0), ctypes.byref(which), t.stream)
+        t.synchronize()
+        el = time.perf_counter() - t0
+    print(f"heat_run_fused {'ramp' if kind == L.GEN_IOTA else 'random'}: {1e3 * el:.2f} ms for {nt} steps", flush=True)
+    a.free()
+    b.free()

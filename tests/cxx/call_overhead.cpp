@@ -93,11 +93,14 @@ int hpx_main(int, char**) {
     for (int rep = 0; rep < 3; ++rep) {
         hpxhip_generate(HPXHIP_U64, HPXHIP_GEN_BITS, 77 + rep, 0, 0, keys.data(), nk, stream);
         const uint64_t sum0 = hpx::parallel::reduce(ex::par.on(exec), keys.begin(), keys.end(), uint64_t(0));
+        // one policy object: its executor's target (a copy of exec's, so its
+        // own stream, cuda_target.cpp:203-211) orders the three calls
+        auto tpol = ex::par(ex::task).on(exec);
         const auto t0 = std::chrono::steady_clock::now();
-        auto fs = hpx::parallel::sort(ex::par(ex::task).on(exec), keys.begin(), keys.end());
+        auto fs = hpx::parallel::sort(tpol, keys.begin(), keys.end());
         const auto t1 = std::chrono::steady_clock::now();
-        auto fr = hpx::parallel::reduce(ex::par(ex::task).on(exec), keys.begin(), keys.end(), uint64_t(0));
-        auto fo = hpx::parallel::is_sorted(ex::par(ex::task).on(exec), keys.begin(), keys.end());
+        auto fr = hpx::parallel::reduce(tpol, keys.begin(), keys.end(), uint64_t(0));
+        auto fo = hpx::parallel::is_sorted(tpol, keys.begin(), keys.end());
         HPX_TEST(fs.get() == keys.end());
         HPX_TEST_EQ(fr.get(), sum0);
         HPX_TEST(fo.get());

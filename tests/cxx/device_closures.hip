@@ -112,6 +112,16 @@ struct bulk_test {
     int base;
     HPX_HOST_DEVICE void operator()(int i) { out[i - base] = 2 * i + 1; }
 };
+// slow on purpose: ~1000 dependent steps per element
+struct bulk_slow {
+    int* out;
+    HPX_HOST_DEVICE static int expect(int i) {
+        uint32_t x = uint32_t(i);
+        for (int k = 0; k < 1000; ++k) x = x * 1664525u + 1013904223u;
+        return int(x >> 1);
+    }
+    HPX_HOST_DEVICE void operator()(int i) { out[i - 3] = expect(i); }
+};
 struct bulk_test_args {
     HPX_HOST_DEVICE void operator()(int i, int* out, int base, int add) { out[i - base] = i + add; }
 };
@@ -150,6 +160,22 @@ void test_executor(Executor& exec, hip::target const& t, std::mt19937& gen, char
     hpx::when_all(ex::bulk_async_execute(exec, bulk_test_args{}, v, out.data(), base, 7)).get();
     h = to_host(out);
     for (std::size_t i = 0; i != v.size(); ++i) HPX_TEST_EQ(h[i], v[i] + 7);
+
+    // 10^6-element bulk_async_execute: the shape is staged (pinned, pooled)
+    // and the call returns while the device still works; every element ran
+    // exactly once, the shape's first element included
+    std::vector<int> big(1000000);
+    std::iota(big.begin(), big.end(), 3);
+    hpx::compute::vector<int, hip::allocator<int>> bo(big.size(), -1, alloc);
+    auto fs = ex::bulk_async_execute(exec, bulk_slow{bo.data()}, big);
+    bool pending = false;
+    for (auto& f : fs) pending = pending || !f.is_ready();
+    HPX_TEST(pending);  // ~10^9 device iterations: not done at return
+    big.assign(big.size(), 0);  // the caller's shape may go away at once
+    hpx::when_all(std::move(fs)).get();
+    std::vector<int> hb = to_host(bo);
+    for (std::size_t i = 0; i != hb.size(); ++i)
+        if (!HPX_TEST_EQ(hb[i], bulk_slow::expect(int(i) + 3))) break;
 }
 
 // ------------------------------------------------ concurrent_executor algorithms

@@ -91,6 +91,31 @@ void test_scans(std::size_t size, hip::target_distribution_policy const& policy)
     hpx::parallel::exclusive_scan(ex::par, in.begin(), in.end(), out.begin(), T(50));
     HPX_TEST(to_host(out) == xver);
 
+    // task policies (inline temporaries), three algorithms in flight at once:
+    // the totals and carries stay on the devices, each future completes from
+    // the segments' streams
+    pvec<T> out2(size, policy);
+    hpx::parallel::fill(ex::par, out.begin(), out.end(), T(0));
+    auto f1 = hpx::parallel::inclusive_scan(ex::par(ex::task), in.begin(), in.end(), out.begin(), std::plus<T>(), T(0));
+    auto f2 =
+        hpx::parallel::exclusive_scan(ex::par(ex::task), in.begin(), in.end(), out2.begin(), T(50), std::plus<T>());
+    auto f3 = hpx::parallel::reduce(ex::par(ex::task), in.begin(), in.end(), T(7), std::plus<T>());
+    HPX_TEST(f2.get() == out2.end());
+    HPX_TEST(f1.get() == out.end());
+    HPX_TEST_EQ(f3.get(), T(T(7) + ver.back()));
+    HPX_TEST(to_host(out) == ver);
+    HPX_TEST(to_host(out2) == xver);
+    // a sub-range whose ends are inside partitions
+    if (size > 20) {
+        std::vector<T> sub(size - 13);
+        std::partial_sum(h.begin() + 5, h.end() - 8, sub.begin());
+        hpx::parallel::inclusive_scan(ex::par(ex::task), in.begin() + 5, in.end() - 8, out.begin() + 5, std::plus<T>(),
+                                      T(0))
+            .get();
+        std::vector<T> got = to_host(out);
+        HPX_TEST(std::equal(sub.begin(), sub.end(), got.begin() + 5));
+    }
+
     // in place (inclusive_scan_tests_inplace_with_policy)
     hpx::parallel::inclusive_scan(ex::par, in.begin(), in.end(), in.begin(), std::plus<T>(), T(0));
     HPX_TEST(to_host(in) == ver);
