@@ -442,6 +442,8 @@ class target {
         std::function<void(unsigned char const*)> on_ready;
     };
 
+    explicit target(std::shared_ptr<handle> h) noexcept : h_(std::move(h)) {}
+
 public:
     target() : target(0) {}
     explicit target(int device) : h_(std::make_shared<handle>()) { h_->device = device; }
@@ -454,8 +456,18 @@ public:
         }
         return *this;
     }
-    target(target&&) = default;
-    target& operator=(target&&) = default;
+    // A move shares the handle (same stream) instead of leaving the source
+    // without one: a moved-from target stays usable (device(), stream(),
+    // synchronize()), and iterators that share the handle stay valid.
+    target(target&& o) noexcept : h_(o.h_) {}
+    target& operator=(target&& o) noexcept {
+        h_ = o.h_;
+        return *this;
+    }
+    // A view of the same handle and stream (not a copy: no new stream).
+    // Device iterators hold one, so they do not point into the object that
+    // handed them out (a vector moved after begin() was taken).
+    static target shared(target const& o) noexcept { return target(o.h_); }
 
     struct native_handle_type {
         handle* h;
@@ -616,7 +628,7 @@ public:
 template <typename T>
 class value_proxy {
     T* p_;
-    hip::target const* t_;
+    hip::target const* t_;  // the iterator's target view, alive while the proxy is used
 
 public:
     value_proxy(T* p, hip::target const* t) : p_(p), t_(t) {}
@@ -634,10 +646,13 @@ public:
     friend std::ostream& operator<<(std::ostream& os, value_proxy const& v) { return os << T(v); }
 };
 
+// Holds a view of its container's target handle (target::shared), not a
+// pointer to the container's target object: iterators stay valid when the
+// container is moved, as std::vector's do, and outlive the moved-from object.
 template <typename T>
 class device_iterator {
     T* p_ = nullptr;
-    hip::target const* t_ = nullptr;
+    hip::target t_;  // default: device 0, no stream until one is asked for
 
 public:
     using iterator_category = std::random_access_iterator_tag;
@@ -648,12 +663,12 @@ public:
     using target_type = hip::target;
 
     device_iterator() = default;
-    device_iterator(T* p, hip::target const* t) : p_(p), t_(t) {}
+    device_iterator(T* p, hip::target const& t) : p_(p), t_(hip::target::shared(t)) {}
     T* device_ptr() const { return p_; }
-    hip::target const& target() const { return *t_; }
+    hip::target const& target() const { return t_; }
 
-    reference operator*() const { return reference(p_, t_); }
-    reference operator[](difference_type i) const { return reference(p_ + i, t_); }
+    reference operator*() const { return reference(p_, &t_); }
+    reference operator[](difference_type i) const { return reference(p_ + i, &t_); }
     device_iterator& operator++() { ++p_; return *this; }
     device_iterator operator++(int) { auto r = *this; ++p_; return r; }
     device_iterator& operator--() { --p_; return *this; }
@@ -702,9 +717,22 @@ public:
     }
     vector(vector const&) = delete;
     vector& operator=(vector const&) = delete;
-    vector(vector&& o) noexcept : alloc_(o.alloc_), size_(o.size_), data_(o.data_) {
+    // the allocator (and its target's handle) moves with the data: iterators
+    // taken before the move keep the same target and stream
+    vector(vector&& o) noexcept : alloc_(std::move(o.alloc_)), size_(o.size_), data_(o.data_) {
         o.data_ = nullptr;
         o.size_ = 0;
+    }
+    vector& operator=(vector&& o) noexcept {
+        if (this != &o) {
+            if (data_) alloc_.deallocate(data_, size_);
+            alloc_ = std::move(o.alloc_);
+            size_ = o.size_;
+            data_ = o.data_;
+            o.data_ = nullptr;
+            o.size_ = 0;
+        }
+        return *this;
     }
     ~vector() {
         if (data_) alloc_.deallocate(data_, size_);
@@ -716,8 +744,8 @@ public:
     T* device_data() const { return data_; }
     T* data() const { return data_; }
     allocator_type const& get_allocator() const { return alloc_; }
-    iterator begin() const { return iterator(data_, &alloc_.target()); }
-    iterator end() const { return iterator(data_ + size_, &alloc_.target()); }
+    iterator begin() const { return iterator(data_, alloc_.target()); }
+    iterator end() const { return iterator(data_ + size_, alloc_.target()); }
     hip::value_proxy<T> operator[](size_type i) const { return hip::value_proxy<T>(data_ + i, &alloc_.target()); }
 };
 

@@ -28,16 +28,18 @@ namespace scan_detail {
 constexpr int kThreads = 1024;
 constexpr int kRounds = 16;
 
-// Rounds per launch variant: 16 where the kernel fits 128 VGPRs without
-// spilling (aligned integer scans); the FP scans (no reassociation, DPP moves
-// not fused into the 64-bit FP adds) and the element-wise unaligned path
-// spill at 16 and use kRoundsFP / 8.
-constexpr int kRoundsFP = 12;
+// Rounds per launch variant: 16 for aligned integer and double scans (r03:
+// double had spilled at 16 and ran 12 rounds -- 2.83 ms for 2^30 f64 --
+// until the deferred round carry (DEFER below) cut its temporaries: 121
+// VGPRs at 16 rounds, 2.68-2.69 ms, profiles/r03_ubench_scan7.log); float
+// (four values and their lane-local scan per vector) still spills at 16 and
+// keeps 12; the element-wise unaligned path uses 8.
+constexpr int kRoundsF32 = 12;
 template <typename T, bool ALIGNED>
 constexpr int rounds_for() {
     if constexpr (!ALIGNED) return 8;
-    else if constexpr (std::is_integral_v<T>) return kRounds;
-    else return kRoundsFP;
+    else if constexpr (std::is_integral_v<T> || sizeof(T) == 8) return kRounds;
+    else return kRoundsF32;
 }
 
 template <typename T, int ROUNDS = kRounds, int THREADS = kThreads>
@@ -78,7 +80,7 @@ __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& 
 // layer's device closures): conv maps T -> X, unwrap_value X -> T.
 template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED, int ROUNDS = kRounds,
           int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false, int LBK = 1,
-          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = true, typename X = T>
+          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = true, typename X = T, bool DEFER = std::is_floating_point_v<X> && sizeof(X) == 8>
 __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, X init,
                                                    const X* prefix_dev, uint32_t* counter, tile_state<X> st) {
     constexpr int V = 16 / sizeof(T);
@@ -143,7 +145,18 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
     }
 
     // ---- per-round lane scan + wave scan; x becomes the wave-local result
+    // DEFER: x[r] = (lane-exclusive prefix within round r) (op) local and the
+    // round totals stay wave-uniform (readlane -> SGPRs); the carry of the
+    // rounds before r is folded in only at the store.  Each round's scan then
+    // finishes without the serial carry chain, so the compiler keeps 4 B of
+    // temporaries per element instead of 6 (it had hoisted every round's wave
+    // scan above the chain and held x, run and the shifted scan of each
+    // round: f64 at 16 rounds spilled 24 VGPRs).  The regrouping keeps the
+    // left-to-right order of the operands (non-commutative user ops).
+    // Default for double only: int64 measured the same either way (2.68-2.70
+    // ms), float at 12 rounds spills 4 VGPRs with it and none without.
     X carry = id;
+    X tr[DEFER ? ROUNDS : 1];
 #pragma unroll
     for (int r = 0; r < ROUNDS; ++r) {
         X local[V];
@@ -156,10 +169,20 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
         }
         const X incl = wave_inclusive_scan(run, op);
         const X excl = wave_shift_right<X, Op>(incl);
-        const X pre = op(carry, excl);
+        if constexpr (DEFER) {
 #pragma unroll
-        for (int e = 0; e < V; ++e) x[r][e] = op(pre, local[e]);
-        carry = op(carry, readlane(incl, kWave - 1));
+            for (int e = 0; e < V; ++e) x[r][e] = op(excl, local[e]);
+            tr[r] = readlane(incl, kWave - 1);
+        } else {
+            const X pre = op(carry, excl);
+#pragma unroll
+            for (int e = 0; e < V; ++e) x[r][e] = op(pre, local[e]);
+            carry = op(carry, readlane(incl, kWave - 1));
+        }
+    }
+    if constexpr (DEFER) {
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) carry = op(carry, tr[r]);
     }
     if constexpr (!EARLY) {
         if (lane == 0) s_wave_total[wave] = carry;
@@ -169,25 +192,29 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
     __syncthreads();
     const X pre = s_wave_total[wave];
 
-    // ---- store
+    // ---- store (DEFER: round r adds the carry of rounds < r here)
+    X rc = pre;
     if (ALIGNED && full) {
         VT* dst = reinterpret_cast<VT*>(out + wbase);
 #pragma unroll
         for (int r = 0; r < ROUNDS; ++r) {
             VT y;
 #pragma unroll
-            for (int e = 0; e < V; ++e) y.v[e] = unwrap_value(op(pre, x[r][e]));
+            for (int e = 0; e < V; ++e) y.v[e] = unwrap_value(op(DEFER ? rc : pre, x[r][e]));
+            if constexpr (DEFER) rc = op(rc, tr[r]);
             if constexpr (NT_STORE) st_stream(&dst[r * kWave + lane], y);
             else dst[r * kWave + lane] = y;
         }
     } else {
 #pragma unroll
-        for (int r = 0; r < ROUNDS; ++r)
+        for (int r = 0; r < ROUNDS; ++r) {
 #pragma unroll
             for (int e = 0; e < V; ++e) {
                 const uint64_t i = wbase + (static_cast<uint64_t>(r) * kWave + lane) * V + e;
-                if (i < n) out[i] = unwrap_value(op(pre, x[r][e]));
+                if (i < n) out[i] = unwrap_value(op(DEFER ? rc : pre, x[r][e]));
             }
+            if constexpr (DEFER) rc = op(rc, tr[r]);
+        }
     }
 }
 

@@ -6,6 +6,7 @@
 //
 // Built against include/ and hpx_amd/libhpxhip.so by `make cxxtests`; run by
 // tests/test_cxx_api.py under pytest -m gpu.
+#include <memory>
 #include <hpx/hpx.hpp>
 #include <hpx/hpx_init.hpp>
 #include <hpx/util/lightweight_test.hpp>
@@ -90,6 +91,34 @@ void test_targets_and_vector() {
     auto moved = std::move(v);
     HPX_TEST_EQ(moved.size(), std::size_t(1000));
     HPX_TEST_EQ(double(moved[3]), 7.0);
+
+    // ownership edge cases: a moved-from target keeps a usable handle (it
+    // shares the stream), iterators taken before a vector is moved stay valid
+    // after the moved-from vector is gone, and move assignment frees the old
+    // allocation and takes the new one with its target
+    hpx::compute::hip::target t1;
+    hpx::compute::hip::target t2(std::move(t1));
+    HPX_TEST_EQ(t1.device(), t2.device());
+    HPX_TEST(t1.stream() != nullptr);
+    HPX_TEST(t1.stream() == t2.stream());
+    t1.synchronize();
+    hpx::compute::hip::target t3;
+    t3 = std::move(t2);
+    HPX_TEST(t3.stream() == t1.stream());
+    using dvec = hpx::compute::vector<double, hpx::compute::hip::allocator<double>>;
+    auto pv = std::make_unique<dvec>(4096, 0.5, alloc);
+    auto b = pv->begin(), e = pv->end();
+    dvec w(std::move(*pv));
+    pv.reset();  // the moved-from vector (and its allocator object) is gone
+    HPX_TEST(b == w.begin() && e == w.end());
+    HPX_TEST(b.target().stream() == w.begin().target().stream());
+    HPX_TEST_EQ(hpx::parallel::reduce(ex::par, b, e, 0.0), 2048.0);
+    HPX_TEST_EQ(double(b[4095]), 0.5);
+    dvec u(8, 1.0, alloc);
+    u = std::move(w);
+    HPX_TEST_EQ(u.size(), std::size_t(4096));
+    HPX_TEST(w.size() == 0 && w.data() == nullptr);
+    HPX_TEST_EQ(hpx::parallel::reduce(ex::par, u.begin(), u.end(), 0.0), 2048.0);
 }
 
 void test_futures(executor_type& exec) {
