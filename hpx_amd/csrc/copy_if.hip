@@ -60,15 +60,20 @@ int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev,
     const uint64_t ntiles = ntiles_for<T, R>(n);
     HPXHIP_CHECK(hipMemsetAsync(ws, 0, align_up(kSlotsOff + ntiles * tile_state<SV>::bytes_per_tile(), 256), s));
     tile_state<SV> st{reinterpret_cast<uint64_t*>(ws + kSlotsOff), device_error_word(s)};
-    // Tile ids from the atomic counter: 2.33 ms vs 2.36 with blockIdx order
-    // for 2^30 int64 (profiles/r02_ubench_tile_order_ab.log).
-    constexpr bool kDynId = true;
+    // r03: the fixed-association look-back (tiles fold their group's
+    // published aggregates plus one group word, lookback.hpp) in blockIdx
+    // order: 2^30 int64 at 50 % hits 2.34 -> 2.20-2.21 ms, 2^31 int32 2.38 ->
+    // 2.30-2.32 (profiles/r03_ubench_copyif7.log).  With the variable-window
+    // look-back the atomic counter had been the faster order (2.33 vs 2.36,
+    // profiles/r02_ubench_tile_order_ab.log).
+    constexpr bool kDynId = false;
+    constexpr bool kFixed = true;
     // Aligned, with the 32-bit look-back state: at most 64 VGPRs (8 waves per SIMD),
     // so two workgroups share a CU.  4-byte elements compiled to 70 VGPRs
     // at the old bound (4 waves per SIMD) and ran one workgroup per CU:
     // int32 2^31 2.77 -> 2.38 ms (profiles/r02_ubench_copyif_occupancy.log).
     constexpr int kMinWaves = (std::is_same_v<SV, uint32_t> && ALIGNED) ? 8 : 4;
-    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId>), dim3(static_cast<unsigned>(ntiles)),
+    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId, false, 1, kFixed>), dim3(static_cast<unsigned>(ntiles)),
                        dim3(kThreads), 0, s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles,
                        prefix0);
     HPXHIP_CHECK_LAUNCH();

@@ -214,9 +214,11 @@ void copy_if_launch(compute::hip::target const& t, T const* in, T* out, uint64_t
     char* ws = static_cast<char*>(scratch(t, state, "copy_if scratch"));
     compute::hip::detail::check(hpxhip_memset_async(ws, 0, state, t.stream()), "copy_if scratch");
     K::tile_state<SV> st{reinterpret_cast<uint64_t*>(ws + 256), error_word(t)};
-    // tile ids from the counter (the shipped choice for copy_if, copy_if.hip);
-    // 4 waves per SIMD: a user predicate may need more than 64 VGPRs
-    hipLaunchKernelGGL((C::k_copy_if<T, P, ALIGNED, R, 4, 0, SV, true>), dim3(static_cast<unsigned>(ntiles)),
+    // blockIdx tile order with the fixed-association look-back (the shipped
+    // choice for copy_if, copy_if.hip); 4 waves per SIMD: a user predicate
+    // may need more than 64 VGPRs
+    hipLaunchKernelGGL((C::k_copy_if<T, P, ALIGNED, R, 4, 0, SV, false, false, 1, true>),
+                       dim3(static_cast<unsigned>(ntiles)),
                        dim3(C::kThreads), 0, stream_of(t), in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws),
                        st, ntiles, static_cast<const uint64_t*>(nullptr));
     launched("copy_if (device closure)");

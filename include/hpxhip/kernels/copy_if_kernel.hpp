@@ -34,7 +34,7 @@ using hit_word = std::conditional_t<(BITS <= 32), uint32_t, uint64_t>;
 // SV: tile-state value type (uint32_t halves the look-back granules; valid
 // while n < 2^32).
 template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4, int ABL = 0, typename SV = uint64_t,
-          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = false, int RPB = 1>
+          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = false, int RPB = 1, bool FIXED = false>
 __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out, uint64_t n, Pred pred,
                                                        uint64_t* count_dev, uint32_t* counter,
                                                        tile_state<SV> st, uint64_t ntiles,
@@ -104,11 +104,22 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out,
         if (tile == 0) {
             // prefix0: hits of a head the caller compacted first (misaligned input)
             if (prefix0) p = static_cast<SV>(*prefix0);
-            if (lane == 0) st.publish(0, static_cast<SV>(p + agg), TILE_INCLUSIVE);
+            if (lane == 0) {
+                if constexpr (FIXED) {  // the fixed-association look-back (lookback.hpp)
+                    st.publish(0, static_cast<SV>(agg), TILE_AGGREGATE);
+                    st.publish(0, p, TILE_INCLUSIVE);
+                } else {
+                    st.publish(0, static_cast<SV>(p + agg), TILE_INCLUSIVE);
+                }
+            }
         } else if constexpr ((ABL & 1) == 0) {
             if (lane == 0) st.publish(tile, static_cast<SV>(agg), TILE_AGGREGATE);
-            p = st.exclusive_prefix(tile, op_plus{});
-            if (lane == 0) st.publish(tile, static_cast<SV>(p + agg), TILE_INCLUSIVE);
+            if constexpr (FIXED) {
+                p = st.exclusive_prefix_fixed(tile, op_plus{});
+            } else {
+                p = st.exclusive_prefix(tile, op_plus{});
+                if (lane == 0) st.publish(tile, static_cast<SV>(p + agg), TILE_INCLUSIVE);
+            }
         }
         if (lane == 0) {
             s_prefix = p;

@@ -153,6 +153,72 @@ struct tile_state {
         }
         return excl;
     }
+
+    // ---- fixed-association form (floating-point scans) -------------------
+    // exclusive_prefix adds up whichever predecessors have published when the
+    // tile looks, so a floating-point scan's association -- and its last bits
+    // -- varied from run to run.  Here the association is fixed: tiles form
+    // groups of 64; E(64g), the exclusive prefix of a group's first tile, is
+    //   E(64g) = E(64(g-1)) (op) fold(aggregate(64(g-1)) .. aggregate(64g-1)),
+    // published by tile 64g in its inclusive slot, and tile t of group g
+    // takes E(64g) (op) fold(aggregate(64g) .. aggregate(t-1)).  Each fold is
+    // one wave reduction over lanes in index order (identity-padded), so the
+    // result is a function of the input alone: bitwise reproducible, like
+    // HPX's par for a fixed core count (scan_partitioner.hpp:62-156).  The
+    // waits are on lower tile ids only (dispatch-order forward progress, as
+    // above) and bounded.  Tile 0 publishes its aggregate and E(0) = the
+    // scan's initial prefix.
+    static constexpr uint64_t kGroup = kWave;
+
+    // Lane-uniform; waits until slot (j, status) is published.
+    __device__ __forceinline__ bool wait_slot(uint64_t j, uint32_t status, T* v, uint32_t& spins) const {
+        const uint64_t* p = slots + (j * 2 + (status == TILE_INCLUSIVE ? 1 : 0)) * G;
+        while (true) {
+            uint64_t a[G];
+            bool ok = true;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                a[g] = __hip_atomic_load(&p[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = ok && static_cast<uint32_t>(a[g] >> 32) == status;
+            }
+            if (ok) {
+                uint32_t w[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) w[g] = static_cast<uint32_t>(a[g]);
+                *v = from_words<T>(w);
+                return true;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kSpinLimit) return false;
+        }
+    }
+
+    // Called by ALL 64 lanes of one wave, tile > 0.  Returns the exclusive
+    // prefix on every lane; a group's first tile also publishes it.
+    template <typename Op>
+    __device__ __forceinline__ T exclusive_prefix_fixed(uint64_t tile, Op op) const {
+        const T id = Op::template identity<T>();
+        const int lane = lane_id();
+        const uint64_t first = tile / kGroup * kGroup;
+        // the aggregates to fold: the previous group's 64 (a group's first
+        // tile) or this group's tiles before this one
+        const uint64_t base = tile == first ? first - kGroup : first;
+        const uint64_t cnt = tile == first ? kGroup : tile - first;
+        uint32_t spins = 0;
+        T a = id;
+        bool ok = true;
+        if (static_cast<uint64_t>(lane) < cnt) ok = wait_slot(base + lane, TILE_AGGREGATE, &a, spins);
+        T e = id;
+        if (ok) ok = wait_slot(base, TILE_INCLUSIVE, &e, spins);  // E(base): base is a group's first tile
+        if (!__all(ok)) {
+            if (lane == 0 && err)
+                __hip_atomic_store(err, HPXHIP_DEVERR_LOOKBACK_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return id;
+        }
+        const T excl = op(readlane(e, 0), wave_reduce(a, op));
+        if (tile == first && lane == 0) publish(tile, excl, TILE_INCLUSIVE);
+        return excl;
+    }
 };
 
 }  // namespace hpxhip

@@ -50,7 +50,14 @@ constexpr uint64_t tile_elems() {
 // Wave 0 of a tile: scans the WAVES wave totals in s_wave_total with DPP,
 // publishes the tile (aggregate, look-back, inclusive) and leaves in
 // s_wave_total[w] the tile prefix (op) the exclusive prefix of wave w.
-template <typename T, typename Op, int WAVES, bool LOOKBACK, int LBK = 1>
+// FIXED: the fixed-association look-back (lookback.hpp) -- tile 0 publishes
+// its aggregate and the initial prefix E(0).  Shipped for every scan (r03):
+// floating-point results become reproducible run to run, and it is also the
+// faster hand-off (2^30 f64 2.64 -> 2.61 ms, int64 2.64-2.65 -> 2.62-2.63;
+// profiles/r03_ubench_scan7_fixed.log): every tile reads 64 aggregates
+// published right after their loads plus one group word, instead of walking
+// a variable window and publishing an inclusive value of its own.
+template <typename T, typename Op, int WAVES, bool LOOKBACK, int LBK = 1, bool FIXED = false>
 __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& st, Op op, const T* prefix_dev, T init,
                                             T* s_wave_total) {
     const T id = Op::template identity<T>();
@@ -62,12 +69,23 @@ __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& 
     T p;
     if (tile == 0) {
         p = prefix_dev ? *prefix_dev : init;
-        if (lane == 0) st.publish(0, op(p, agg), TILE_INCLUSIVE);
+        if (lane == 0) {
+            if constexpr (FIXED) {
+                st.publish(0, agg, TILE_AGGREGATE);
+                st.publish(0, p, TILE_INCLUSIVE);  // E(0)
+            } else {
+                st.publish(0, op(p, agg), TILE_INCLUSIVE);
+            }
+        }
     } else {
         if constexpr (LOOKBACK) {
             if (lane == 0) st.publish(tile, agg, TILE_AGGREGATE);
-            p = st.template exclusive_prefix<Op, LBK>(tile, op);
-            if (lane == 0) st.publish(tile, op(p, agg), TILE_INCLUSIVE);
+            if constexpr (FIXED) {
+                p = st.exclusive_prefix_fixed(tile, op);
+            } else {
+                p = st.template exclusive_prefix<Op, LBK>(tile, op);
+                if (lane == 0) st.publish(tile, op(p, agg), TILE_INCLUSIVE);
+            }
         } else {
             p = id;  // ablation only: measures the pass without the tile hand-off
         }
@@ -80,7 +98,7 @@ __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& 
 // layer's device closures): conv maps T -> X, unwrap_value X -> T.
 template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED, int ROUNDS = kRounds,
           int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false, int LBK = 1,
-          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = true, typename X = T, bool DEFER = std::is_floating_point_v<X> && sizeof(X) == 8>
+          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = true, typename X = T, bool DEFER = std::is_floating_point_v<X> && sizeof(X) == 8, bool FIXED = true>
 __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, X init,
                                                    const X* prefix_dev, uint32_t* counter, tile_state<X> st) {
     constexpr int V = 16 / sizeof(T);
@@ -141,7 +159,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
         const X wt = wave_reduce(lt, op);
         if (lane == 0) s_wave_total[wave] = wt;
         __syncthreads();
-        if (wave == 0) tile_prefix<X, Op, WAVES, LOOKBACK, LBK>(tile, st, op, prefix_dev, init, s_wave_total);
+        if (wave == 0) tile_prefix<X, Op, WAVES, LOOKBACK, LBK, FIXED>(tile, st, op, prefix_dev, init, s_wave_total);
     }
 
     // ---- per-round lane scan + wave scan; x becomes the wave-local result
@@ -187,7 +205,7 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
     if constexpr (!EARLY) {
         if (lane == 0) s_wave_total[wave] = carry;
         __syncthreads();
-        if (wave == 0) tile_prefix<X, Op, WAVES, LOOKBACK, LBK>(tile, st, op, prefix_dev, init, s_wave_total);
+        if (wave == 0) tile_prefix<X, Op, WAVES, LOOKBACK, LBK, FIXED>(tile, st, op, prefix_dev, init, s_wave_total);
     }
     __syncthreads();
     const X pre = s_wave_total[wave];

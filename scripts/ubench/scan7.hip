@@ -1,5 +1,6 @@
 // Microbenchmark (round 3): f64 inclusive plus-scan tile shapes and the deferred round carry
-// (DEFER: round totals held wave-uniform, carry folded in at the store).  The shipped
+// (DEFER: round totals held wave-uniform, carry folded in at the store),
+// and the fixed-association look-back (FIXED, reproducible FP scans).  The shipped
 // FP scan runs 1024 threads x 12 rounds (16 spill 24 VGPRs: 4 waves/SIMD cap a
 // wave at 128 registers).  Fewer threads per tile raise the register cap:
 // 512 threads x 32 rounds (2 waves/SIMD, 256 VGPRs) and 256 x 64 (1 wave/SIMD)
@@ -32,7 +33,7 @@ struct bench {
            B / t[0] / 1e6 / 80.0, ok ? "ok" : "MISMATCH");
     fflush(stdout);
   }
-  template <int R, int TH, int MINW = 1, bool DEFER = true>
+  template <int R, int TH, int MINW = 1, bool DEFER = true, bool FIXED = false>
   void shipped(const char* name) {
     const uint64_t tile = scan_detail::tile_elems<T, R, TH>();
     const uint64_t ntiles = (N + tile - 1) / tile;
@@ -40,7 +41,7 @@ struct bench {
     tile_state<T> st{reinterpret_cast<uint64_t*>(ws + 256), err};
     run(name, [&] {
       CK(hipMemsetAsync(ws, 0, total, 0));
-      scan_detail::k_scan<T, Conv, op_plus, true, true, R, TH, true, MINW, false, 1, false, true, T, DEFER><<<ntiles, TH>>>(
+      scan_detail::k_scan<T, Conv, op_plus, true, true, R, TH, true, MINW, false, 1, false, true, T, DEFER, FIXED><<<ntiles, TH>>>(
             in, out, N, Conv{}, op_plus{}, T(0), static_cast<const T*>(nullptr), reinterpret_cast<uint32_t*>(ws), st);
     }, tile);
   }
@@ -62,15 +63,11 @@ int main() {
   for (int rep = 0; rep < 2; ++rep) {
     k_ones<double><<<8192, 256>>>((double*)in, N); CK(hipDeviceSynchronize());
     bd.shipped<12, 1024, 1, false>("f64 T1024 R12 (shipped r02)");
-    bd.shipped<12, 1024>("f64 T1024 R12 defer");
     bd.shipped<16, 1024>("f64 T1024 R16 defer");
-    bd.shipped<24, 512>("f64 T512 R24 defer");
-    bd.shipped<32, 512>("f64 T512 R32 defer");
+    bd.shipped<16, 1024, 1, true, true>("f64 T1024 R16 defer fixed-assoc");
     k_ones<int64_t><<<8192, 256>>>((int64_t*)in, N); CK(hipDeviceSynchronize());
-    bi.shipped<16, 1024, 1, false>("i64 T1024 R16 (shipped r02)");
-    bi.shipped<16, 1024>("i64 T1024 R16 defer");
-    bi.shipped<32, 512>("i64 T512 R32 defer");
-    bi.shipped<20, 1024>("i64 T1024 R20 defer");
+    bi.shipped<16, 1024, 1, false>("i64 T1024 R16 (shipped)");
+    bi.shipped<16, 1024, 1, false, true>("i64 T1024 R16 fixed-assoc");
   }
   uint32_t h = 0; CK(hipMemcpy(&h, err, 4, hipMemcpyDeviceToHost)); printf("deverr %u\n", h);
   return 0;

@@ -314,6 +314,37 @@ def test_scan_fp_tolerance(pol, gpu_target, dt):
     assert np.all(np.abs(got - exact) <= k * u * exact + 1e-300)
 
 
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("incl", [True, False])
+def test_scan_fp_reproducible(pol, gpu_target, dt, incl):
+    """FP scans use the fixed-association look-back (lookback.hpp
+    exclusive_prefix_fixed): the result is a function of the input alone, so
+    repeated runs agree bit for bit -- over many 64-tile groups (2^25 + 5
+    elements: 256-1024 tiles), mixed signs, a ragged last tile -- and stay
+    within the scan tolerance of a 64-bit-mantissa cumulative sum."""
+    n = (1 << 25) + 5
+    a = rnd(dt, n, 77) - dt(0.5)
+    d = dev(a, gpu_target)
+    outs = []
+    for _ in range(3):
+        o = hpx.vector(n, dtype=dt, tgt=gpu_target)
+        if incl:
+            P.inclusive_scan(pol, d.begin(), d.end(), o.begin(), F.plus, dt(0.25))
+        else:
+            P.exclusive_scan(pol, d.begin(), d.end(), o.begin(), dt(0.25))
+        outs.append(o.to_host())
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o.view(np.uint8), outs[0].view(np.uint8))
+    exact = np.cumsum(np.concatenate([[0.25], a.astype(np.longdouble)]))
+    exact = exact[1:] if incl else exact[:-1]
+    u = 2.0 ** -24 if dt == np.float32 else 2.0 ** -53
+    mag = np.cumsum(np.concatenate([[0.25], np.abs(a).astype(np.longdouble)]))
+    mag = mag[1:] if incl else mag[:-1]
+    tile = 1024 * 12 * (16 // np.dtype(dt).itemsize)
+    k = (n + tile - 1) // tile + 96
+    assert np.all(np.abs(outs[0].astype(np.longdouble) - exact) <= k * u * mag)
+
+
 def test_scan_large_property(pol, gpu_target):
     """Size-independent property at 2^27: inclusive - exclusive == input and
     last inclusive == reduce (int64, exact)."""
