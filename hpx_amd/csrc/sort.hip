@@ -346,25 +346,45 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         HPXHIP_CHECK_LAUNCH();
         return offsets();
     };
-    // one stable onesweep pass; ctl word: its digit shift or -1 (not run)
-    auto pass = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, int rb, const int32_t* word) -> int {
+    // one stable onesweep pass; ctl word: its digit shift or -1 (not run).
+    // Launch geometry: passes the plan usually takes get one workgroup per
+    // tile (a new workgroup starts as soon as one leaves); passes it usually
+    // skips -- the LSD fallback of a hybrid-sized sort, the second-byte pass
+    // of the 17-bit form -- a persistent grid of two workgroups per CU
+    // claiming tiles (k_onesweep PERSIST), so skipping them costs one gate read
+    // per workgroup.  A skipped 2^30-key pass with one workgroup per tile
+    // dispatched 131072 workgroups that only read the gate: ~0.1 ms each,
+    // ~0.9 ms per sort (19.3 -> 20.2 ms when the plan moved to the device);
+    // running every pass persistent instead cost far more (26.3 ms: the
+    // segment sort and the prefix passes lose the dispatcher's overlap of a
+    // leaving workgroup with a starting one; profiles/r03_sort_probe_persistent.log).
+    auto pass = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, int rb, const int32_t* word,
+                    bool persist) -> int {
         const uint64_t nt = L.ntiles;
         const uint64_t zbytes = align_up(256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), 16);
         hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
                            reinterpret_cast<uint4*>(counter), zbytes / 16, word);
         HPXHIP_CHECK_LAUNCH();
-        const dim3 grid(static_cast<unsigned>(nt)), block(TS::threads);
+        const uint64_t cap = 2ull * static_cast<uint64_t>(current_device_info().cus);
+        const dim3 grid(static_cast<unsigned>(persist && nt > cap ? cap : nt)), block(TS::threads);
         auto launch = [&](auto gtag, auto rbtag) {
             using G = decltype(gtag);
             constexpr int RB = decltype(rbtag)::value;
             // Tile ids: blockIdx for 32-bit keys (4 x 8-bit passes 15.9 vs
             // 16.3 ms at 2^30), the atomic counter for 64-bit keys (9-bit
             // pass 5.85 vs 6.23 ms, byte pass 4.93 vs 5.00;
-            // profiles/r02_ubench_tile_order_ab.log).
+            // profiles/r02_ubench_tile_order_ab.log); persistent grids
+            // always claim from the counter.
             constexpr bool DYN = sizeof(U) == 8;
-            hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB, true, DYN>),
-                               grid, block, 0, s, kin, kout, vin, vout, n, 0, RB == 9 ? xstart : start,
-                               reinterpret_cast<G*>(base + L.lb), counter, err, X{}, word);
+            if (persist)
+                hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB, true, true,
+                                               true>),
+                                   grid, block, 0, s, kin, kout, vin, vout, n, 0, RB == 9 ? xstart : start,
+                                   reinterpret_cast<G*>(base + L.lb), counter, err, X{}, word, nt);
+            else
+                hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB, true, DYN>),
+                                   grid, block, 0, s, kin, kout, vin, vout, n, 0, RB == 9 ? xstart : start,
+                                   reinterpret_cast<G*>(base + L.lb), counter, err, X{}, word);
         };
         using R8 = std::integral_constant<int, 8>;
         using R9 = std::integral_constant<int, 9>;
@@ -405,25 +425,52 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
 
     // ---- hybrid: prefix passes (keys -> alt -> keys), bucket bounds, per-bucket LDS sort
     if (mode) {
-        if (!HAS_VAL && mode == 17 && (rc = pass(kc, ka, nullptr, nullptr, 9, ctl + C_A9))) return rc;
-        if ((rc = pass(kc, ka, vc, va, 8, ctl + C_A8))) return rc;
-        if ((rc = pass(ka, kc, va, vc, 8, ctl + C_B))) return rc;
+        if (!HAS_VAL && mode == 17 && (rc = pass(kc, ka, nullptr, nullptr, 9, ctl + C_A9, false))) return rc;
+        // the second-byte pass runs in the 16-bit form only (pairs; keys the
+        // 17-bit form does not fit)
+        if ((rc = pass(kc, ka, vc, va, 8, ctl + C_A8, mode == 17))) return rc;
+        if ((rc = pass(ka, kc, va, vc, 8, ctl + C_B, false))) return rc;
         hipLaunchKernelGGL((k_bucket_bounds<U, X>), dim3((kMaxBuckets + 1 + 255) / 256), dim3(256), 0, s, kc, n, 0, 0,
                            0, 0u, X{}, bounds, ctl + C_BOUNDS);
         HPXHIP_CHECK_LAUNCH();
         auto* oversized = reinterpret_cast<uint32_t*>(ctl + C_OVERSIZED);
+        // The segment sort the plan usually takes: one workgroup per bucket
+        // over the buckets a typical plan has (twice n / 8192, at most the
+        // 2^17 a plan can have; workgroups past the planned count leave), then
+        // a grid striding over any further buckets (k_bucket_sort PERSIST,
+        // two workgroups per CU: a skewed plan with more, smaller buckets), so
+        // a small sort does not dispatch 2^17 workgroups.  Striding over all
+        // buckets instead ran the 2^30 segment sort 7.2 -> 9.7 ms: the loop
+        // costs the kernel 19 more spilled VGPRs
+        // (profiles/r03_sort_probe_seg_persist.log,
+        // r03_sort_kernel_stats_seg_persist.csv).  The 1024-thread keys
+        // segment (buckets over 9216, rare) strides over all of them, one
+        // workgroup per CU.
+        const unsigned cus = static_cast<unsigned>(current_device_info().cus);
+        const uint64_t want = 2 * (n / 8192 + 1);
+        const uint32_t g0 = static_cast<uint32_t>(want > kMaxBuckets ? kMaxBuckets : want);
         if constexpr (HAS_VAL) {
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true, true>),
-                               dim3(kMaxBuckets / 2), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, vc, oversized,
-                               ctl + C_SEGA);
+                               dim3(g0), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, vc, oversized,
+                               ctl + C_SEGA, 0u);
+            HPXHIP_CHECK_LAUNCH();
+            if (g0 < kMaxBuckets)
+                hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true, true, true>),
+                                   dim3(cus), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, vc, oversized,
+                                   ctl + C_SEGA, g0);
         } else {
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true>),
-                               dim3(kMaxBuckets), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
-                               ctl + C_SEGA);
+                               dim3(g0), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
+                               ctl + C_SEGA, 0u);
             HPXHIP_CHECK_LAUNCH();
-            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItems, 16, uint32_t, false, true>),
-                               dim3(kMaxBuckets / 2), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, nullptr,
-                               oversized, ctl + C_SEGB);
+            if (g0 < kMaxBuckets)
+                hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true, true>),
+                                   dim3(2 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
+                                   oversized, ctl + C_SEGA, g0);
+            HPXHIP_CHECK_LAUNCH();
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItems, 16, uint32_t, false, true, true>),
+                               dim3(cus), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, nullptr,
+                               oversized, ctl + C_SEGB, 0u);
         }
         HPXHIP_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_sort_fallback, dim3(1), dim3(64), 0, s, ctl);
@@ -431,10 +478,13 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         if (first > 0 && (rc = count_rest(ctl + C_HIST_B))) return rc;
     }
 
-    // ---- LSD over the live digits (keys <-> alt), when planned
+    // ---- LSD over the live digits (keys <-> alt), when planned: the plan of
+    // a small sort (mode 0) or the fallback of a hybrid-sized one (persistent
+    // grids: usually skipped)
     for (int i = 0; i < passes; ++i) {
         const bool even = (i & 1) == 0;
-        if ((rc = pass(even ? kc : ka, even ? ka : kc, even ? vc : va, even ? va : vc, 8, ctl + C_LSD + i))) return rc;
+        if ((rc = pass(even ? kc : ka, even ? ka : kc, even ? vc : va, even ? va : vc, 8, ctl + C_LSD + i, mode != 0)))
+            return rc;
     }
     hipLaunchKernelGGL((k_copy_gated<U>), dim3(grid_for(n)), dim3(256), 0, s, ka, kc, n, ctl + C_COPY);
     HPXHIP_CHECK_LAUNCH();

@@ -161,15 +161,22 @@ __global__ __launch_bounds__(R) void k_bin_offsets(const unsigned long long* __r
 // every key is stored from registers straight to its final position.  It
 // frees 64 KiB of LDS but the scattered 8-B stores make the pass 3x slower
 // (14.3 vs 4.85 ms at 2^30 u64, profiles/r02_ubench_onesweep_direct.log).
+// PERSIST (r03, the device-planned sort): a grid of about two workgroups
+// per CU claims tiles from the counter until ntiles are done.  The plan
+// gates every pass on the device, so passes it skips are still launched; a
+// skipped 2^30-key pass had dispatched 131072 workgroups that only read the
+// gate and left (~0.1 ms each, ~0.9 ms per sort over the skipped second-byte
+// and LSD passes); a persistent grid leaves after one read per workgroup.
 template <typename U, typename VAL, bool HAS_VAL, typename G, typename X, int THREADS = 512, int ITEMS = 16,
-          int LBB = 8, int RB = 8, bool STAGE = true, bool DYN_ID = HPXHIP_TILE_DYN_ID>
+          int LBB = 8, int RB = 8, bool STAGE = true, bool DYN_ID = HPXHIP_TILE_DYN_ID, bool PERSIST = false>
 __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin, U* __restrict__ kout,
                                                        const VAL* __restrict__ vin, VAL* __restrict__ vout,
                                                        uint64_t n, int shift,
                                                        const unsigned long long* __restrict__ bin_start,
                                                        G* __restrict__ lb, uint32_t* __restrict__ counter,
                                                        uint32_t* __restrict__ err, X xf,
-                                                       const int32_t* __restrict__ ctl = nullptr) {
+                                                       const int32_t* __restrict__ ctl = nullptr, uint64_t ntiles = 0) {
+    static_assert(!PERSIST || STAGE, "the persistent form keeps the LDS-staged write-out");
     // device-planned sort (sort.hip): *ctl = this launch's digit shift, or
     // -1 when the plan does not take this pass (every block returns at once)
     if (ctl) {
@@ -195,12 +202,18 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     const int t = threadIdx.x;
     const int wave = t / kWave;
     const int lane = lane_id();
-    // tile order = dispatch order (lookback.hpp); DYN_ID: ablation with ids
-    // from the atomic counter
-    if (DYN_ID && t == 0) s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // one tile; the persistent form calls it in a loop, the plain form once
+    // (a loop around the body in the plain form changes its register
+    // allocation)
+    auto one = [&]() -> bool {
+    // tile order = dispatch order (lookback.hpp); DYN_ID / PERSIST: ids from
+    // the atomic counter
+    if ((DYN_ID || PERSIST) && t == 0)
+        s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int i = t; i < WAVES * R; i += THREADS) (&s_whist[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t tile = DYN_ID ? s_tile : blockIdx.x;
+    const uint64_t tile = (DYN_ID || PERSIST) ? s_tile : blockIdx.x;
+    if (PERSIST && tile >= ntiles) return false;
     const uint64_t tile_base = tile * TILE;
     const uint64_t wbase = tile_base + static_cast<uint64_t>(wave) * (TILE / WAVES);
 
@@ -330,7 +343,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
                 if constexpr (HAS_VAL) vout[dst] = v[r];
             }
         }
-        return;
+        return false;
     }
 
     // ---- coalesced write of the LDS-sorted tile
@@ -345,6 +358,13 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             kout[dst] = key;
             if constexpr (HAS_VAL) vout[dst] = s_vals[i];
         }
+    }
+    return true;
+    };
+    if constexpr (PERSIST) {
+        while (one()) __syncthreads();  // the tile's LDS readers are done before the next claim
+    } else {
+        one();
     }
 }
 
@@ -411,16 +431,23 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 // a segment: no bounds read-back and no host packing between the prefix
 // passes and this kernel.  A bucket too large for the LDS is left alone and
 // raises *oversized (the host then finishes it by per-bucket LSD).
+// PERSIST (device-planned sort, BOUNDS only): a fixed grid strides over the
+// planned buckets (bucket b by workgroup b mod gridDim), so a launch the plan
+// skips costs one gate read per workgroup instead of one dispatch per bucket.
 template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16, typename VAL = uint32_t,
-          bool HAS_VAL = false, bool BOUNDS = false>
+          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false>
 __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
     void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf,
                        VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr,
-                       const int32_t* __restrict__ ctl = nullptr) {
+                       const int32_t* __restrict__ ctl = nullptr, uint32_t first_bucket = 0) {
+    static_assert(!PERSIST || BOUNDS, "the persistent form strides over bucket bounds");
     // device-planned sort: ctl = {on, buckets, top_single}; the grid covers
-    // the largest bucket count, blocks past the planned one return
+    // the largest bucket count (or strides over it), blocks past the planned
+    // count return
+    uint32_t nbk = PERSIST ? first_bucket + gridDim.x : first_bucket + blockIdx.x + 1;
     if (ctl) {
-        if (!ctl[0] || blockIdx.x >= static_cast<uint32_t>(ctl[1])) return;
+        if (!ctl[0]) return;
+        nbk = static_cast<uint32_t>(ctl[1]);
         top_single = ctl[2];
     }
     constexpr int WAVES = THREADS / kWave;
@@ -436,22 +463,27 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     const int t = threadIdx.x;
     const int wave = t / kWave;
     const int lane = lane_id();
+    const int top_planned = top_single;
+    // one bucket (segment) bk; the persistent form calls it in a loop, the
+    // plain form once -- a loop around the body in the plain form cost the
+    // compiler 19 spilled VGPRs
+    auto one = [&](uint32_t bk) {
     uint64_t b, mm;
     if constexpr (BOUNDS) {
-        b = seg[blockIdx.x];
-        mm = seg[blockIdx.x + 1] - b;
+        b = seg[bk];
+        mm = seg[bk + 1] - b;
         if (mm > static_cast<uint64_t>(THREADS) * ITEMS) {
             if (t == 0) __hip_atomic_store(oversized, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
     } else {
-        b = seg[2 * blockIdx.x];  // (begin, end) pairs
-        mm = seg[2 * blockIdx.x + 1] - b;
+        b = seg[2 * bk];  // (begin, end) pairs
+        mm = seg[2 * bk + 1] - b;
     }
     const uint32_t m = static_cast<uint32_t>(mm);
     if (m < 2) return;
     const U diff = xf(keys[b]) ^ xf(keys[b + m - 1]);
-    int top = top_single;
+    int top = top_planned;
     if (diff) {
         const int hb = BITS - (sizeof(U) == 8 ? __builtin_clzll(static_cast<uint64_t>(diff))
                                                : __builtin_clz(static_cast<uint32_t>(diff)));
@@ -609,6 +641,17 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
         const uint32_t vlead = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(gvals) % 64) / sizeof(VAL);
         for (uint32_t i = t; i < m + vlead; i += THREADS)
             if (i >= vlead) st_stream(&gvals[i - vlead], s_vals[i - vlead]);
+    }
+    };
+    // first_bucket: a launch may cover the buckets from there on (a plain
+    // launch sized for the typical plan, then a striding one for the rest)
+    if constexpr (PERSIST) {
+        for (uint32_t bk = first_bucket + blockIdx.x; bk < nbk; bk += gridDim.x) {
+            one(bk);
+            __syncthreads();  // s_keys / s_vals read out before the next bucket's passes
+        }
+    } else if (first_bucket + blockIdx.x < nbk) {
+        one(first_bucket + blockIdx.x);
     }
 }
 

@@ -103,6 +103,23 @@ def test_heavy_duplicates(pol, gpu_target):
     check(pol, gpu_target, vals[rng.integers(0, 1 << 16, n)])
 
 
+def test_buckets_past_the_typical_grid(pol, gpu_target):
+    """The segment sort is launched with one workgroup per bucket for the
+    buckets a typical plan of n keys has (2 n / 8192) and a striding launch
+    for the rest (sort.hip): skewed keys whose planned buckets lie past that
+    grid -- top byte 0xF0 for all keys but one (17-bit form, buckets from
+    0xF0 << 9 on), a constant top byte (16-bit form on the next two bytes,
+    more buckets than the grid) -- must be sorted by the second launch."""
+    rng = np.random.default_rng(0xB0C)
+    n = 1 << 22
+    low = rng.integers(0, 1 << 56, n, dtype=np.uint64)
+    h = low | np.uint64(0xF0 << 56)
+    h[12345] = low[12345]
+    check(pol, gpu_target, h)
+    check(pol, gpu_target, h, True)
+    check(pol, gpu_target, low | np.uint64(0xC3 << 56))
+
+
 @pytest.mark.parametrize("bits", [24, 56])
 def test_low_bit_ranges(pol, gpu_target, bits):
     # keys below 2^24 (three live bytes, many duplicates: the prefix is bytes 2
