@@ -515,7 +515,11 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
         __syncthreads();  // earlier readers of s_keys / s_whist are done
         for (int i = t; i < WAVES * kRadix / 2; i += THREADS) reinterpret_cast<uint32_t*>(&s_whist[0][0])[i] = 0;
         __syncthreads();
-        uint32_t rank[ITEMS];
+        // ranks (< 2^16, static_assert above) packed two per register: the
+        // kernel sits at the 128-VGPR bound of two workgroups per CU
+        uint32_t rank2[(ITEMS + 1) / 2];
+#pragma unroll
+        for (int r = 0; r < (ITEMS + 1) / 2; ++r) rank2[r] = 0;
 #pragma unroll
         for (int r = 0; r < ITEMS; ++r) {
             const uint64_t act = active(r);
@@ -525,7 +529,7 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
             const uint32_t below = peers_below(peers);
             const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(peers));
             const uint32_t old = s_whist[wave][d];
-            rank[r] = old + below;
+            rank2[r / 2] |= (old + below) << (16 * (r & 1));
             if (((act >> lane) & 1u) && below == 0) s_whist[wave][d] = static_cast<uint16_t>(old + cnt);
         }
         __syncthreads();
@@ -555,7 +559,7 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
             if (act == 0) break;
             if ((act >> lane) & 1u) {
                 const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
-                const uint32_t pos = s_local[d] + s_whist[wave][d] + rank[r];
+                const uint32_t pos = s_local[d] + s_whist[wave][d] + ((rank2[r / 2] >> (16 * (r & 1))) & 0xffffu);
                 s_keys[pos] = k[r];
                 if constexpr (HAS_VAL) s_vals[pos] = v[r];
             }
