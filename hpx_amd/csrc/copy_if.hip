@@ -68,12 +68,17 @@ int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev,
     // profiles/r02_ubench_tile_order_ab.log).
     constexpr bool kDynId = false;
     constexpr bool kFixed = true;
+    // 8-byte elements: four wave rounds of hits per LDS batch (one wait per
+    // batch), 2.176-2.181 -> 2.164-2.168 ms at 2^30 int64
+    // (profiles/r03_ubench_copyif7_writeout.log); no gain for 4-byte ones
+    // (profiles/r02_ubench_copyif_writeout.log)
+    constexpr int kRpb = (sizeof(T) == 8 && ALIGNED) ? 4 : 1;
     // Aligned, with the 32-bit look-back state: at most 64 VGPRs (8 waves per SIMD),
     // so two workgroups share a CU.  4-byte elements compiled to 70 VGPRs
     // at the old bound (4 waves per SIMD) and ran one workgroup per CU:
     // int32 2^31 2.77 -> 2.38 ms (profiles/r02_ubench_copyif_occupancy.log).
     constexpr int kMinWaves = (std::is_same_v<SV, uint32_t> && ALIGNED) ? 8 : 4;
-    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId, false, 1, kFixed>), dim3(static_cast<unsigned>(ntiles)),
+    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId, false, kRpb, kFixed>), dim3(static_cast<unsigned>(ntiles)),
                        dim3(kThreads), 0, s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles,
                        prefix0);
     HPXHIP_CHECK_LAUNCH();

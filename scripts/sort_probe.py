@@ -1,7 +1,8 @@
 """Sort size sweep on one GPU: hpxhip_sort / hpxhip_sort_by_key over random
 keys at 2^20..2^30, device time from HIP events (best of 3, generation
 subtracted), host time of the call itself, and an is_sorted + checksum
-check of every result.  usage: python scripts/sort_probe.py [maxlog]"""
+check of every result.  usage: python scripts/sort_probe.py [maxlog]
+(SORT_ONLY=u64|u32|pairs: that case at 2^maxlog only)."""
 import ctypes
 import os
 import sys
@@ -66,7 +67,14 @@ def run(dt, logn, kv=False, reps=3):
 
 
 maxlog = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+# SORT_ONLY=u64|u32|pairs: that case at 2^maxlog only (PMC target runs)
+only = os.environ.get("SORT_ONLY")
 print(f"{'case':28s} {'ms':>9s} {'Gkeys/s':>8s} {'host_ms':>8s} ok", flush=True)
+if only:
+    dt, kv = {"u64": (np.uint64, False), "u32": (np.uint32, False), "pairs": (np.uint64, True)}[only]
+    d, h, ok = run(dt, maxlog, kv, reps=2)
+    print(f"{only + ' 2^' + str(maxlog):28s} {d:9.3f} {(1 << maxlog) / d / 1e6:8.2f} {h:8.3f} {ok}", flush=True)
+    sys.exit(0)
 for logn in range(20, maxlog + 1, 2):
     for dt, kv, name in ((np.uint64, False, "u64"), (np.uint32, False, "u32"), (np.uint64, True, "u64/u64 pairs")):
         if kv and logn > 28:
