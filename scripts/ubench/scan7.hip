@@ -1,6 +1,7 @@
 // Microbenchmark (round 3): f64 inclusive plus-scan tile shapes and the deferred round carry
 // (DEFER: round totals held wave-uniform, carry folded in at the store),
-// and the fixed-association look-back (FIXED, reproducible FP scans).  The shipped
+// and the fixed-association look-back (FIXED, reproducible FP scans); then
+// (after FIXED shipped) tile shapes with several workgroups per CU.  The shipped
 // FP scan runs 1024 threads x 12 rounds (16 spill 24 VGPRs: 4 waves/SIMD cap a
 // wave at 128 registers).  Fewer threads per tile raise the register cap:
 // 512 threads x 32 rounds (2 waves/SIMD, 256 VGPRs) and 256 x 64 (1 wave/SIMD)
@@ -61,13 +62,16 @@ int main() {
   bench<int64_t> bi{N, (int64_t*)in, (int64_t*)out, ws, err, e0, e1};
   bench<double> bd{N, (double*)in, (double*)out, ws, err, e0, e1};
   for (int rep = 0; rep < 2; ++rep) {
-    k_ones<double><<<8192, 256>>>((double*)in, N); CK(hipDeviceSynchronize());
-    bd.shipped<12, 1024, 1, false>("f64 T1024 R12 (shipped r02)");
-    bd.shipped<16, 1024>("f64 T1024 R16 defer");
-    bd.shipped<16, 1024, 1, true, true>("f64 T1024 R16 defer fixed-assoc");
     k_ones<int64_t><<<8192, 256>>>((int64_t*)in, N); CK(hipDeviceSynchronize());
-    bi.shipped<16, 1024, 1, false>("i64 T1024 R16 (shipped)");
-    bi.shipped<16, 1024, 1, false, true>("i64 T1024 R16 fixed-assoc");
+    bi.shipped<16, 1024, 1, false, true>("i64 T1024 R16 fixed (shipped)");
+    bi.shipped<16, 512, 2, false, true>("i64 T512 R16 2/CU fixed");
+    bi.shipped<8, 1024, 8, false, true>("i64 T1024 R8 2/CU fixed");
+    bi.shipped<16, 256, 4, false, true>("i64 T256 R16 4/CU fixed");
+    bi.shipped<8, 512, 8, false, true>("i64 T512 R8 4/CU fixed");
+    bi.shipped<32, 512, 1, false, true>("i64 T512 R32 1/CU fixed");
+    k_ones<double><<<8192, 256>>>((double*)in, N); CK(hipDeviceSynchronize());
+    bd.shipped<16, 1024, 1, true, true>("f64 T1024 R16 defer fixed (shipped)");
+    bd.shipped<16, 512, 2, true, true>("f64 T512 R16 2/CU defer fixed");
   }
   uint32_t h = 0; CK(hipMemcpy(&h, err, 4, hipMemcpyDeviceToHost)); printf("deverr %u\n", h);
   return 0;
