@@ -487,37 +487,46 @@ def reduction_max(var, identity=None):
     return reduction(var, _ident(var, var.reshape(-1)[0]) if identity is None else identity, F.maximum)
 
 
-def _for_loop_reduce(pol, n, vars_, red, body):
-    """The for_loop with one reduction: the body's inputs feed the
-    transform_reduce kernels (unary or binary map), and the loop exit folds
-    the single view into the live-out variable (for_loop_reduction.hpp:60-66)."""
-    try:
-        ins = [vars_[i] for i in body.ins]
-    except IndexError:
-        raise IndexError("for_loop_n: loop body refers to a variable that is not passed") from None
-    if not all(isinstance(v, iterator) for v in ins):
-        raise TypeError("for_loop_n: the reduction body must read device iterators")
-    if n > 0 and any(it.pos < 0 or it.pos + n - 1 >= it.vec.size() for it in ins):
-        raise ValueError("for_loop_n: an induction walks outside its vector")
-    stream, tgt, is_task = _context(pol, *ins)
-    adt = dtype_code(red.var.dtype)
-    dev, host = _slots_for(tgt).next()
-    fn = body.fn
-    if isinstance(fn, F.Unary):
-        L.call("hpxhip_transform_reduce", ins[0].dtype, adt, red.op.kind, fn.kind, L.scalars_buf(adt, fn.scalars),
-               L.scalar_buf(adt, red.identity), _vp(ins[0].address), n, _vp(dev), stream, None, 0)
-    else:
-        if ins[0].dtype != ins[1].dtype:
+def _for_loop_reduce(pol, n, vars_, reds, parts):
+    """The for_loop with reductions: each reduction's body (an accumulate
+    naming its position) feeds the transform_reduce kernels (unary or binary
+    map) -- one launch per reduction, all on the loop's stream -- and the
+    loop exit folds every view into its live-out variable
+    (for_loop_reduction.hpp:60-66), once all of them are back."""
+    launches = []
+    for red, body in zip(reds, parts):
+        try:
+            ins = [vars_[i] for i in body.ins]
+        except IndexError:
+            raise IndexError("for_loop_n: loop body refers to a variable that is not passed") from None
+        if not all(isinstance(v, iterator) for v in ins):
+            raise TypeError("for_loop_n: the reduction body must read device iterators")
+        if n > 0 and any(it.pos < 0 or it.pos + n - 1 >= it.vec.size() for it in ins):
+            raise ValueError("for_loop_n: an induction walks outside its vector")
+        if isinstance(body.fn, F.Binary) and ins[0].dtype != ins[1].dtype:
             raise TypeError("for_loop_n: both inputs of a binary body must have one dtype")
-        L.call("hpxhip_transform_reduce_binary", ins[0].dtype, adt, red.op.kind, fn.kind,
-               L.scalars_buf(adt, fn.scalars), L.scalar_buf(adt, red.identity), _vp(ins[0].address),
-               _vp(ins[1].address), n, _vp(dev), stream, None, 0)
-    L.call("hpxhip_memcpy_async", _vp(host), _vp(dev), 8, L.D2H, stream)
+        launches.append((red, body, ins))
+    stream, tgt, is_task = _context(pol, *[it for _, _, ins in launches for it in ins])
+    views = []
+    for red, body, ins in launches:
+        adt = dtype_code(red.var.dtype)
+        dev, host = _slots_for(tgt).next()
+        fn = body.fn
+        if isinstance(fn, F.Unary):
+            L.call("hpxhip_transform_reduce", ins[0].dtype, adt, red.op.kind, fn.kind, L.scalars_buf(adt, fn.scalars),
+                   L.scalar_buf(adt, red.identity), _vp(ins[0].address), n, _vp(dev), stream, None, 0)
+        else:
+            L.call("hpxhip_transform_reduce_binary", ins[0].dtype, adt, red.op.kind, fn.kind,
+                   L.scalars_buf(adt, fn.scalars), L.scalar_buf(adt, red.identity), _vp(ins[0].address),
+                   _vp(ins[1].address), n, _vp(dev), stream, None, 0)
+        L.call("hpxhip_memcpy_async", _vp(host), _vp(dev), 8, L.D2H, stream)
+        views.append((red, host, adt))
 
     def exit_iteration():
-        flat = red.var.reshape(-1)
-        with np.errstate(over="ignore"):  # integer combiners wrap like the kernels (and T in C++)
-            flat[0] = red.op(flat[0], red.var.dtype.type(_read_host(host, adt)))
+        for red, host, adt in views:
+            flat = red.var.reshape(-1)
+            with np.errstate(over="ignore"):  # integer combiners wrap like the kernels (and T in C++)
+                flat[0] = red.op(flat[0], red.var.dtype.type(_read_host(host, adt)))
 
     return _finish(is_task, stream, tgt, exit_iteration)
 
@@ -554,9 +563,11 @@ def _for_loop(pol, first, first_stride, count, *args):
     base + stride*k, for_loop_induction.hpp:210-219) and the body writes one
     of them from one or two others (functional.assign).  All-stride-1 loops
     run on the vectorised elementwise transform kernels, others on the
-    strided ones; returns None (future<void> under par(task)).  With one ``reduction`` argument
-    (for_loop_reduction.hpp) the body is a functional.accumulate and the
-    loop runs on the transform_reduce kernels."""
+    strided ones; returns None (future<void> under par(task)).  With
+    ``reduction`` arguments (for_loop_reduction.hpp; any number of them) the
+    body is a functional.accumulate, or functional.accumulate_all of one
+    accumulate per reduction, and the loop runs on the transform_reduce
+    kernels."""
     if not args:
         raise TypeError("for_loop_n: missing loop body")
     *inds, body = args
@@ -564,9 +575,13 @@ def _for_loop(pol, first, first_stride, count, *args):
     if reds and first_stride != 1:
         raise ValueError("for_loop_n: a reduction loop walks its loop variable with stride 1")
     if reds:
-        if len(reds) > 1:
-            raise TypeError("for_loop_n: one reduction per loop is carried by the C ABI")
-        body = F.require(body, F.Accumulate, "for_loop_n")
+        # any number of reductions (for_loop.hpp:802-812): a body that
+        # accumulates into each of them -- accumulate() for one,
+        # accumulate_all(accumulate(...), ...) for several
+        if isinstance(body, F.Accumulate):
+            parts = (body,)
+        else:
+            parts = F.require(body, F.Accumulates, "for_loop_n").parts
         if not isinstance(first, iterator):
             raise TypeError("for_loop_n: the loop variable must be a device iterator")
         for ind in inds:
@@ -577,9 +592,14 @@ def _for_loop(pol, first, first_stride, count, *args):
         if n < 0:
             raise ValueError("for_loop_n: negative count")
         vars_ = [first] + [a.value if isinstance(a, induction) else a for a in inds]
-        if not (0 <= body.red < len(vars_)) or vars_[body.red] is not reds[0]:
-            raise IndexError("for_loop_n: accumulate() must name the reduction's position")
-        return _for_loop_reduce(pol, n, vars_, reds[0], body)
+        named = []
+        for a in parts:
+            if not (0 <= a.red < len(vars_)) or not isinstance(vars_[a.red], reduction):
+                raise IndexError("for_loop_n: accumulate() must name a reduction's position")
+            named.append(vars_[a.red])
+        if len(named) != len(reds) or any(all(r is not x for x in named) for r in reds):
+            raise ValueError("for_loop_n: every reduction needs exactly one accumulate() in the body")
+        return _for_loop_reduce(pol, n, vars_, named, parts)
     body = F.require(body, F.LoopBody, "for_loop_n")
     for ind in inds:
         if not isinstance(ind, induction):

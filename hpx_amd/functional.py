@@ -246,6 +246,23 @@ def accumulate(red: int, fn, *ins) -> Accumulate:
     raise TypeError("accumulate: a Unary functor takes one loop variable, a Binary functor two")
 
 
+@dataclass(frozen=True)
+class Accumulates:
+    """Body of a for_loop with several reductions (for_loop.hpp:802-812
+    takes any number of reduction arguments): one Accumulate per reduction,
+    e.g. ``[](it, T& sum, T& sq) { sum += *it; sq += *it * *it; }`` is
+    ``accumulate_all(accumulate(1, identity(), 0), accumulate(2, square(), 0))``."""
+    parts: tuple
+
+
+def accumulate_all(*parts) -> Accumulates:
+    if not parts or not all(isinstance(a, Accumulate) for a in parts):
+        raise TypeError("accumulate_all: one or more accumulate(...) bodies")
+    if len({a.red for a in parts}) != len(parts):
+        raise ValueError("accumulate_all: each reduction is accumulated by one body")
+    return Accumulates(tuple(parts))
+
+
 # ------------------------------------------------------------------ compare
 @dataclass(frozen=True)
 class Compare:

@@ -822,6 +822,13 @@ class segmented:
     def transform_inclusive_scan(self, pol, first, last, dest, op, conv, init=0):
         return self._scan(pol, first, last, dest, op, init, True, conv)
 
+    def transform_exclusive_scan(self, pol, first, last, dest, init, op, conv):
+        """segmented_algorithms/transform_exclusive_scan.hpp:31-44: the
+        segmented exclusive scan with conv applied to every element (segment
+        totals of conv(x), carries init (op) S_0 (op) ... in segment order),
+        transform_exclusive_scan.hpp:317's argument order."""
+        return self._scan(pol, first, last, dest, op, init, False, conv)
+
     # --- sort: local radix sort + exact global cut + one all-to-all + merge
     def sort(self, pol, first, last=None, comp=F.less):
         """Globally sorted partitioned_vector (BASELINE configs[2]; HPX 1.4

@@ -117,8 +117,25 @@ struct loop_assign {
 template <std::size_t Red, typename F, std::size_t... In>
 struct loop_accumulate {
     static_assert(sizeof...(In) == 1 || sizeof...(In) == 2, "loop_accumulate: one or two inputs");
+    static constexpr std::size_t red = Red;
     F f;
 };
+
+// loop_accumulate_all<A...> is the body of a for_loop with several
+// reductions (for_loop.hpp:802-812 takes any number): one loop_accumulate per
+// reduction, e.g. `[](it, T& sum, T& sq) { sum += *it; sq += *it * *it; }` is
+// accumulate_all(loop_accumulate<1, identity>{}, loop_accumulate<2, square>{})
+// (template arguments of the inputs omitted).  Up to eight reductions (their
+// views travel back in one 64-byte result slot).
+template <typename... A>
+struct loop_accumulate_all {
+    static_assert(sizeof...(A) >= 1 && sizeof...(A) <= 8, "loop_accumulate_all: one to eight reductions");
+    std::tuple<A...> parts;
+};
+template <typename... A>
+loop_accumulate_all<A...> accumulate_all(A const&... a) {
+    return {std::tuple<A...>(a...)};
+}
 
 // ---- reduction operators not in <functional> ------------------------------
 struct minimum {

@@ -41,8 +41,11 @@
 #include <algorithm>
 #include <array>
 #include <cstring>
+#include <functional>
 #include <iterator>
+#include <tuple>
 #include <type_traits>
+#include <vector>
 
 namespace hpx { namespace parallel {
 inline namespace v1 {
@@ -819,9 +822,14 @@ template <typename T, typename Op>
 int64_t loop_stride(reduction_helper<T, Op> const&) { return 1; }
 template <std::size_t N>
 using strides_t = std::array<int64_t, N>;
-template <typename P, typename Vars, std::size_t N, std::size_t Red, typename F, std::size_t... In>
-result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n,
-                                compute::hip::functional::loop_accumulate<Red, F, In...> const& b) {
+// One reduction's share of a reduction loop: its body's inputs feed the
+// transform_reduce kernels, the view lands at `out` (device) and `fold`
+// returns the exit_iteration that folds it into the live-out variable
+// (for_loop_reduction.hpp:60-66).
+template <typename Vars, std::size_t N, std::size_t Red, typename F, std::size_t... In>
+std::function<void(unsigned char const*)> launch_accumulate(
+    hip::target const& t, Vars const& v, strides_t<N> const& st, uint64_t n,
+    compute::hip::functional::loop_accumulate<Red, F, In...> const& b, void* out) {
     if (((st[In] != 1) || ...))
         throw hpx::exception(HPXHIP_ERROR_UNSUPPORTED,
                              "for_loop_n: a reduction loop reads its inductions with stride 1 (the transform_reduce "
@@ -830,39 +838,83 @@ result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, ui
     using T = std::decay_t<decltype(red.identity_)>;
     using Op = std::decay_t<decltype(red.op_)>;
     static_assert(std::is_same<std::decay_t<decltype(red)>, reduction_helper<T, Op>>::value,
-                  "loop_accumulate: position Red must name the loop's reduction");
+                  "loop_accumulate: position Red must name one of the loop's reductions");
+    static_assert(sizeof(T) <= 8, "for_loop reductions of up to 8-byte types");
     auto ins = std::make_tuple(std::get<In>(v)...);
     auto in0 = std::get<0>(ins);
     using TI = value_t<decltype(in0)>;
-    auto const& t = target_of(p, in0);
     T s[2] = {};
     T init = red.identity_;
-    auto slot = t.make_result_slot();
     if constexpr (sizeof...(In) == 1) {
         tr::unary_t<F>::scalars(b.f, s);
         check(hpxhip_transform_reduce(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::unary_t<F>::kind, s, &init,
-                                      raw_ptr(in0), n, slot.device(), t.stream(), nullptr, 0),
+                                      raw_ptr(in0), n, out, t.stream(), nullptr, 0),
               "for_loop_n");
     } else {
         auto in1 = std::get<1>(ins);
         static_assert(std::is_same<TI, value_t<decltype(in1)>>::value, "for_loop_n: both inputs need one element type");
         tr::binary_t<F>::scalars(b.f, s);
         check(hpxhip_transform_reduce_binary(dt<TI>, dt<T>, tr::binop_t<Op>::kind, tr::binary_t<F>::kind, s, &init,
-                                             raw_ptr(in0), raw_ptr(in1), n, slot.device(), t.stream(), nullptr, 0),
+                                             raw_ptr(in0), raw_ptr(in1), n, out, t.stream(), nullptr, 0),
               "for_loop_n");
     }
-    fetch_slot(t, slot, sizeof(T), "for_loop_n result");
     T* var = &red.var_;
     Op op = red.op_;
-    // exit_iteration (for_loop_reduction.hpp:60-66): fold the view into var
-    // as soon as the view is back -- under par(task) on the completion, so
-    // var is final once the future is ready (not only after get()).
+    return [var, op](unsigned char const* bytes) {
+        T view;
+        std::memcpy(&view, bytes, sizeof(T));
+        *var = op(*var, view);
+    };
+}
+
+template <typename T>
+struct is_reduction : std::false_type {};
+template <typename T, typename Op>
+struct is_reduction<reduction_helper<T, Op>> : std::true_type {};
+template <typename Vars, std::size_t... I>
+constexpr std::size_t count_reductions(std::index_sequence<I...>) {
+    return (std::size_t(0) + ... + (is_reduction<std::decay_t<std::tuple_element_t<I, Vars>>>::value ? 1 : 0));
+}
+template <std::size_t... R>
+constexpr bool distinct_positions() {
+    constexpr std::size_t r[] = {R...};
+    for (std::size_t i = 0; i < sizeof...(R); ++i)
+        for (std::size_t j = i + 1; j < sizeof...(R); ++j)
+            if (r[i] == r[j]) return false;
+    return true;
+}
+
+// The reduction loop: every reduction's kernels on the loop's stream, the
+// views back in one result slot (8 bytes each), and one exit_iteration that
+// folds all of them -- under par(task) on the completion, so the live-out
+// variables are final once the future is ready (not only after get()).
+template <typename P, typename Vars, std::size_t N, typename... A>
+result_t<P, void> for_loop_reductions(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n, A const&... parts) {
+    static_assert(distinct_positions<A::red...>(), "for_loop: each reduction is accumulated by one body");
+    static_assert(count_reductions<Vars>(std::make_index_sequence<N>{}) == sizeof...(A),
+                  "for_loop: every reduction argument needs a loop_accumulate in the body");
+    auto const& t = target_of(p, std::get<0>(v));
+    auto slot = t.make_result_slot();
+    std::vector<std::function<void(unsigned char const*)>> folds;
+    std::size_t k = 0;
+    (folds.push_back(launch_accumulate(t, v, st, n, parts, static_cast<char*>(slot.device()) + 8 * k++)), ...);
+    fetch_slot(t, slot, 8 * sizeof...(A), "for_loop_n result");
     return finish_slot<void>(p, t, std::move(slot), [](unsigned char const*) {},
-                             [var, op](unsigned char const* b) {
-                                 T view;
-                                 std::memcpy(&view, b, sizeof(T));
-                                 *var = op(*var, view);
+                             [folds = std::move(folds)](unsigned char const* b) {
+                                 for (std::size_t i = 0; i < folds.size(); ++i) folds[i](b + 8 * i);
                              });
+}
+template <typename P, typename Vars, std::size_t N, std::size_t Red, typename F, std::size_t... In>
+result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n,
+                                compute::hip::functional::loop_accumulate<Red, F, In...> const& b) {
+    return for_loop_reductions(std::forward<P>(p), v, st, n, b);
+}
+// several reductions (for_loop.hpp:802-812)
+template <typename P, typename Vars, std::size_t N, typename... A>
+result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n,
+                                compute::hip::functional::loop_accumulate_all<A...> const& b) {
+    return std::apply(
+        [&](A const&... parts) { return for_loop_reductions(std::forward<P>(p), v, st, n, parts...); }, b.parts);
 }
 template <typename P, typename Vars, std::size_t N, std::size_t Out, typename F, std::size_t In0>
 result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n,
@@ -915,11 +967,6 @@ result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, ui
         [] {});
 }
 
-template <typename T>
-struct is_reduction : std::false_type {};
-template <typename T, typename Op>
-struct is_reduction<reduction_helper<T, Op>> : std::true_type {};
-
 // Any other body: body(first + i*stride, induction_k + i*stride_k, ...) on a
 // kernel instantiated for it (hipcc only).  Loop variables reach the body as
 // raw device pointers, as in for_loop_compute.cu:40-48 (`int* A, int* B, int* C`).
@@ -945,6 +992,8 @@ template <std::size_t Out, typename F, std::size_t... In>
 struct is_builtin_body<compute::hip::functional::loop_assign<Out, F, In...>> : std::true_type {};
 template <std::size_t Red, typename F, std::size_t... In>
 struct is_builtin_body<compute::hip::functional::loop_accumulate<Red, F, In...>> : std::true_type {};
+template <typename... A>
+struct is_builtin_body<compute::hip::functional::loop_accumulate_all<A...>> : std::true_type {};
 
 template <typename P, typename Vars, std::size_t N, typename B,
           typename = std::enable_if_t<!is_builtin_body<std::decay_t<B>>::value>>

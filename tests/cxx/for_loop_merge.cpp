@@ -135,6 +135,32 @@ void test_for_loop_reduction(std::mt19937& gen) {
     hpx::parallel::for_loop_n(ex::par.on(exec), d.begin(), c.size(), hpx::parallel::induction(de.begin()),
                               hpx::parallel::reduction_plus(ip), dot);
     HPX_TEST_EQ(ip, std::inner_product(c.begin(), c.end(), e.begin(), T(5)));
+
+    // several reductions in one loop (for_loop.hpp:802-812): sum, min, max
+    // and the inner product with an induction, sync and task forms
+    for (bool task : {false, true}) {
+        T s2 = 7, lo = c[1], hi = c[1], ip2 = 11;
+        auto all = fn::accumulate_all(fn::loop_accumulate<1, fn::identity, 0>{},
+                                      fn::loop_accumulate<2, fn::identity, 0>{},
+                                      fn::loop_accumulate<3, fn::identity, 0>{},
+                                      fn::loop_accumulate<5, fn::multiply, 0, 4>{});
+        auto args = [&](auto pol) {
+            return hpx::parallel::for_loop_n(pol, d.begin(), c.size(), hpx::parallel::reduction_plus(s2),
+                                             hpx::parallel::reduction_min(lo), hpx::parallel::reduction_max(hi),
+                                             hpx::parallel::induction(de.begin()), hpx::parallel::reduction_plus(ip2),
+                                             all);
+        };
+        if (task) {
+            hpx::future<void> fa = args(ex::par(ex::task).on(exec));
+            fa.get();
+        } else {
+            args(ex::par.on(exec));
+        }
+        HPX_TEST_EQ(s2, std::accumulate(c.begin(), c.end(), T(7)));
+        HPX_TEST_EQ(lo, *std::min_element(c.begin(), c.end()));
+        HPX_TEST_EQ(hi, *std::max_element(c.begin(), c.end()));
+        HPX_TEST_EQ(ip2, std::inner_product(c.begin(), c.end(), e.begin(), T(11)));
+    }
 }
 
 // Task-form reduce / transform_reduce / copy_if with inline temporary

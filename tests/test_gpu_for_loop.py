@@ -131,6 +131,29 @@ def test_for_loop_reduction_bits(gpu_target, which):
     assert int(v[0]) == int(op.reduce(c, initial=ident))
 
 
+@pytest.mark.parametrize("task", [False, True])
+def test_for_loop_several_reductions(gpu_target, task):
+    """for_loop_n(policy, first, size, reduction..., reduction..., f) takes
+    any number of reductions (for_loop.hpp:802-812): sum, min and max of one
+    range plus the inner product with an induction, in one loop; every
+    live-out variable is folded with its own combiner."""
+    rng = np.random.default_rng(6)
+    a = rng.integers(-1000, 1000, 100003, dtype=np.int64)
+    b = rng.integers(-1000, 1000, 100003, dtype=np.int64)
+    da, db = hpx.vector.from_host(a, gpu_target), hpx.vector.from_host(b, gpu_target)
+    pol = (ex.par(ex.task) if task else ex.par).on(hpx.default_executor(gpu_target))
+    s, lo, hi, dot = (np.array([v], np.int64) for v in (5, a[0], a[0], 7))
+    r = P.for_loop_n(pol, da.begin(), len(a), P.reduction_plus(s), P.reduction_min(lo), P.reduction_max(hi),
+                     P.induction(db.begin()), P.reduction_plus(dot),
+                     F.accumulate_all(F.accumulate(1, F.identity(), 0), F.accumulate(2, F.identity(), 0),
+                                      F.accumulate(3, F.identity(), 0), F.accumulate(5, F.multiply(), 0, 4)))
+    if task:
+        r.get()
+    assert int(s[0]) == 5 + int(a.sum())
+    assert int(lo[0]) == int(a.min()) and int(hi[0]) == int(a.max())
+    assert int(dot[0]) == 7 + int(np.dot(a, b))
+
+
 def test_for_loop_reduction_inner_product_and_empty(gpu_target):
     """A reduction body reading the loop iterator and an induction
     (transform_reduce_binary kernels); an empty loop leaves var op identity."""
@@ -156,7 +179,7 @@ def test_for_loop_reduction_argument_checks(gpu_target):
         P.for_loop_n(pol, d.begin(), 16, P.reduction_plus(s), F.assign(0, F.add_value(1), 0))
     with pytest.raises(IndexError):  # accumulate must name the reduction's position
         P.for_loop_n(pol, d.begin(), 16, P.reduction_plus(s), F.accumulate(0, F.identity(), 0))
-    with pytest.raises(TypeError):
+    with pytest.raises(ValueError):  # two reductions, only one accumulated
         P.for_loop_n(pol, d.begin(), 16, P.reduction_plus(s), P.reduction_plus(s),
                      F.accumulate(1, F.identity(), 0))
     with pytest.raises(ValueError):  # the induction read by the body runs past its vector

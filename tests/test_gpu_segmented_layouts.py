@@ -74,6 +74,10 @@ def test_scan_and_transform_mixed_layouts(gpu_target, kin, kout):
     S.algorithms.exclusive_scan(pol, pv.begin(), pv.end(), out.begin(), 5)
     gpu_target.synchronize()
     np.testing.assert_array_equal(out.local.to_host(), O.segmented_scan(x, 5, kin or 1, False))
+    # segmented transform_exclusive_scan (transform_exclusive_scan.hpp:317 argument order)
+    S.algorithms.transform_exclusive_scan(pol, pv.begin(), pv.end(), out.begin(), -4, F.plus, F.multiply_step(3))
+    gpu_target.synchronize()
+    np.testing.assert_array_equal(out.local.to_host(), np.concatenate([[-4], -4 + np.cumsum(3 * x)[:-1]]))
     S.algorithms.transform(pol, pv.begin() + 10, pv.end(), out.begin(), F.add_value(7))
     gpu_target.synchronize()
     np.testing.assert_array_equal(out.local.to_host()[:n - 10], x[10:] + 7)

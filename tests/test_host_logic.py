@@ -32,3 +32,16 @@ def test_reduction_live_out_checks():
         P.reduction(np.zeros(1), 0.0, lambda a, b: a + b)  # not an hpx_amd combiner
     with pytest.raises(TypeError):
         F.accumulate(1, F.identity(), 0, 1)
+
+
+def test_accumulate_all_validation():
+    """Several reductions per for_loop (for_loop.hpp:802-812): accumulate_all
+    takes one accumulate per reduction position; the loop checks that every
+    reduction argument is named exactly once (no device needed: the checks
+    run before any launch)."""
+    with pytest.raises(ValueError):
+        F.accumulate_all(F.accumulate(1, F.identity(), 0), F.accumulate(1, F.square(), 0))
+    with pytest.raises(TypeError):
+        F.accumulate_all()
+    body = F.accumulate_all(F.accumulate(1, F.identity(), 0), F.accumulate(2, F.square(), 0))
+    assert [a.red for a in body.parts] == [1, 2]

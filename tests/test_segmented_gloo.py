@@ -35,7 +35,7 @@ class NumpyEngine:
 
     def reduce_into(self, vec, lo, hi, op, conv, acc_dt, out):
         dt = np.dtype(vec.dtype)
-        x = vec[lo:hi].astype(dt)
+        x = [dt.type(conv(v)) for v in vec[lo:hi].astype(dt)]
         ident = S._identity(op.kind, {np.dtype(np.int64): 2, np.dtype(np.float64): 5}[dt])
         r = np.array([ident], dt)[0]
         for v in x:
@@ -59,7 +59,7 @@ class NumpyEngine:
         dt = src.dtype
         acc = self._w2v(carry[:1], dt)[0]
         for i in range(lo, hi):
-            nxt = OPS[op.kind](acc, src[i])
+            nxt = OPS[op.kind](acc, dt.type(conv(src[i])))
             dst[dlo + i - lo] = nxt if inclusive else acc
             acc = nxt
 
@@ -134,6 +134,9 @@ def _layout_worker(rank, size, port, q):
             alg.exclusive_scan(None, pi.begin() + 17, pi.end() - 5, out.begin() + 17, 2)
             res[("excl_sub", name)] = (out.lo, out.local.copy())
             res[("parts", name)] = (pi.get_num_partitions(), pi.my_segments())
+            # transform_exclusive_scan (segmented_algorithms/transform_exclusive_scan.hpp:31)
+            alg.transform_exclusive_scan(None, pi.begin(), pi.end(), out.begin(), -4, F.plus, F.multiply_step(3))
+            res[("texcl", name)] = (out.lo, out.local.copy())
             fo = HostPV(np.zeros(n, np.float64), comm, lay)
             alg.inclusive_scan(None, pf.begin(), pf.end(), fo.begin(), F.plus, 0.25)
             res[("incl_f64", name)] = (fo.lo, fo.local.copy())
@@ -263,6 +266,9 @@ def test_partitioned_vector_layouts_gloo(size):
         np.testing.assert_array_equal(sub[17:n - 5], exp)
         np.testing.assert_array_equal(_gather(results, ("incl_f64", name), n, np.float64),
                                       O.segmented_scan(xf, 0.25, k, True))
+        # transform_exclusive_scan(init -4, plus, x -> 3x): exact for integers
+        np.testing.assert_array_equal(_gather(results, ("texcl", name), n),
+                                      np.concatenate([[-4], -4 + np.cumsum(3 * x)[:-1]]))
     for name in ("loc->3", "loc->10", "7->loc", "3->1"):
         np.testing.assert_array_equal(_gather(results, ("mixed", name), n), np.cumsum(x))
         np.testing.assert_array_equal(_gather(results, ("mixed_transform", name), n), x + 5)
