@@ -970,11 +970,64 @@ result_t<P, void> for_loop_body(P&& p, Vars const& v, strides_t<N> const& st, ui
 // Any other body: body(first + i*stride, induction_k + i*stride_k, ...) on a
 // kernel instantiated for it (hipcc only).  Loop variables reach the body as
 // raw device pointers, as in for_loop_compute.cu:40-48 (`int* A, int* B, int* C`).
+// A generic body with reductions (hipcc only): body(first + i*stride,
+// induction_k + i*stride_k, ..., T& view_r, ...) -- every reduction reaches
+// the body as a reference to the thread's private view, which starts at the
+// reduction's identity (for_loop_reduction.hpp:35-132); the views are
+// combined on the device in a fixed order (device_closures.hpp) and folded
+// into the live-out variables on the loop's completion.
+template <typename V>
+auto loop_reduce_arg(V const& x, int64_t stride) {
+    if constexpr (is_reduction<V>::value) {
+        using T = std::decay_t<decltype(x.identity_)>;
+        using Op = std::decay_t<decltype(x.op_)>;
+        (void)stride;
+        return red_arg<T, Op>{x.identity_, x.op_};
+    } else {
+        return strided_ptr<std::remove_pointer_t<std::decay_t<decltype(raw_ptr(x))>>>{raw_ptr(x), stride};
+    }
+}
+template <typename P, typename Vars, std::size_t N, typename B, std::size_t... I>
+result_t<P, void> for_loop_generic_reduce(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n, B const& body,
+                                          std::index_sequence<I...>) {
+    auto const& t = target_of(p, std::get<0>(v));
+    constexpr std::size_t nred = count_reductions<Vars>(std::index_sequence<I...>{});
+    auto slot = t.make_result_slot();
+    void* ws = nullptr;
+    check(hpxhip_stream_scratch(t.stream(), kLoopReduceMaxBlocks * nred * sizeof(uint64_t), &ws),
+          "for_loop reduction scratch");
+    auto* partials = static_cast<uint64_t*>(ws);
+    device_loop_reduce(t, body, n, partials, static_cast<uint64_t*>(slot.device()),
+                       loop_reduce_arg(std::get<I>(v), st[I])...);
+    fetch_slot(t, slot, 8 * nred, "for_loop_n result");
+    std::vector<std::function<void(unsigned char const*)>> folds;
+    (
+        [&] {
+            auto const& x = std::get<I>(v);
+            if constexpr (is_reduction<std::decay_t<decltype(x)>>::value) {
+                using T = std::decay_t<decltype(x.identity_)>;
+                T* var = &x.var_;
+                auto op = x.op_;
+                folds.push_back([var, op](unsigned char const* b) {
+                    T view;
+                    std::memcpy(&view, b, sizeof(T));
+                    *var = op(*var, view);
+                });
+            }
+        }(),
+        ...);
+    return finish_slot<void>(p, t, std::move(slot), [](unsigned char const*) {},
+                             [folds = std::move(folds)](unsigned char const* b) {
+                                 for (std::size_t k = 0; k < folds.size(); ++k) folds[k](b + 8 * k);
+                             });
+}
+
 template <typename P, typename Vars, std::size_t N, typename B, std::size_t... I>
 result_t<P, void> for_loop_generic(P&& p, Vars const& v, strides_t<N> const& st, uint64_t n, B const& body,
-                                   std::index_sequence<I...>) {
-    static_assert(!(is_reduction<std::decay_t<std::tuple_element_t<I, Vars>>>::value || ...),
-                  "for_loop: reductions need a functional::loop_accumulate body");
+                                   std::index_sequence<I...> seq) {
+    if constexpr ((is_reduction<std::decay_t<std::tuple_element_t<I, Vars>>>::value || ...)) {
+        return for_loop_generic_reduce(std::forward<P>(p), v, st, n, body, seq);
+    } else {
     auto ptrs = std::make_tuple(raw_ptr(std::get<I>(v))...);
     return run_elementwise<void>(
         p, std::get<0>(v), n,
@@ -985,6 +1038,7 @@ result_t<P, void> for_loop_generic(P&& p, Vars const& v, strides_t<N> const& st,
                             std::get<I>(ptrs) + o * st[I], st[I]}...);
         },
         [] {});
+    }
 }
 template <typename Body>
 struct is_builtin_body : std::false_type {};

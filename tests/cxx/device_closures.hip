@@ -217,6 +217,56 @@ void test_concurrent_algorithms(std::mt19937& gen) {
         if (!HPX_TEST_EQ(he[i], h[i] * h[i] - 3)) break;
 }
 
+// for_loop with a lambda body and reductions (for_loop_reduction.hpp:35-132,
+// for_loop_reduction.cpp's bodies with device iterators): each reduction
+// reaches the body as a reference to a private view; several reductions and
+// an induction in one loop, sync and task forms, an empty loop.
+void test_for_loop_lambda_reductions(std::mt19937& gen) {
+    using T = int64_t;
+    std::vector<T> h(1000003), g(h.size());
+    std::uniform_int_distribution<T> dis(-1000, 1000);
+    for (auto& x : h) x = dis(gen);
+    for (auto& x : g) x = dis(gen);
+    hip::target t;
+    hip::allocator<T> a(t);
+    hpx::compute::vector<T, hip::allocator<T>> d(h.size(), a), e(g.size(), a);
+    hpx::parallel::copy(ex::par, h.begin(), h.end(), d.begin());
+    hpx::parallel::copy(ex::par, g.begin(), g.end(), e.begin());
+    hip::default_executor exec(t);
+    for (bool task : {false, true}) {
+        T sum = 3, mx = h[0], dot = -5;
+        uint64_t odd = 0;
+        auto body = [] HPX_HOST_DEVICE(T * x, T & s, T & m, T * y, T & dp, uint64_t & o) {
+            s += *x;
+            m = *x > m ? *x : m;
+            dp += *x * *y;
+            o += (*x & 1) ? 1u : 0u;
+        };
+        auto run = [&](auto pol) {
+            return hpx::parallel::for_loop_n(pol, d.data(), h.size(), hpx::parallel::reduction_plus(sum),
+                                             hpx::parallel::reduction_max(mx), hpx::parallel::induction(e.data()),
+                                             hpx::parallel::reduction_plus(dot), hpx::parallel::reduction_plus(odd),
+                                             body);
+        };
+        if (task) {
+            hpx::future<void> f = run(ex::par(ex::task).on(exec));
+            f.wait();  // the live-outs are final once the future is ready
+            f.get();
+        } else {
+            run(ex::par.on(exec));
+        }
+        HPX_TEST_EQ(sum, std::accumulate(h.begin(), h.end(), T(3)));
+        HPX_TEST_EQ(mx, *std::max_element(h.begin(), h.end()));
+        HPX_TEST_EQ(dot, std::inner_product(h.begin(), h.end(), g.begin(), T(-5)));
+        HPX_TEST_EQ(odd, uint64_t(std::count_if(h.begin(), h.end(), [](T x) { return (x & 1) != 0; })));
+    }
+    // an empty loop leaves every live-out at var (op) identity
+    double p = 2.5;
+    hpx::parallel::for_loop_n(ex::par.on(exec), d.data(), 0, hpx::parallel::reduction_multiplies(p),
+                              [] HPX_HOST_DEVICE(T * x, double& q) { q *= double(*x); });
+    HPX_TEST_EQ(p, 2.5);
+}
+
 int hpx_main(int argc, char* argv[]) {
     unsigned seed = argc > 1 ? unsigned(std::strtoul(argv[1], nullptr, 10)) : std::random_device{}();
     std::cout << "using seed: " << seed << std::endl;
@@ -229,6 +279,7 @@ int hpx_main(int argc, char* argv[]) {
     hip::concurrent_executor cexec(target, 3);
     test_executor(cexec, target, gen, "concurrent_executor");
     test_concurrent_algorithms(gen);
+    test_for_loop_lambda_reductions(gen);
     return hpx::finalize();
 }
 
