@@ -30,9 +30,22 @@ using namespace hpxhip::scan_detail;
 // with the smallest tiles (8 rounds), so one size serves every launch.
 constexpr size_t kSlotsOff = 256;
 
-template <typename T, int ROUNDS>
+template <typename T, int ROUNDS, int THREADS = kThreads>
 uint64_t ntiles_for(uint64_t n) {
-    return (n + tile_elems<T, ROUNDS>() - 1) / tile_elems<T, ROUNDS>();
+    return (n + tile_elems<T, ROUNDS, THREADS>() - 1) / tile_elems<T, ROUNDS, THREADS>();
+}
+
+// Workgroup size per variant (r03): aligned 8-byte scans run 512-thread
+// tiles of 16 rounds (128 KiB), two workgroups per CU -- with the fixed
+// look-back one workgroup's loads and stores now overlap the other's scan:
+// 2^30 int64 2.635-2.638 -> 2.580-2.581 ms, f64 2.607-2.612 -> 2.591-2.592
+// (profiles/r03_ubench_scan7_shapes.log; with the variable-window look-back
+// the same shape had been slower, r02_ubench_scan_shapes_blockidx.log).
+// The tile has as many elements as a 1024 x 8 one, so the scratch sizing
+// below covers it; float (12 rounds) and the element-wise path keep 1024.
+template <typename T, bool ALIGNED>
+constexpr int threads_for() {
+    return (ALIGNED && (std::is_integral_v<T> || sizeof(T) == 8) && rounds_for<T, ALIGNED>() == 16) ? 512 : kThreads;
 }
 
 // [counter | tile slots | head carry]: the carry of a split-off head
@@ -50,11 +63,14 @@ template <typename T, bool INCL, bool ALIGNED, typename Conv, typename Op>
 int launch_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init, const T* prefix_dev, char* ws,
                 hipStream_t s) {
     constexpr int R = rounds_for<T, ALIGNED>();
-    const uint64_t ntiles = ntiles_for<T, R>(n);
+    constexpr int TH = threads_for<T, ALIGNED>();
+    static_assert(tile_elems<T, R, TH>() >= tile_elems<T, 8>(), "scratch is sized for 1024 x 8-round tiles");
+    const uint64_t ntiles = ntiles_for<T, R, TH>(n);
     HPXHIP_CHECK(hipMemsetAsync(ws, 0, align_up(kSlotsOff + ntiles * tile_state<T>::bytes_per_tile(), 256), s));
     tile_state<T> st{reinterpret_cast<uint64_t*>(ws + kSlotsOff), device_error_word(s)};
-    hipLaunchKernelGGL((k_scan<T, Conv, Op, INCL, ALIGNED, R>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads),
-                       0, s, in, out, n, conv, op, init, prefix_dev, reinterpret_cast<uint32_t*>(ws), st);
+    hipLaunchKernelGGL((k_scan<T, Conv, Op, INCL, ALIGNED, R, TH, true, TH == kThreads ? 1 : 4>),
+                       dim3(static_cast<unsigned>(ntiles)), dim3(TH), 0, s, in, out, n, conv, op, init, prefix_dev,
+                       reinterpret_cast<uint32_t*>(ws), st);
     HPXHIP_CHECK_LAUNCH();
     return 0;
 }
