@@ -12,9 +12,9 @@ namespace copy_if_detail {
 constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / kWave;
 
-template <typename T, int ROUNDS>
+template <typename T, int ROUNDS, int THREADS = kThreads>
 constexpr uint64_t tile_elems() {
-    return static_cast<uint64_t>(kThreads) * ROUNDS * (16 / sizeof(T));
+    return static_cast<uint64_t>(THREADS) * ROUNDS * (16 / sizeof(T));
 }
 
 __device__ __forceinline__ uint32_t rank_below(uint64_t mask) {
@@ -34,23 +34,25 @@ using hit_word = std::conditional_t<(BITS <= 32), uint32_t, uint64_t>;
 // SV: tile-state value type (uint32_t halves the look-back granules; valid
 // while n < 2^32).
 template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4, int ABL = 0, typename SV = uint64_t,
-          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = false, int RPB = 1, bool FIXED = false>
-__global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out, uint64_t n, Pred pred,
+          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = false, int RPB = 1, bool FIXED = false,
+          int THREADS = kThreads>
+__global__ __launch_bounds__(THREADS, MINW) void k_copy_if(const T* in, T* out, uint64_t n, Pred pred,
                                                        uint64_t* count_dev, uint32_t* counter,
                                                        tile_state<SV> st, uint64_t ntiles,
                                                        const uint64_t* prefix0 = nullptr) {
     constexpr int V = 16 / sizeof(T);
-    constexpr uint64_t TILE = tile_elems<T, ROUNDS>();
-    constexpr uint64_t WAVE_ELEMS = TILE / kWaves;
+    constexpr int WAVES = THREADS / kWave;
+    constexpr uint64_t TILE = tile_elems<T, ROUNDS, THREADS>();
+    constexpr uint64_t WAVE_ELEMS = TILE / WAVES;
     using VT = vec<T, V>;
     using H = hit_word<ROUNDS * V>;
     static_assert(ROUNDS * V <= 64, "hit bits per lane");
 
     __shared__ uint32_t s_tile;
-    __shared__ uint32_t s_wave_total[kWaves];
+    __shared__ uint32_t s_wave_total[WAVES];
     __shared__ uint64_t s_prefix;
     static_assert(ROUNDS % RPB == 0, "rounds per write-out batch");
-    __shared__ T s_stage[kWaves][kWave * V * RPB];  // RPB wave rounds of hits, compacted
+    __shared__ T s_stage[WAVES][kWave * V * RPB];  // RPB wave rounds of hits, compacted
 
     if constexpr (DYN_ID) {  // ablation: tile ids from the atomic counter
         if (threadIdx.x == 0)
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if(const T* in, T* out,
     __syncthreads();
     uint32_t wave_prefix = 0, agg = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
+    for (int w = 0; w < WAVES; ++w) {
         if (w < wave) wave_prefix += s_wave_total[w];
         agg += s_wave_total[w];
     }

@@ -2,7 +2,9 @@
 // (FIXED: tiles read their group's published aggregates plus one group
 // prefix word, lookback.hpp exclusive_prefix_fixed) against the shipped
 // variable-window look-back, tile ids from the counter and from blockIdx
-// (int32 also at 6 and 4 rounds: 8 rounds spill 12-14 VGPRs at 64);
+// (int32 also at 6 and 4 rounds: 8 rounds spill 12-14 VGPRs at 64), and
+// with the fixed look-back, nt stores and RPB-round write-out batches (int64);
+// then (after those shipped) 512- and 256-thread tiles, more workgroups per CU;
 // int64 at 2^30 and int32 at 2^31, predicate !(x < 0) on ~50 % hits.  Each
 // variant's output is compared element for element with the first run's.
 // build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../include -I../../hpx_amd/csrc copyif7.hip -o copyif7
@@ -32,15 +34,15 @@ struct harness {
   using P = pred_fn<HPXHIP_P_NOT_LT, T>;
   uint64_t N; T *in, *out, *ref_out; char* ws; uint32_t* err; uint64_t* cnt; unsigned long long* bad;
   hipEvent_t e0, e1; uint64_t ref = 0;
-  template <bool DYN, bool FIXED, int R = 8>
+  template <bool DYN, bool FIXED, int R = 8, bool NTS = false, int RPB = 1, int TH = kThreads, int MINW = 8>
   void run(const char* name) {
     using SV = uint32_t;
-    const uint64_t ntiles = (N + tile_elems<T, R>() - 1) / tile_elems<T, R>();
+    const uint64_t ntiles = (N + tile_elems<T, R, TH>() - 1) / tile_elems<T, R, TH>();
     const size_t total = align_up(256 + ntiles * tile_state<SV>::bytes_per_tile(), 256);
     tile_state<SV> st{reinterpret_cast<uint64_t*>(ws + 256), err};
     auto launch = [&] {
       CK(hipMemsetAsync(ws, 0, total, 0));
-      k_copy_if<T, P, true, R, 8, 0, SV, DYN, false, 1, FIXED><<<ntiles, kThreads>>>(in, out, N, P{0}, cnt,
+      k_copy_if<T, P, true, R, MINW, 0, SV, DYN, NTS, RPB, FIXED, TH><<<ntiles, TH>>>(in, out, N, P{0}, cnt,
           reinterpret_cast<uint32_t*>(ws), st, ntiles);
     };
     launch(); CK(hipDeviceSynchronize());
@@ -74,19 +76,16 @@ int main() {
     {
       harness<int64_t> h{1ull << 30, (int64_t*)in, (int64_t*)out, (int64_t*)ref_out, ws, err, cnt, bad, e0, e1};
       k_fill<int64_t><<<((1ull << 30) + 255) / 256, 256>>>(h.in, h.N); CK(hipDeviceSynchronize());
-      h.run<true, false>("atomic (shipped)");
-      h.run<true, true>("atomic fixed-assoc");
-      h.run<false, false>("blockIdx");
-      h.run<false, true>("blockIdx fixed-assoc");
+      h.run<false, true, 8, false, 4>("T1024 R8 RPB4 2/CU (shipped)");
+      h.run<false, true, 8, false, 4, 512, 8>("T512 R8 RPB4 4/CU");
+      h.run<false, true, 16, false, 2, 512, 4>("T512 R16 RPB2 2/CU");
+      h.run<false, true, 8, false, 4, 256, 8>("T256 R8 RPB4 8/CU");
     }
     {
       harness<int32_t> h{1ull << 31, (int32_t*)in, (int32_t*)out, (int32_t*)ref_out, ws, err, cnt, bad, e0, e1};
       k_fill<int32_t><<<((1ull << 31) + 255) / 256, 256>>>(h.in, h.N); CK(hipDeviceSynchronize());
-      h.run<true, false>("atomic (shipped)");
-      h.run<true, true>("atomic fixed-assoc");
-      h.run<false, true>("blockIdx fixed-assoc");
-      h.run<true, true, 6>("atomic fixed-assoc R6");
-      h.run<true, true, 4>("atomic fixed-assoc R4");
+      h.run<false, true>("i32 T1024 R8 2/CU (shipped)");
+      h.run<false, true, 8, false, 1, 512, 8>("i32 T512 R8 4/CU");
     }
   }
   uint32_t e = 0; CK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost)); printf("deverr %u\n", e);
