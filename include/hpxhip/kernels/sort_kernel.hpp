@@ -271,7 +271,14 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
 #pragma unroll
         for (int w = 0; w < R / kWave; ++w)
             if (w < wave) pre += s_wsum[w];
-        s_local[t] = pre + count_incl - tile_count;
+        const uint32_t loc = pre + count_incl - tile_count;
+        s_local[t] = loc;
+        // the per-wave offsets become tile positions (< TILE fits CT), so
+        // the scatter reads one LDS word per key instead of two
+        if constexpr (STAGE) {
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) s_whist[w][t] = static_cast<CT>(s_whist[w][t] + loc);
+        }
     }
     __syncthreads();
 
@@ -281,7 +288,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
         const uint64_t i = wbase + r * kWave + lane;
         if (STAGE && (full || i < n)) {
             const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
-            const uint32_t pos = s_local[d] + s_whist[wave][d] + rank[r];
+            const uint32_t pos = s_whist[wave][d] + rank[r];
             s_keys[pos] = k[r];
             if constexpr (HAS_VAL) s_vals[pos] = v[r];
         }
@@ -457,7 +464,6 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     __shared__ alignas(16) U s_keys[THREADS * ITEMS];
     __shared__ alignas(16) VAL s_vals[HAS_VAL ? THREADS * ITEMS : 1];
     __shared__ uint16_t s_whist[WAVES][kRadix];
-    __shared__ uint32_t s_local[kRadix];
     __shared__ uint32_t s_wsum[kRadix / kWave];
 
     const int t = threadIdx.x;
@@ -550,7 +556,11 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
 #pragma unroll
             for (int w = 0; w < kRadix / kWave; ++w)
                 if (w < wave) pre += s_wsum[w];
-            s_local[t] = pre + incl - count;
+            // per-wave offsets -> segment positions (< 2^16): one LDS word
+            // per key in the scatter instead of two
+            const uint32_t loc = pre + incl - count;
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) s_whist[w][t] = static_cast<uint16_t>(s_whist[w][t] + loc);
         }
         __syncthreads();
 #pragma unroll
@@ -559,7 +569,7 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
             if (act == 0) break;
             if ((act >> lane) & 1u) {
                 const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
-                const uint32_t pos = s_local[d] + s_whist[wave][d] + ((rank2[r / 2] >> (16 * (r & 1))) & 0xffffu);
+                const uint32_t pos = s_whist[wave][d] + ((rank2[r / 2] >> (16 * (r & 1))) & 0xffffu);
                 s_keys[pos] = k[r];
                 if constexpr (HAS_VAL) s_vals[pos] = v[r];
             }
