@@ -465,6 +465,7 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     __shared__ alignas(16) VAL s_vals[HAS_VAL ? THREADS * ITEMS : 1];
     __shared__ uint16_t s_whist[WAVES][kRadix];
     __shared__ uint32_t s_wsum[kRadix / kWave];
+    __shared__ U s_ends[2];
 
     const int t = threadIdx.x;
     const int wave = t / kWave;
@@ -488,14 +489,6 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     }
     const uint32_t m = static_cast<uint32_t>(mm);
     if (m < 2) return;
-    const U diff = xf(keys[b]) ^ xf(keys[b + m - 1]);
-    int top = top_planned;
-    if (diff) {
-        const int hb = BITS - (sizeof(U) == 8 ? __builtin_clzll(static_cast<uint64_t>(diff))
-                                               : __builtin_clz(static_cast<uint32_t>(diff)));
-        top = hb > top ? hb : top;
-    }
-    if (top <= 0) return;  // all keys equal
 
     const uint32_t wbase = static_cast<uint32_t>(wave) * CHUNK;
     const uint32_t have = m > wbase ? m - wbase : 0u;
@@ -515,6 +508,31 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
         k[r] = on ? ld_stream(&gkeys[wbase + r * kWave + lane]) : U(0);
         if constexpr (HAS_VAL) v[r] = on ? ld_stream(&gvals[wbase + r * kWave + lane]) : VAL(0);
     }
+    // The segment's first and last keys (their highest differing bit is the
+    // top of the LDS passes) come from the registers just loaded, through
+    // LDS: reading them from global memory first had put one more dependent
+    // round trip in front of every segment's loads.
+    {
+        const uint32_t last = m - 1;
+        const uint32_t lw = last / CHUNK, lo = last % CHUNK;
+        if (t == 0) s_ends[0] = k[0];
+        if (static_cast<uint32_t>(wave) == lw && static_cast<uint32_t>(lane) == lo % kWave) {
+            U x = k[0];
+#pragma unroll
+            for (int r = 1; r < ITEMS; ++r)
+                if (static_cast<uint32_t>(r) == lo / kWave) x = k[r];
+            s_ends[1] = x;
+        }
+        __syncthreads();
+    }
+    const U diff = xf(s_ends[0]) ^ xf(s_ends[1]);
+    int top = top_planned;
+    if (diff) {
+        const int hb = BITS - (sizeof(U) == 8 ? __builtin_clzll(static_cast<uint64_t>(diff))
+                                               : __builtin_clz(static_cast<uint32_t>(diff)));
+        top = hb > top ? hb : top;
+    }
+    if (top <= 0) return;  // all keys equal
 
     // one stable pass on the digit at `shift`: registers -> s_keys (ranked)
     auto pass = [&](int shift) {
