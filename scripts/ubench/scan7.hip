@@ -1,7 +1,8 @@
 // Microbenchmark (round 3): f64 inclusive plus-scan tile shapes and the deferred round carry
 // (DEFER: round totals held wave-uniform, carry folded in at the store),
 // and the fixed-association look-back (FIXED, reproducible FP scans); then
-// (after FIXED shipped) tile shapes with several workgroups per CU.  The shipped
+// (after FIXED shipped) tile shapes with several workgroups per CU; then
+// (after the 512 x 16 shape shipped) 384- and 768-thread shapes.  The shipped
 // FP scan runs 1024 threads x 12 rounds (16 spill 24 VGPRs: 4 waves/SIMD cap a
 // wave at 128 registers).  Fewer threads per tile raise the register cap:
 // 512 threads x 32 rounds (2 waves/SIMD, 256 VGPRs) and 256 x 64 (1 wave/SIMD)
@@ -63,15 +64,12 @@ int main() {
   bench<double> bd{N, (double*)in, (double*)out, ws, err, e0, e1};
   for (int rep = 0; rep < 2; ++rep) {
     k_ones<int64_t><<<8192, 256>>>((int64_t*)in, N); CK(hipDeviceSynchronize());
-    bi.shipped<16, 1024, 1, false, true>("i64 T1024 R16 fixed (shipped)");
-    bi.shipped<16, 512, 2, false, true>("i64 T512 R16 2/CU fixed");
-    bi.shipped<8, 1024, 8, false, true>("i64 T1024 R8 2/CU fixed");
-    bi.shipped<16, 256, 4, false, true>("i64 T256 R16 4/CU fixed");
-    bi.shipped<8, 512, 8, false, true>("i64 T512 R8 4/CU fixed");
-    bi.shipped<32, 512, 1, false, true>("i64 T512 R32 1/CU fixed");
-    k_ones<double><<<8192, 256>>>((double*)in, N); CK(hipDeviceSynchronize());
-    bd.shipped<16, 1024, 1, true, true>("f64 T1024 R16 defer fixed (shipped)");
-    bd.shipped<16, 512, 2, true, true>("f64 T512 R16 2/CU defer fixed");
+    bi.shipped<16, 512, 4, false, true>("i64 T512 R16 2/CU fixed (shipped)");
+    bi.shipped<12, 384, 5, false, true>("i64 T384 R12 3/CU fixed");
+    bi.shipped<16, 384, 4, false, true>("i64 T384 R16 2/CU fixed");
+    bi.shipped<12, 512, 4, false, true>("i64 T512 R12 2/CU fixed");
+    bi.shipped<20, 512, 3, false, true>("i64 T512 R20 1/CU fixed");
+    bi.shipped<8, 768, 4, false, true>("i64 T768 R8 fixed");
   }
   uint32_t h = 0; CK(hipMemcpy(&h, err, 4, hipMemcpyDeviceToHost)); printf("deverr %u\n", h);
   return 0;
