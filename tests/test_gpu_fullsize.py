@@ -207,3 +207,25 @@ def test_sort_2p30_oversized_bucket(pol, gpu_target):
     assert P.reduce(pol, keys.begin(), keys.end(), 0, F.bit_xor) == xor0
     assert P.reduce(pol, keys.begin(), keys.end(), 0, F.plus) == sum0
     keys.free()
+
+
+def test_fp_scan_reproducible_2p30(pol, gpu_target):
+    """The fixed-association look-back at the benchmark's size (configs[1]
+    names double): two inclusive scans of the same 2^30 mixed-sign doubles,
+    with other scans launched between them, agree bit for bit (their int64
+    views subtract to zero everywhere, checked on the device)."""
+    n = 1 << 30
+    x = hpx.vector(n, dtype=np.float64, tgt=gpu_target)
+    P.generate(pol, x.begin(), x.end(), "unit", 0xF00D)
+    P.transform(pol, x.begin(), x.end(), x.begin(), F.add_value(-0.5))
+    y1 = hpx.vector(n, dtype=np.float64, tgt=gpu_target)
+    y2 = hpx.vector(n, dtype=np.float64, tgt=gpu_target)
+    P.inclusive_scan(pol, x.begin(), x.end(), y1.begin(), F.plus, 0.0)
+    P.exclusive_scan(pol, x.begin(), x.end(), y2.begin(), 0.0)  # other work in between
+    P.inclusive_scan(pol, x.begin() + 1, x.end(), y2.begin() + 1, F.plus, 0.0)
+    P.inclusive_scan(pol, x.begin(), x.end(), y2.begin(), F.plus, 0.0)
+    d = hpx.vector(n, dtype=np.int64, tgt=gpu_target)
+    L.call("hpxhip_transform_binary", L.I64, L.I64, L.I64, L.B_SUB, L.scalars_buf(L.I64, []),
+           ctypes.c_void_p(y1.data()), ctypes.c_void_p(y2.data()), ctypes.c_void_p(d.data()), n, gpu_target.stream)
+    assert P.reduce(pol, d.begin(), d.end(), 0, F.bit_or) == 0
+    assert np.isfinite(window(y1, n - 1, 1, np.float64)[0])
