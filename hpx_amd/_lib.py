@@ -155,6 +155,9 @@ def _preload_torch():
         pass
 
 
+ABI_VERSION = 1  # HPXHIP_ABI_VERSION, include/hpxhip.h
+
+
 def load(path: str | None = None):
     """Load (once) and return the ctypes library; raises if it is missing."""
     global _lib
@@ -174,6 +177,10 @@ def load(path: str | None = None):
             fn.restype = ctypes.c_int
         lib.hpxhip_error_string.argtypes = [ctypes.c_int]
         lib.hpxhip_error_string.restype = ctypes.c_char_p
+        # the binding and the library must agree on the C ABI (include/hpxhip.h)
+        got = lib.hpxhip_abi_version()
+        if got != ABI_VERSION:
+            raise ImportError(f"hpx_amd: {p} implements C ABI version {got}, this binding expects {ABI_VERSION}")
         _lib = lib
         return lib
 
