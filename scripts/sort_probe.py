@@ -2,7 +2,7 @@
 keys at 2^20..2^30, device time from HIP events (best of 3, generation
 subtracted), host time of the call itself, and an is_sorted + checksum
 check of every result.  usage: python scripts/sort_probe.py [maxlog]
-(SORT_ONLY=u64|u32|pairs: that case at 2^maxlog only)."""
+(SORT_ONLY=u64|u32|pairs|u64r16|u64r24: that case at 2^maxlog only)."""
 import ctypes
 import os
 import sys
@@ -36,13 +36,16 @@ def ms(a, b):
     return f.value
 
 
-def run(dt, logn, kv=False, reps=3):
+def run(dt, logn, kv=False, reps=3, key_range=None):
     n = 1 << logn
     k = hpx.vector(n, dtype=dt, tgt=t)
     v = hpx.vector(n, dtype=np.uint64, tgt=t) if kv else None
     best, host = 1e30, 1e30
     for r in range(reps):
-        P.generate(pol, k.begin(), k.end(), "bits", 7 + r)
+        if key_range:
+            P.generate(pol, k.begin(), k.end(), "range", 7 + r, 0, key_range - 1)
+        else:
+            P.generate(pol, k.begin(), k.end(), "bits", 7 + r)
         if kv:
             P.generate(pol, v.begin(), v.end(), "iota", 0, 0, 0)
         t.synchronize()
@@ -71,8 +74,11 @@ maxlog = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 only = os.environ.get("SORT_ONLY")
 print(f"{'case':28s} {'ms':>9s} {'Gkeys/s':>8s} {'host_ms':>8s} ok", flush=True)
 if only:
-    dt, kv = {"u64": (np.uint64, False), "u32": (np.uint32, False), "pairs": (np.uint64, True)}[only]
-    d, h, ok = run(dt, maxlog, kv, reps=2)
+    # u64r16 / u64r24: keys below 2^16 / 2^24 (two / three live digits)
+    dt, kv, kr = {"u64": (np.uint64, False, None), "u32": (np.uint32, False, None),
+                  "pairs": (np.uint64, True, None), "u64r16": (np.uint64, False, 1 << 16),
+                  "u64r24": (np.uint64, False, 1 << 24)}[only]
+    d, h, ok = run(dt, maxlog, kv, reps=2, key_range=kr)
     print(f"{only + ' 2^' + str(maxlog):28s} {d:9.3f} {(1 << maxlog) / d / 1e6:8.2f} {h:8.3f} {ok}", flush=True)
     sys.exit(0)
 for logn in range(20, maxlog + 1, 2):
