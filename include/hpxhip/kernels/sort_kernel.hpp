@@ -199,13 +199,19 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     __shared__ U s_keys[STAGE ? TILE : 1];
     __shared__ VAL s_vals[(HAS_VAL && STAGE) ? TILE : 1];
 
-    const int t = threadIdx.x;
-    const int wave = t / kWave;
-    const int lane = lane_id();
+    const int t_id = threadIdx.x;
+    const int lane_ = lane_id();
     // one tile; the persistent form calls it in a loop, the plain form once
     // (a loop around the body in the plain form changes its register
     // allocation)
     auto one = [&]() -> bool {
+    int t = t_id, lane = lane_;
+    // persistent form: the thread and lane ids are re-derived per tile, so
+    // the compiler does not hoist every lane-dependent address of the body
+    // out of the tile loop (kept live across it, those had taken the kernel
+    // from 94 to 156 VGPRs: one workgroup per CU instead of two)
+    if constexpr (PERSIST) asm volatile("" : "+v"(t), "+v"(lane));
+    const int wave = t / kWave;
     // tile order = dispatch order (lookback.hpp); DYN_ID / PERSIST: ids from
     // the atomic counter
     if ((DYN_ID || PERSIST) && t == 0)
@@ -467,14 +473,17 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     __shared__ uint32_t s_wsum[kRadix / kWave];
     __shared__ U s_ends[2];
 
-    const int t = threadIdx.x;
-    const int wave = t / kWave;
-    const int lane = lane_id();
+    const int t_id = threadIdx.x;
+    const int lane_ = lane_id();
     const int top_planned = top_single;
     // one bucket (segment) bk; the persistent form calls it in a loop, the
     // plain form once -- a loop around the body in the plain form cost the
     // compiler 19 spilled VGPRs
     auto one = [&](uint32_t bk) {
+    int t = t_id, lane = lane_;
+    // as in k_onesweep: ids re-derived per bucket in the persistent form
+    if constexpr (PERSIST) asm volatile("" : "+v"(t), "+v"(lane));
+    const int wave = t / kWave;
     uint64_t b, mm;
     if constexpr (BOUNDS) {
         b = seg[bk];
