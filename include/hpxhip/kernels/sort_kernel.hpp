@@ -387,6 +387,8 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
 // keys are ordered by a (8 + b2)-bit prefix; every prefix value is a
 // contiguous bucket.
 constexpr int kMaxBuckets = 1 << 17;
+// longest run of equal-prefix keys the segment sort orders by insertion
+constexpr uint32_t kRunMax = 16;
 
 template <typename U, typename X>
 __device__ __forceinline__ uint32_t bucket_of(U k, int s1, int s2, int b2, X xf) {
@@ -429,10 +431,14 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 //      16-bit counters) on the 16 bits under `top`: the keys are then in
 //      order up to runs that agree on all those bits (for 2^30 random keys a
 //      16384-key bucket has runs of 1.1 keys on average, rarely over 5);
-//   2. odd-even transposition of neighbours by whole keys until a round
+//   2. (r03) each run of keys equal on those bits is sorted by insertion by
+//      the thread that finds its first key (one detection sweep); a segment
+//      with a run longer than kRunMax goes on to
+//   3. odd-even transposition of neighbours by whole keys until a round
 //      swaps nothing -- an inversion can only sit inside one run, so the
-//      rounds needed are the longest run's length;
-//   3. a segment whose runs do not settle within OE_MAX rounds (skewed low
+//      rounds needed are the longest run's length (round 2 ran these for
+//      every segment: 2 x (longest run + 1) LDS sweeps);
+//   4. a segment whose runs do not settle within OE_MAX rounds (skewed low
 //      bits) is finished by stable LSD passes over every bit under `top`.
 // Six 8-bit LDS passes for the 48 bits under a 16-bit prefix took 2.4 ms
 // each at 2^30 keys (VALU-bound ranking); this form replaces four of them.
@@ -625,6 +631,54 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
             continue;
         }
         if (lsd || top <= 16 || OE_MAX < 0) break;  // OE_MAX < 0: ablation (two passes only)
+        // Runs of keys equal on the passes' bits (and above) are sorted in
+        // place by the thread that finds the run's start, by insertion
+        // (stable: strictly greater keys move).  One detection sweep and one
+        // sort step replace the odd-even rounds' 2 x (longest run + 1)
+        // sweeps; a run longer than RUN_MAX sends the segment on to the
+        // odd-even rounds below.
+        {
+            const int fs = top - 16;
+            auto pre = [&](const U& x) { return xf(x) >> fs; };
+            uint32_t starts = 0;
+#pragma unroll 3
+            for (int j = 0; j < ITEMS; ++j) {
+                const uint32_t i = static_cast<uint32_t>(t) + static_cast<uint32_t>(j) * THREADS;
+                if (i + 1 < m) {
+                    const U a = pre(s_keys[i]);
+                    if (a == pre(s_keys[i + 1]) && (i == 0 || pre(s_keys[i - 1]) != a)) starts |= 1u << j;
+                }
+            }
+            __syncthreads();  // detection reads done before any run moves
+            int long_run = 0;
+            while (starts) {
+                const int j = __builtin_ctz(starts);
+                starts &= starts - 1;
+                const uint32_t s = static_cast<uint32_t>(t) + static_cast<uint32_t>(j) * THREADS;
+                const U p0 = pre(s_keys[s]);
+                uint32_t e = s + 2;  // the detection saw s + 1 in the run
+                while (e < m && e - s <= kRunMax && pre(s_keys[e]) == p0) ++e;
+                if (e - s > kRunMax) {
+                    long_run = 1;
+                    continue;
+                }
+                for (uint32_t p = s + 1; p < e; ++p) {
+                    const U x = s_keys[p];
+                    uint32_t q = p;
+                    while (q > s && xf(s_keys[q - 1]) > xf(x)) --q;
+                    if (q == p) continue;
+                    VAL y{};
+                    if constexpr (HAS_VAL) y = s_vals[p];
+                    for (uint32_t r = p; r > q; --r) {
+                        s_keys[r] = s_keys[r - 1];
+                        if constexpr (HAS_VAL) s_vals[r] = s_vals[r - 1];
+                    }
+                    s_keys[q] = x;
+                    if constexpr (HAS_VAL) s_vals[q] = y;
+                }
+            }
+            if (!__syncthreads_or(long_run)) break;
+        }
         bool settled = false;
         for (int it = 0; it < OE_MAX && !settled; ++it) {
             int swapped = 0;

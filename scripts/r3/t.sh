@@ -1,4 +1,4 @@
-# round 3, lease t: persistent passes with the per-tile id re-derivation (102-105 VGPRs, was 156) --
+# round 3, lease t: persistent passes with per-tile id re-derivation (102-105 VGPRs, was 156) and the segment sort's run-insertion step --
 # sort tests, then small-range keys (LSD path, persistent grids) vs uniform keys, then kernel stats
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

@@ -120,6 +120,23 @@ def test_buckets_past_the_typical_grid(pol, gpu_target):
     check(pol, gpu_target, low | np.uint64(0xC3 << 56))
 
 
+@pytest.mark.parametrize("choices", [1, 2, 8, 64])
+def test_equal_prefix_runs(pol, gpu_target, choices):
+    """Runs of keys equal on every bit the segment sort's two LDS passes order
+    (k_bucket_sort step 2: each run sorted by insertion by the thread that
+    finds its start; a run over kRunMax = 16 keys goes on to the odd-even
+    rounds, and past OE_MAX rounds to the LSD): bits [20, 47) take one of
+    `choices` values, so the keys sharing a 17-bit prefix split into runs of
+    about 64 / choices keys (2^23 keys) with random low 20 bits."""
+    rng = np.random.default_rng(0x5EED + choices)
+    n = 1 << 23
+    mids = rng.integers(0, 1 << 27, choices, dtype=np.uint64)
+    h = (rng.integers(0, 1 << 17, n, dtype=np.uint64) << np.uint64(47)) \
+        | (mids[rng.integers(0, choices, n)] << np.uint64(20)) | rng.integers(0, 1 << 20, n, dtype=np.uint64)
+    check(pol, gpu_target, h)
+    check(pol, gpu_target, h, True)
+
+
 @pytest.mark.parametrize("bits", [24, 56])
 def test_low_bit_ranges(pol, gpu_target, bits):
     # keys below 2^24 (three live bytes, many duplicates: the prefix is bytes 2
@@ -178,6 +195,19 @@ def check_kv(pol, tgt, k, v, desc=False):
     ek, ev = O.sort_by_key(k, v, desc)
     np.testing.assert_array_equal(gk, ek)
     np.testing.assert_array_equal(gv, ev)
+
+
+def test_sort_by_key_equal_prefix_runs_stable(pol, gpu_target):
+    # the insertion step moves values with their keys and keeps equal keys in
+    # input order: runs of ~8 keys with 4 random low bits (many equal keys)
+    rng = np.random.default_rng(0xAB1E)
+    n = 1 << 22
+    mids = rng.integers(0, 1 << 43, 4, dtype=np.uint64)
+    k = (rng.integers(0, 1 << 17, n, dtype=np.uint64) << np.uint64(47)) \
+        | (mids[rng.integers(0, 4, n)] << np.uint64(4)) | rng.integers(0, 16, n, dtype=np.uint64)
+    v = np.arange(n, dtype=np.uint64)
+    check_kv(pol, gpu_target, k, v)
+    check_kv(pol, gpu_target, k, v, True)
 
 
 @pytest.mark.parametrize("vdt", [np.uint64, np.uint32])
