@@ -21,6 +21,10 @@ kernel, and the HPX-par host baseline (oracle restatement) on a 2^27 sample.
 
 Usage: python bench.py [--gpus N --steps K --warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
+`--gpus N` (N > 1) without torchrun starts the N ranks itself (launch_ranks);
+a WORLD_SIZE that differs from --gpus is an error.  The JSON line carries
+`ranks` (the communicator's size) and `rank_devices` (per rank: device
+ordinal and PCI ids, all-gathered).
 """
 from __future__ import annotations
 
@@ -76,6 +80,64 @@ def pct(gbs):
     return round(100.0 * gbs / HBM_PEAK_GBS, 2)
 
 
+def launch_ranks(argv, n):
+    """`bench.py --gpus N` (N > 1) without a torchrun environment: run the
+    same command as N ranks under torch.distributed.run (one process per
+    GPU, rendezvous on 127.0.0.1) and return its exit code.  This process
+    stays a plain launcher: it never imports the HIP library or torch, so
+    no GPU state exists in it (and nothing is exec'd over a GPU process).
+    Rank 0 prints the one JSON line; a rank that fails or hangs past the
+    collective timeout makes the whole launch exit non-zero."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    rc = subprocess.call(cmd, env=env)
+    with open("/proc/self/maps") as f:
+        if "libhpxhip" in f.read():
+            print("bench.py launcher: the HIP library was loaded in the launcher process", file=sys.stderr)
+            return rc or 3
+    return rc
+
+
+def launch_probe(args):
+    """Hidden launcher check (no GPU): each rank joins a gloo group with the
+    collective timeout and rank 0 prints one JSON line with every rank's
+    RANK / LOCAL_RANK / WORLD_SIZE and pid."""
+    import torch.distributed as dist
+    from datetime import timedelta
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    mine = {k: int(os.environ.get(k, "0")) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    mine["pid"] = os.getpid()
+    mine["hip_library_loaded"] = "libhpxhip" in open("/proc/self/maps").read()
+    ranks = [mine]
+    if world > 1:
+        dist.init_process_group("gloo", timeout=timedelta(seconds=float(
+            os.environ.get("HPXHIP_COLLECTIVE_TIMEOUT_S", "600"))))
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        size = dist.get_world_size()
+        dist.destroy_process_group()
+    else:
+        size = 1
+    if mine["RANK"] == 0:
+        print(json.dumps({"launch_probe": True, "n_gpus": args.gpus, "ranks": size, "rank_env": ranks}), flush=True)
+
+
+def rank_devices(comm, tgt):
+    """[[rank, device ordinal, PCI bus id, PCI device id], ...] of every rank,
+    all-gathered, so the JSON line shows which GPUs the ranks ran on."""
+    p = tgt.properties()
+    mine = np.array([comm.rank, tgt.device, p["pci_bus_id"], p["pci_device_id"]], np.int64)
+    if comm.size == 1:
+        return [mine.tolist()]
+    return np.asarray(comm.allgather_host(mine)).reshape(comm.size, -1).tolist()
+
+
 def main(argv=None, comm_tgt=None):
     """argv: command line (default sys.argv); comm_tgt: an already built
     (communicator, target) pair -- the multi-rank test drives the N > 1 path
@@ -92,9 +154,23 @@ def main(argv=None, comm_tgt=None):
     ap.add_argument("--stencil-steps", type=int, default=100)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--triad-only", action="store_true", help=argparse.SUPPRESS)  # PMC child mode
+    # launcher check without a GPU: the ranks rendezvous over gloo and report
+    # their environment (tests/test_bench_launcher.py)
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
     if args.triad_only:
         return triad_only(args.logn)
+    if comm_tgt is None:
+        env_world = os.environ.get("WORLD_SIZE")
+        if env_world is None and args.gpus > 1:
+            # `bench.py --gpus N` outside torchrun: start the N ranks here,
+            # before anything in this process touches the GPU
+            sys.exit(launch_ranks(sys.argv[1:] if argv is None else list(argv), args.gpus))
+        if env_world is not None and int(env_world) != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}; refusing to report "
+                     f"a {env_world}-rank run as {args.gpus} GPUs")
+    if args.launch_probe:
+        return launch_probe(args)
 
     import hpx_amd as hpx
     from hpx_amd import _lib as L
@@ -102,8 +178,9 @@ def main(argv=None, comm_tgt=None):
 
     comm, tgt = comm_tgt if comm_tgt is not None else S.init_distributed()
     rank, world = comm.rank, comm.size
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if comm_tgt is None and world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the communicator has {world} ranks")
+    devices = rank_devices(comm, tgt)
     stream = tgt.stream
     pol = ex.par.on(hpx.default_executor(tgt))
     # The step runs under par(task), as an HPX program composes asynchronous
@@ -180,6 +257,8 @@ def main(argv=None, comm_tgt=None):
         "value": round(value, 1),
         "unit": "GB/s",
         "n_gpus": world,
+        "ranks": comm.size,
+        "rank_devices": devices,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),

@@ -108,7 +108,8 @@ class target:
         return {"name": p.name.decode(), "arch": p.arch.decode(), "compute_units": p.compute_units,
                 "wave_size": p.wave_size, "total_global_mem": p.total_global_mem,
                 "clock_khz": p.clock_khz, "memory_clock_khz": p.memory_clock_khz,
-                "memory_bus_width": p.memory_bus_width}
+                "memory_bus_width": p.memory_bus_width, "pci_bus_id": p.pci_bus_id,
+                "pci_device_id": p.pci_device_id}
 
     def processing_units_count(self) -> int:
         return self.properties()["compute_units"]

@@ -1088,6 +1088,13 @@ class heat_solver:
 
 
 # ------------------------------------------------------------- comm factory
+def collective_timeout():
+    """Bound on any one collective (HPXHIP_COLLECTIVE_TIMEOUT_S, default 600 s):
+    a rank that never arrives ends the job with an error instead of a hang."""
+    import datetime
+    return datetime.timedelta(seconds=float(os.environ.get("HPXHIP_COLLECTIVE_TIMEOUT_S", "600")))
+
+
 def init_distributed(tgt_from_local_rank: bool = True):
     """torchrun rendezvous (MASTER_ADDR 127.0.0.1), backend "nccl" (RCCL);
     returns (comm, target).  World size 1 without torchrun -> LocalComm."""
@@ -1100,5 +1107,5 @@ def init_distributed(tgt_from_local_rank: bool = True):
     import torch.distributed as dist
     torch.cuda.set_device(tgt.device)
     if not dist.is_initialized():
-        dist.init_process_group("nccl", device_id=torch.device("cuda", tgt.device))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", tgt.device), timeout=collective_timeout())
     return TorchComm(tgt), tgt

@@ -60,6 +60,7 @@ def test_bench_two_ranks_one_json_line(gpu_target):
     lines = [ln for ln in res[0].splitlines() if ln.startswith("{")]
     assert len(lines) == 1 and res[1].strip() == ""
     d = json.loads(lines[0])
+    assert d["ranks"] == 2 and [r[0] for r in d["rank_devices"]] == [0, 1]
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["global_elements"] == 2 * (1 << 22)
     x = d["extras"]
     assert x["segmented_sort_uint64"]["sorted_and_ordered"] is True
