@@ -21,7 +21,7 @@ OFLAGS   := -O2 -fPIC -std=c++17 -ffp-contract=off -Wall -pthread
 .PHONY: all lib oracle clean cxxtests oracle-sanitize
 
 # C++ tests of include/hpx (plain g++ host code linked to the C ABI library)
-CXXT     := compute_api algorithms_known_answer stream_hip for_loop_merge stencil_partitioned call_overhead
+CXXT     := compute_api algorithms_known_answer stream_hip for_loop_merge stencil_partitioned call_overhead exception_list
 CXXTBIN  := $(CXXT:%=tests/cxx/bin/%)
 CXXHDR   := $(shell find include -name '*.hpp') include/hpxhip.h
 TFLAGS   := -O2 -std=c++17 -Wall -Wextra -Wno-unused-parameter -pthread -Iinclude

@@ -55,6 +55,29 @@ class OutOfMemory(HpxHipError, MemoryError):
     """hpx::out_of_memory analogue (hpx/compute/cuda/allocator.hpp:118-124)."""
 
 
+class exception_list(HpxHipError):
+    """hpx::exception_list (hpx/exception_list.hpp:28-97): the error a
+    parallel algorithm reports.  Every failure other than an allocation
+    failure (OutOfMemory, a MemoryError) is wrapped in one
+    (parallel/exception_list.hpp:20-111); iterating yields the original
+    exceptions."""
+
+    def __init__(self, exceptions=()):
+        self.exceptions = list(exceptions)
+        first = self.exceptions[0] if self.exceptions else None
+        self.status = getattr(first, "status", ERROR_INVALID_ARGUMENT)
+        RuntimeError.__init__(self, "; ".join(str(e) for e in self.exceptions) or "hpx::exception_list")
+
+    def __len__(self):
+        return len(self.exceptions)
+
+    def size(self):
+        return len(self.exceptions)
+
+    def __iter__(self):
+        return iter(self.exceptions)
+
+
 class DeviceProps(ctypes.Structure):
     _fields_ = [
         ("name", ctypes.c_char * 256),
@@ -84,6 +107,8 @@ _d = ctypes.c_double
 # name -> argtypes (restype int unless noted)
 SIGNATURES = {
     "hpxhip_abi_version": [],
+    "hpxhip_debug_inject_error": [_i, _i],
+    "hpxhip_debug_raise_device_error": [ctypes.c_void_p, ctypes.c_uint32],
     "hpxhip_device_error": [_i, ctypes.POINTER(ctypes.c_uint32)],
     "hpxhip_get_device_count": [ctypes.POINTER(_i)],
     "hpxhip_set_device": [_i],

@@ -30,6 +30,7 @@ as the source/destination of ``copy`` (a transfer).
 from __future__ import annotations
 
 import ctypes
+import functools
 import threading
 
 import numpy as np
@@ -657,3 +658,51 @@ def _for_loop(pol, first, first_stride, count, *args):
 def for_loop(pol, first, last, *args):
     """for_loop.hpp for_loop(policy, first, last, inductions..., f)."""
     return for_loop_n(pol, first, _check_range(first, last), *args)
+
+
+# ------------------------------------------------------------ error contract
+# dispatch.hpp:122-124,164-168 and parallel/exception_list.hpp:20-111: an
+# algorithm's failure reaches the caller as hpx::exception_list (raised under
+# a synchronous policy, held by the returned future under a task policy),
+# except an allocation failure, which stays std::bad_alloc (OutOfMemory, a
+# MemoryError).  Python's argument errors (TypeError for a functor with no
+# device mapping, ValueError / IndexError for malformed ranges) stand for the
+# reference's compile-time rejections and precondition checks and pass
+# unchanged.
+_ARGUMENT_ERRORS = (TypeError, ValueError, IndexError, ZeroDivisionError)
+
+
+def _algorithm_error(e):
+    if isinstance(e, (MemoryError, L.exception_list) + _ARGUMENT_ERRORS):
+        return e
+    return L.exception_list([e])
+
+
+def _guarded(fn):
+    @functools.wraps(fn)
+    def run(pol, *args, **kw):
+        try:
+            r = fn(pol, *args, **kw)
+        except _ARGUMENT_ERRORS:
+            raise
+        except Exception as e:  # noqa: BLE001 -- rethrown under the contract
+            err = _algorithm_error(e)
+            if getattr(pol, "is_task", False):
+                from .future import make_exceptional_future
+                return make_exceptional_future(err)
+            if err is e:
+                raise
+            raise err from e
+        if isinstance(r, future):
+            r._error_map = _algorithm_error
+        return r
+    return run
+
+
+for _name in ("generate", "fill", "fill_n", "for_each", "for_each_n", "copy", "copy_n", "copy_if", "transform",
+              "reduce", "transform_reduce", "inclusive_scan", "exclusive_scan", "transform_inclusive_scan",
+              "transform_exclusive_scan", "sort", "is_sorted", "sort_by_key", "merge", "for_loop_n", "for_loop",
+              "for_loop_n_strided", "for_loop_strided"):
+    if _name in globals():
+        globals()[_name] = _guarded(globals()[_name])
+del _name

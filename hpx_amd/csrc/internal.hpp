@@ -47,7 +47,21 @@ struct annotate {
     annotate(const annotate&) = delete;
     annotate& operator=(const annotate&) = delete;
 };
-#define HPXHIP_ANNOTATE(name) ::hpxhip::annotate hpxhip_annotate_(name)
+// Fault injection (hpxhip_debug_inject_error): the injected status, taken by
+// the next algorithm entry on this thread.
+extern thread_local int g_inject_status;
+extern thread_local int g_inject_count;
+inline int take_injected_error() {
+    if (__builtin_expect(g_inject_count == 0, 1)) return 0;
+    --g_inject_count;
+    return g_inject_status;
+}
+// Every C-ABI algorithm entry starts with this: its roctx range, then an
+// injected failure if one is pending.
+#define HPXHIP_ANNOTATE(name)                              \
+    ::hpxhip::annotate hpxhip_annotate_(name);             \
+    if (int injected_ = ::hpxhip::take_injected_error())   \
+        return injected_
 
 template <typename T>
 struct tag {

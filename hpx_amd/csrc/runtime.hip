@@ -226,6 +226,28 @@ int hpxhip_device_error(int device, uint32_t* code) {
     return 0;
 }
 
+extern "C++" {
+namespace hpxhip {
+thread_local int g_inject_status = 0;
+thread_local int g_inject_count = 0;
+}  // namespace hpxhip
+}
+
+int hpxhip_debug_inject_error(int status, int count) {
+    if (count < 0 || (count > 0 && status == HPXHIP_SUCCESS)) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hpxhip::g_inject_status = status;
+    hpxhip::g_inject_count = count;
+    return 0;
+}
+
+int hpxhip_debug_raise_device_error(hpxhip_stream stream, uint32_t code) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    uint32_t* w = hpxhip::device_error_word(s);
+    if (!w) return HPXHIP_ERROR_OUT_OF_MEMORY;
+    HPXHIP_CHECK(hipMemsetD32Async(w, code, 1, s));
+    return 0;
+}
+
 // ------------------------------------------------------------- devices
 int hpxhip_get_device_count(int* count) {
     if (!count) return HPXHIP_ERROR_INVALID_ARGUMENT;

@@ -58,6 +58,7 @@ class future:
         self._done = ready
         self._deps = tuple(deps)
         self._lock = threading.Lock()
+        self._error_map = None  # set on an algorithm's future: failures -> exception_list
 
     # -- construction helpers ------------------------------------------
     @classmethod
@@ -110,7 +111,7 @@ class future:
                 if self._thunk is not None:
                     self._value = self._thunk()
             except BaseException as e:  # exceptional future, like set_exception
-                self._exc = e
+                self._exc = self._error_map(e) if self._error_map is not None else e
             self._done = True
             self._thunk = None
 

@@ -17,6 +17,8 @@
 #pragma once
 
 #include <hpxhip.h>
+#include <hpx/exception.hpp>
+#include <hpx/exception_list.hpp>
 
 #include <atomic>
 #include <condition_variable>
@@ -39,20 +41,8 @@
 namespace hpx {
 
 // ------------------------------------------------------------------ errors
-// hpx::exception analogues for the error paths of the reference:
-// kernel_error (detail/launch.hpp:106-113), out_of_memory (allocator.hpp:118-124).
-struct exception : std::runtime_error {
-    int status;
-    exception(int s, std::string const& what) : std::runtime_error(what), status(s) {}
-};
-struct kernel_error : exception {
-    using exception::exception;
-};
-struct out_of_memory : std::bad_alloc {
-    std::string msg;
-    explicit out_of_memory(std::string m) : msg(std::move(m)) {}
-    const char* what() const noexcept override { return msg.c_str(); }
-};
+// hpx::exception, kernel_error, out_of_memory: <hpx/exception.hpp>;
+// hpx::exception_list: <hpx/exception_list.hpp>.
 
 namespace compute { namespace hip { namespace detail {
 inline void check(int status, char const* what) {
@@ -82,6 +72,10 @@ struct shared_state {
     typename std::conditional<std::is_void<T>::value, int, T>::type value{};
     std::vector<std::function<void()>> continuations;
     std::once_flag evaluated;  // value_fn runs once, on the first get()
+    // The future of a parallel algorithm under a task policy: its failure is
+    // reported as the algorithm's error (bad_alloc or hpx::exception_list,
+    // hpx/parallel/exception_list.hpp:81-111), set by parallel::detail::guarded.
+    bool algorithm_result = false;
 
     void set_ready(int status) {
         std::vector<std::function<void()>> conts;
@@ -110,17 +104,20 @@ class future {
     void resolve() {
         st_->wait();
         std::call_once(st_->evaluated, [this] {
-            if (st_->exc || !st_->value_fn) return;
-            try {
-                if constexpr (std::is_void<T>::value) st_->value_fn();
-                else st_->value = st_->value_fn();
-            } catch (...) {
-                st_->exc = std::current_exception();
+            if (!st_->exc && st_->value_fn) {
+                try {
+                    if constexpr (std::is_void<T>::value) st_->value_fn();
+                    else st_->value = st_->value_fn();
+                } catch (...) {
+                    st_->exc = std::current_exception();
+                }
             }
+            if (st_->exc && st_->algorithm_result) st_->exc = hpx::detail::to_algorithm_error(st_->exc);
         });
     }
 
 public:
+    using result_type = T;
     future() = default;
     explicit future(std::shared_ptr<state> s) : st_(std::move(s)) {}
     bool valid() const { return static_cast<bool>(st_); }
@@ -137,6 +134,14 @@ public:
     bool has_exception() {
         resolve();
         return static_cast<bool>(st_->exc);
+    }
+    bool has_value() {
+        resolve();
+        return !st_->exc;
+    }
+    std::exception_ptr get_exception_ptr() {
+        resolve();
+        return st_->exc;
     }
     // hpx::future::then -- runs the continuation on the thread that calls get()
     // on the returned future (deferred), after this future is ready.
@@ -174,6 +179,18 @@ inline future<void> make_ready_future() {
     auto st = std::make_shared<lcos::detail::shared_state<void>>();
     st->set_ready(0);
     return future<void>(st);
+}
+// hpx/lcos/future.hpp make_exceptional_future: a ready future holding e.
+template <typename T>
+future<T> make_exceptional_future(std::exception_ptr e) {
+    auto st = std::make_shared<lcos::detail::shared_state<T>>();
+    st->exc = std::move(e);
+    st->set_ready(0);
+    return future<T>(st);
+}
+template <typename T, typename E>
+future<T> make_exceptional_future(E const& e) {
+    return make_exceptional_future<T>(std::make_exception_ptr(e));
 }
 
 // when_all over a vector of futures (hpx/lcos/when_all.hpp): ready once every
@@ -469,6 +486,15 @@ public:
     // handed them out (a vector moved after begin() was taken).
     static target shared(target const& o) noexcept { return target(o.h_); }
 
+    struct native_handle_type;
+    // A non-owning view of a handle: same device and stream, no reference
+    // count (an aliasing shared_ptr without a control block), so copying it
+    // costs a pointer copy.  Device iterators and value proxies hold one; it
+    // stays valid while a target that owns the handle lives (the container's
+    // allocator), as the reference's target_ptr does (target_ptr.hpp:63-65).
+    static target view(native_handle_type nh);
+    static target view(target const& o) noexcept { return target(std::shared_ptr<handle>(std::shared_ptr<handle>(), o.h_.get())); }
+
     struct native_handle_type {
         handle* h;
         int get_device() const { return h->device; }
@@ -556,6 +582,10 @@ public:
     friend bool operator==(target const& a, target const& b) { return a.h_->device == b.h_->device; }
     friend bool operator!=(target const& a, target const& b) { return !(a == b); }
 };
+inline target target::view(native_handle_type nh) {
+    if (!nh.h) return target(0);  // a default-constructed iterator: device 0
+    return target(std::shared_ptr<handle>(std::shared_ptr<handle>(), nh.h));
+}
 inline std::vector<target> get_local_targets() {
     int n = 0;
     detail::check(hpxhip_get_device_count(&n), "hpxhip_get_device_count");
@@ -625,34 +655,39 @@ public:
 };
 
 // --------------------------------------------------------- device iterator
+// value_proxy.hpp:25-124: element access from the host, one copy each way.
+// Holds a view of the container's target handle (not a pointer into the
+// iterator that made it), so a proxy outlives a temporary iterator.
 template <typename T>
 class value_proxy {
     T* p_;
-    hip::target const* t_;  // the iterator's target view, alive while the proxy is used
+    hip::target t_;  // non-owning view (target::view)
 
 public:
-    value_proxy(T* p, hip::target const* t) : p_(p), t_(t) {}
+    value_proxy(T* p, hip::target t) : p_(p), t_(std::move(t)) {}
     operator T() const {
         T v;
-        detail::check(hpxhip_memcpy_async(&v, p_, sizeof(T), HPXHIP_D2H, t_->stream()), "value_proxy read");
-        t_->synchronize();
+        detail::check(hpxhip_memcpy_async(&v, p_, sizeof(T), HPXHIP_D2H, t_.stream()), "value_proxy read");
+        t_.synchronize();
         return v;
     }
     value_proxy& operator=(T const& v) {
-        detail::check(hpxhip_memcpy_async(p_, &v, sizeof(T), HPXHIP_H2D, t_->stream()), "value_proxy write");
-        t_->synchronize();
+        detail::check(hpxhip_memcpy_async(p_, &v, sizeof(T), HPXHIP_H2D, t_.stream()), "value_proxy write");
+        t_.synchronize();
         return *this;
     }
     friend std::ostream& operator<<(std::ostream& os, value_proxy const& v) { return os << T(v); }
 };
 
-// Holds a view of its container's target handle (target::shared), not a
-// pointer to the container's target object: iterators stay valid when the
-// container is moved, as std::vector's do, and outlive the moved-from object.
+// Holds the container's target handle by raw pointer (a native handle), not
+// a pointer to the container's target object: iterators stay valid when the
+// container is moved, as std::vector's do, while the data lives.  Trivially
+// copyable (a copy is two pointers, no reference count, no new stream), so a
+// device closure may capture one.
 template <typename T>
 class device_iterator {
     T* p_ = nullptr;
-    hip::target t_;  // default: device 0, no stream until one is asked for
+    hip::target::native_handle_type h_{nullptr};  // null: device 0
 
 public:
     using iterator_category = std::random_access_iterator_tag;
@@ -663,12 +698,13 @@ public:
     using target_type = hip::target;
 
     device_iterator() = default;
-    device_iterator(T* p, hip::target const& t) : p_(p), t_(hip::target::shared(t)) {}
+    device_iterator(T* p, hip::target const& t) : p_(p), h_(t.native_handle()) {}
     T* device_ptr() const { return p_; }
-    hip::target const& target() const { return t_; }
+    // a non-owning view of the container's target (same stream)
+    hip::target target() const { return hip::target::view(h_); }
 
-    reference operator*() const { return reference(p_, &t_); }
-    reference operator[](difference_type i) const { return reference(p_ + i, &t_); }
+    reference operator*() const { return reference(p_, target()); }
+    reference operator[](difference_type i) const { return reference(p_ + i, target()); }
     device_iterator& operator++() { ++p_; return *this; }
     device_iterator operator++(int) { auto r = *this; ++p_; return r; }
     device_iterator& operator--() { --p_; return *this; }
@@ -746,7 +782,9 @@ public:
     allocator_type const& get_allocator() const { return alloc_; }
     iterator begin() const { return iterator(data_, alloc_.target()); }
     iterator end() const { return iterator(data_ + size_, alloc_.target()); }
-    hip::value_proxy<T> operator[](size_type i) const { return hip::value_proxy<T>(data_ + i, &alloc_.target()); }
+    hip::value_proxy<T> operator[](size_type i) const {
+        return hip::value_proxy<T>(data_ + i, hip::target::view(alloc_.target()));
+    }
 };
 
 }  // namespace compute

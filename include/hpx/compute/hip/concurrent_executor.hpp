@@ -94,12 +94,29 @@ public:
     }
     // :173-199 with concurrent_executor_parameters (chunk = ceil(n / streams)):
     // the shape is cut into one chunk per stream, each chunk one bulk launch
-    // on its own stream, one future per chunk; nothing waits for the device.
+    // on its own stream; nothing waits for the device.  As in the reference
+    // (one async_execute per element, :171-193) the result holds one future
+    // per shape element: the elements of a chunk share its future.
     template <typename F, typename Shape, typename... Ts>
     std::vector<hpx::future<void>> bulk_async_execute(F&& f, Shape const& shape, Ts&&... ts) const {
+        std::vector<hpx::future<void>> result;
+        for (auto& c : bulk_chunks(f, shape, ts...))
+            for (std::size_t i = 0; i < c.second; ++i) result.push_back(c.first);
+        return result;
+    }
+    template <typename F, typename Shape, typename... Ts>
+    void bulk_sync_execute(F&& f, Shape const& shape, Ts&&... ts) const {
+        for (auto& c : bulk_chunks(f, shape, ts...)) c.first.get();
+    }
+
+private:
+    // (future of the chunk's launch, elements in the chunk) per chunk
+    template <typename F, typename Shape, typename... Ts>
+    std::vector<std::pair<hpx::future<void>, std::size_t>> bulk_chunks(F const& f, Shape const& shape,
+                                                                       Ts const&... ts) const {
         using V = typename std::decay<decltype(*std::begin(shape))>::type;
         std::vector<V> all(std::begin(shape), std::end(shape));
-        std::vector<hpx::future<void>> result;
+        std::vector<std::pair<hpx::future<void>, std::size_t>> chunks;
         const std::size_t k = execs_.size();
         const std::size_t chunk = concurrent_executor_parameters{}.get_chunk_size(*this, f, k, all.size());
         for (std::size_t off = 0; off < all.size(); off += chunk) {
@@ -112,14 +129,12 @@ public:
                 V const* end() const { return e; }
             };
             e.bulk_launch(f, range{all.data() + off, all.data() + off + cnt}, ts...);  // staged before it returns
-            result.push_back(e.target().get_future());
+            chunks.emplace_back(e.target().get_future(), cnt);
         }
-        return result;
+        return chunks;
     }
-    template <typename F, typename Shape, typename... Ts>
-    void bulk_sync_execute(F&& f, Shape const& shape, Ts&&... ts) const {
-        for (auto& fu : bulk_async_execute(std::forward<F>(f), shape, std::forward<Ts>(ts)...)) fu.get();
-    }
+
+public:
     void synchronize() const {
         for (auto const& e : execs_) e.target().synchronize();
     }

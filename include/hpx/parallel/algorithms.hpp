@@ -69,10 +69,12 @@ using policy_t = typename std::decay<P>::type;
 template <typename P>
 constexpr bool is_task = policy_t<P>::is_task;
 
+// The target an algorithm runs on, as a non-owning view (same stream; no
+// copy, which would get a stream of its own).
 template <typename P, typename It>
-hip::target const& target_of(P const& p, It const& it) {
+hip::target target_of(P const& p, It const& it) {
     if constexpr (policy_t<P>::has_executor) {
-        return p.executor().target();
+        return hip::target::view(p.executor().target());
     } else {
         static_assert(is_dev<It>, "raw device pointers need a policy with a HIP executor (par.on(exec))");
         return it.target();
@@ -112,6 +114,41 @@ auto raw_ptr(It it) {
 
 template <typename P, typename R>
 using result_t = typename util::detail::algorithm_result<P, R>::type;
+
+// Error contract of every algorithm (dispatch.hpp:122-124, 164-168;
+// parallel/exception_list.hpp:20-165): a failure other than std::bad_alloc
+// reaches the caller as hpx::exception_list -- thrown under a synchronous
+// policy, stored in the returned future under a task policy (including
+// failures that surface only when the device work completes: the future is
+// flagged so that get() applies the same rule) -- and par_unseq terminates.
+template <typename P>
+constexpr bool is_unseq = std::is_same<policy_t<P>, execution::parallel_unsequenced_policy>::value;
+
+template <typename P, typename Res, typename Body>
+Res guarded(Body&& body) {
+    if constexpr (is_unseq<P>) {
+        try {
+            return body();
+        } catch (...) {
+            std::terminate();
+        }
+    } else if constexpr (is_task<P>) {
+        try {
+            Res f = body();
+            if (f.valid()) f.shared()->algorithm_result = true;
+            return f;
+        } catch (...) {
+            return hpx::make_exceptional_future<typename Res::result_type>(
+                hpx::detail::to_algorithm_error(std::current_exception()));
+        }
+    } else {
+        try {
+            return body();
+        } catch (...) {
+            std::rethrow_exception(hpx::detail::to_algorithm_error(std::current_exception()));
+        }
+    }
+}
 
 // Finish an algorithm whose device work is queued on t's stream.
 template <typename R, typename P, typename Fn>
@@ -212,6 +249,7 @@ auto host_ptr(It it) {
 }
 
 }  // namespace detail
+namespace algo {
 
 // ------------------------------------------------------------- for_each
 // A function object with a traits::unary mapping runs on the library kernel;
@@ -399,6 +437,7 @@ detail::result_t<P, util::tagged_pair<In, Out>> transform(P&& p, In first, In la
     }
 }
 
+}  // namespace algo
 namespace detail {
 template <typename P, typename In1, typename In2, typename Out, typename F>
 result_t<P, util::tagged_tuple<In1, In2, Out>> transform_binary(P&& p, In1 first1, uint64_t n, In2 first2, Out dest,
@@ -438,6 +477,7 @@ result_t<P, util::tagged_tuple<In1, In2, Out>> transform_binary(P&& p, In1 first
     }
 }
 }  // namespace detail
+namespace algo {
 
 template <typename P, typename In1, typename In2, typename Out, typename F,
           typename = typename std::enable_if<detail::is_dev<Out> || detail::is_seg<Out>>::type>
@@ -455,6 +495,7 @@ detail::result_t<P, util::tagged_tuple<In1, In2, Out>> transform(P&& p, In1 firs
 }
 
 // ------------------------------------------------------------ reductions
+}  // namespace algo
 namespace detail {
 // *out_dev <- init (op) conv(x_0) (op) ... over [first, first + n), queued on
 // t's stream (the library kernel for mapped functors, a kernel instantiated
@@ -516,6 +557,7 @@ result_t<P, T> reduce_impl(P&& p, It first, It last, T init, Op&& op, Conv&& con
     }
 }
 }  // namespace detail
+namespace algo {
 
 template <typename P, typename It, typename T, typename Op>
 detail::result_t<P, T> reduce(P&& p, It first, It last, T init, Op&& op) {
@@ -539,6 +581,7 @@ detail::result_t<P, T> transform_reduce(P&& p, It first, It last, T init, Red&& 
                                   std::forward<Conv>(conv));
 }
 
+}  // namespace algo
 namespace detail {
 template <typename T, typename P, typename It1, typename It2, typename Red, typename Comb>
 result_t<P, T> reduce_binary_impl(P&& p, It1 first1, It1 last1, It2 first2, T init, Red&& red, Comb&& comb) {
@@ -566,6 +609,7 @@ result_t<P, T> reduce_binary_impl(P&& p, It1 first1, It1 last1, It2 first2, T in
     return finish_slot<T>(p, t, std::move(slot), load_value<T>{});
 }
 }  // namespace detail
+namespace algo {
 
 // transform_reduce_binary.hpp:323 -- inner product with std::plus / std::multiplies
 template <typename P, typename It1, typename It2, typename T,
@@ -583,6 +627,7 @@ detail::result_t<P, T> transform_reduce(P&& p, It1 first1, It1 last1, It2 first2
 }
 
 // ------------------------------------------------------------------ scans
+}  // namespace algo
 namespace detail {
 template <typename P, typename In, typename Out, typename Op, typename Conv, typename T>
 result_t<P, Out> scan_impl(P&& p, In first, In last, Out dest, Op&& op, Conv&& conv, T init, bool inclusive) {
@@ -603,6 +648,7 @@ result_t<P, Out> scan_impl(P&& p, In first, In last, Out dest, Op&& op, Conv&& c
 }
 using ident = hpx::compute::hip::functional::identity;
 }  // namespace detail
+namespace algo {
 
 // inclusive_scan.hpp:288 (op, init) and :320 (init, op)
 template <typename P, typename In, typename Out, typename A, typename B>
@@ -747,6 +793,7 @@ detail::result_t<P, util::tagged_tuple<In1, In2, Out>> merge(P&& p, In1 first1, 
     return detail::finish<R>(p, t, [last1, last2, end] { return R{last1, last2, end}; });
 }
 
+}  // namespace algo
 // --------------------------------------------------------------- for_loop
 // for_loop_induction.hpp:210-219: an induction over an iterator, value at
 // iteration i = it + stride * i (stride 1 on the device: contiguous kernels).
@@ -1062,6 +1109,7 @@ auto for_loop_dispatch(P&& p, It first, int64_t first_stride, uint64_t n, Tuple&
     return for_loop_body(std::forward<P>(p), vars, st, n, std::get<last>(args));
 }
 }  // namespace detail
+namespace algo {
 
 // for_loop.hpp:808 for_loop_n(policy, first, size, inductions..., body) with
 // a loop_assign body (the C ABI cannot carry arbitrary closures).
@@ -1102,6 +1150,40 @@ detail::result_t<P, void> for_loop_strided(P&& p, It first, It last, S stride, A
     const uint64_t a = static_cast<uint64_t>(st > 0 ? st : -st);
     return for_loop_n_strided(std::forward<P>(p), first, (len + a - 1) / a, stride, std::forward<Args>(args)...);
 }
+
+}  // namespace algo
+// The public algorithms: each forwards to its definition in namespace algo
+// under the error contract above (detail::guarded).
+#define HPXHIP_GUARDED_ALGORITHM(name)                                                                     \
+    template <typename P, typename... A,                                                                    \
+              typename = std::enable_if_t<execution::is_execution_policy<std::decay_t<P>>::value>>          \
+    auto name(P&& p, A&&... a)->decltype(algo::name(std::forward<P>(p), std::forward<A>(a)...)) {           \
+        using R_ = decltype(algo::name(std::forward<P>(p), std::forward<A>(a)...));                         \
+        return detail::guarded<P, R_>([&]() -> R_ { return algo::name(std::forward<P>(p), std::forward<A>(a)...); }); \
+    }
+HPXHIP_GUARDED_ALGORITHM(for_each)
+HPXHIP_GUARDED_ALGORITHM(for_each_n)
+HPXHIP_GUARDED_ALGORITHM(fill)
+HPXHIP_GUARDED_ALGORITHM(fill_n)
+HPXHIP_GUARDED_ALGORITHM(copy)
+HPXHIP_GUARDED_ALGORITHM(copy_n)
+HPXHIP_GUARDED_ALGORITHM(copy_if)
+HPXHIP_GUARDED_ALGORITHM(transform)
+HPXHIP_GUARDED_ALGORITHM(reduce)
+HPXHIP_GUARDED_ALGORITHM(transform_reduce)
+HPXHIP_GUARDED_ALGORITHM(inclusive_scan)
+HPXHIP_GUARDED_ALGORITHM(exclusive_scan)
+HPXHIP_GUARDED_ALGORITHM(transform_inclusive_scan)
+HPXHIP_GUARDED_ALGORITHM(transform_exclusive_scan)
+HPXHIP_GUARDED_ALGORITHM(sort)
+HPXHIP_GUARDED_ALGORITHM(is_sorted)
+HPXHIP_GUARDED_ALGORITHM(sort_by_key)
+HPXHIP_GUARDED_ALGORITHM(merge)
+HPXHIP_GUARDED_ALGORITHM(for_loop_n)
+HPXHIP_GUARDED_ALGORITHM(for_loop)
+HPXHIP_GUARDED_ALGORITHM(for_loop_n_strided)
+HPXHIP_GUARDED_ALGORITHM(for_loop_strided)
+#undef HPXHIP_GUARDED_ALGORITHM
 
 }  // namespace v1
 }}  // namespace hpx::parallel

@@ -157,6 +157,16 @@ const char* hpxhip_error_string(int status);
 /* Reads and clears the device error word of `device` (kernel-side faults
    that must not hang the GPU, e.g. a look-back spin that gave up). */
 int hpxhip_device_error(int device, uint32_t* code);
+/* Fault injection for the error-path tests -- the role HPX's throw_always /
+   throw_bad_alloc test functors play (tests/unit/parallel/algorithms/
+   foreach_tests.hpp:120-205).  hpxhip_debug_inject_error: the next `count`
+   algorithm entry points called on this host thread return `status` without
+   enqueuing anything (count 0 cancels).  hpxhip_debug_raise_device_error:
+   enqueues on `stream` a write of `code` into the device error word, as a
+   kernel that gave up a bounded spin does, so the failure surfaces only when
+   the queued work completes. */
+int hpxhip_debug_inject_error(int status, int count);
+int hpxhip_debug_raise_device_error(hpxhip_stream stream, uint32_t code);
 
 /* ------------------------------------------------ devices (targets) */
 int hpxhip_get_device_count(int* count);

@@ -93,6 +93,7 @@ void f(hpx::compute::vector<int>& a) {
     ("partitioned_vector", []),
     ("stencil_partitioned", []),
     ("call_overhead", []),
+    ("exception_list", []),
 ])
 def test_cxx_program(prog, args):
     exe = os.path.join(BIN, prog)
@@ -102,3 +103,16 @@ def test_cxx_program(prog, args):
     print(r.stdout[-4000:])
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert f"{prog}: all tests passed" in r.stdout
+
+
+def test_par_unseq_error_terminates():
+    """handle_exception_impl<parallel_unsequenced_policy> (parallel/
+    exception_list.hpp:138-158): an algorithm error under par_unseq calls
+    std::terminate.  The failure (a reversed range over an empty vector) is
+    raised before any device call, so this runs without a GPU."""
+    exe = os.path.join(BIN, "exception_list")
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} not built (run `make cxxtests`)")
+    r = subprocess.run([exe, "unseq"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == -6, (r.returncode, r.stdout, r.stderr)
+    assert "returned" not in r.stdout and "negative range" in r.stderr
