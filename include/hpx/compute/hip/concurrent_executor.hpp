@@ -100,7 +100,11 @@ public:
     template <typename F, typename Shape, typename... Ts>
     std::vector<hpx::future<void>> bulk_async_execute(F&& f, Shape const& shape, Ts&&... ts) const {
         std::vector<hpx::future<void>> result;
-        for (auto& c : bulk_chunks(f, shape, ts...))
+        auto chunks = bulk_chunks(f, shape, ts...);
+        std::size_t total = 0;
+        for (auto const& c : chunks) total += c.second;
+        result.reserve(total);
+        for (auto& c : chunks)
             for (std::size_t i = 0; i < c.second; ++i) result.push_back(c.first);
         return result;
     }

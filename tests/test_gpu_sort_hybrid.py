@@ -4,13 +4,18 @@ the top byte and the 9 bits under it (17-bit form) or the two top live bytes
 (16-bit form) --, bucket bounds by lower_bound over buckets of the top byte
 plus b2 bits, b2 chosen from the histograms, one LDS-resident sort per
 bucket (512- or 1024-thread segments); a bucket over its segment's capacity
-sends the whole sort to the LSD over the live digits.  Checked element for
-element against numpy's sort on the distributions that steer it down each
-branch, in both forms (HPXHIP_SORT_HYBRID=17 / 16).  Sizes start at the
-hybrid's 2^22-key threshold.
+sends the whole sort to the LSD over the live digits.  Keys-only buckets of
+the 17-bit form are sorted by k_seg_sort_keys (one atomic counting pass on 12
+bits + insertion of the runs; r04), which hands buckets with long runs or over
+its capacity to k_bucket_sort (two stable LDS passes); HPXHIP_SORT_SEG=stable
+runs k_bucket_sort for every bucket.  Checked element for element against the
+oracle on the distributions that steer it down each branch, in every form
+(HPXHIP_SORT_HYBRID=17 with either segment kernel, and 16).  Sizes start at
+the hybrid's 2^22-key threshold.
 
-Parity: std::sort's order for integer keys (sort.hpp:78-229 via the oracle's
-O.sort, itself numpy's stable sort) and the IEEE total order for doubles."""
+Parity: std::sort's order for integer keys (sort.hpp:78-229, restated by the
+oracle's O.sort as std::sort on the keys' ordered bits, oracle/oracle.cpp) and
+the IEEE total order for doubles (-0.0 before +0.0)."""
 import numpy as np
 import pytest
 
@@ -27,9 +32,10 @@ def pol(gpu_target):
     return ex.par.on(hpx.default_executor(gpu_target))
 
 
-@pytest.fixture(params=["17", "16"], autouse=True)
+@pytest.fixture(params=["17", "17-stable", "16"], autouse=True)
 def form(request, monkeypatch):
-    monkeypatch.setenv("HPXHIP_SORT_HYBRID", request.param)
+    monkeypatch.setenv("HPXHIP_SORT_HYBRID", request.param.split("-")[0])
+    monkeypatch.setenv("HPXHIP_SORT_SEG", "stable" if request.param.endswith("stable") else "atomic")
     return request.param
 
 
@@ -122,17 +128,32 @@ def test_buckets_past_the_typical_grid(pol, gpu_target):
 
 @pytest.mark.parametrize("choices", [1, 2, 8, 64])
 def test_equal_prefix_runs(pol, gpu_target, choices):
-    """Runs of keys equal on every bit the segment sort's two LDS passes order
-    (k_bucket_sort step 2: each run sorted by insertion by the thread that
-    finds its start; a run over kRunMax = 16 keys goes on to the odd-even
-    rounds, and past OE_MAX rounds to the LSD): bits [20, 47) take one of
-    `choices` values, so the keys sharing a 17-bit prefix split into runs of
-    about 64 / choices keys (2^23 keys) with random low 20 bits."""
+    """Runs of keys equal on every bit the segment sort's LDS passes order
+    (k_bucket_sort step 2 / k_seg_sort_keys step 3: each run sorted by
+    insertion by the thread that finds its start; a run over kRunMax = 16 keys
+    goes on to the odd-even rounds, and past OE_MAX rounds to the LSD -- in
+    k_seg_sort_keys, to k_bucket_sort through the relist): bits [20, 47) take
+    one of `choices` values, so the keys sharing a 17-bit prefix split into
+    runs of about 64 / choices keys (2^23 keys) with random low 20 bits."""
     rng = np.random.default_rng(0x5EED + choices)
     n = 1 << 23
     mids = rng.integers(0, 1 << 27, choices, dtype=np.uint64)
     h = (rng.integers(0, 1 << 17, n, dtype=np.uint64) << np.uint64(47)) \
         | (mids[rng.integers(0, choices, n)] << np.uint64(20)) | rng.integers(0, 1 << 20, n, dtype=np.uint64)
+    check(pol, gpu_target, h)
+    check(pol, gpu_target, h, True)
+
+
+def test_bucket_over_the_atomic_segment_capacity(pol, gpu_target):
+    """A bucket the plan accepts (<= 9216 keys) but over k_seg_sort_keys'
+    capacity (512 x 17 = 8704): 4800 extra keys on the prefix (0x12, 0b101)
+    make the plan take b2 = 3 (buckets of ~4096 keys) with that one bucket at
+    ~8900 keys, which goes through the relist to k_bucket_sort."""
+    rng = np.random.default_rng(0xCAB)
+    n = 1 << 23
+    h = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    h[:4800] = (np.uint64(0x12) << np.uint64(56)) | (np.uint64(5) << np.uint64(53)) \
+        | rng.integers(0, 1 << 53, 4800, dtype=np.uint64)
     check(pol, gpu_target, h)
     check(pol, gpu_target, h, True)
 
