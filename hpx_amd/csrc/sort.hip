@@ -44,7 +44,6 @@
 
 #include <algorithm>
 #include <cstdlib>
-#include <string>
 #include <utility>
 #include <vector>
 
@@ -72,7 +71,7 @@ struct tile_shape {
 
 struct sort_layout {
     uint64_t ntiles;
-    size_t alt_keys, alt_vals, hist, xhist, bits, start, xstart, bounds, relist, ctl, counter, lb, lb_bytes, total;
+    size_t alt_keys, alt_vals, hist, xhist, bits, start, xstart, bounds, ctl, counter, lb, lb_bytes, total;
     bool wide;  // 64-bit granules
 };
 
@@ -97,8 +96,6 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     off += kXBins * 8;
     L.bounds = off;  // hybrid: bucket bounds (up to 2^17 + 1)
     off = align_up(off + 8 * (kMaxBuckets + 1), 256);
-    L.relist = off;  // buckets k_seg_sort_keys leaves to k_bucket_sort
-    off = align_up(off + 4 * kMaxBuckets, 256);
     L.ctl = off;  // the device-side plan (ctl words below)
     off += 256;
     L.counter = off;  // counter (16 B) immediately followed by lb: one zero fill per pass
@@ -133,16 +130,6 @@ constexpr uint64_t kCapKV = static_cast<uint64_t>(kSegThreads16) * kSegItemsKV;
 template <typename U>
 constexpr int field17_shift() { return static_cast<int>(8 * sizeof(U)) - 17; }
 constexpr uint64_t kHybridMin = 1ull << 22;
-// keys-only segments of the 17-bit form: one atomic counting pass
-// (k_seg_sort_keys, 512 x 17 keys + 8 KiB of counters, two per CU); the
-// buckets it leaves go to k_bucket_sort.  HPXHIP_SORT_SEG=stable: the two
-// stable LDS passes of k_bucket_sort for every bucket (round 3; A/B).
-constexpr int kSegItemsAtomic = 17;
-
-bool seg_atomic() {
-    const char* e = std::getenv("HPXHIP_SORT_SEG");
-    return !(e && std::string(e) == "stable");
-}
 
 int hybrid_mode() {
     const char* e = std::getenv("HPXHIP_SORT_HYBRID");
@@ -173,7 +160,6 @@ enum : int {
     C_NLSD = 27,       // live digits
     C_DIGITS = 28,     // [28, 36): live digits, least significant first
     C_FIRST = 36,      // the first histogram counted digits [first, passes)
-    C_RELIST = 37,     // buckets k_seg_sort_keys appended to the relist
     C_WORDS = 40
 };
 static_assert(C_WORDS * 4 <= 256, "plan words fit their slot");
@@ -473,20 +459,9 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                                    dim3(cus), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, vc, oversized,
                                    ctl + C_SEGA, g0);
         } else {
-            auto* relist = reinterpret_cast<uint32_t*>(base + L.relist);
-            auto* relist_n = reinterpret_cast<uint32_t*>(ctl + C_RELIST);
-            if (seg_atomic()) {
-                hipLaunchKernelGGL((k_seg_sort_keys<U, X, kSegThreads17, kSegItemsAtomic>), dim3(g0),
-                                   dim3(kSegThreads17), 0, s, kc, bounds, X{}, relist, relist_n, ctl + C_SEGA);
-                HPXHIP_CHECK_LAUNCH();
-                hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true, true, true>),
-                                   dim3(2 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
-                                   ctl + C_SEGA, 0u, relist, relist_n);
-            } else {
-                hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true>),
-                                   dim3(g0), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
-                                   ctl + C_SEGA, 0u);
-            }
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true>),
+                               dim3(g0), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
+                               ctl + C_SEGA, 0u);
             HPXHIP_CHECK_LAUNCH();
             if (g0 < kMaxBuckets)
                 hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true, true>),

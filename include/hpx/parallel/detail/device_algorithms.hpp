@@ -72,6 +72,17 @@ struct dev_op<Op, true> {
     using type = builtin_op_t<Op>;
 };
 
+// the scans' device operator: a built-in kind, or the user operator without
+// an identity (K::noid_op)
+template <typename Op, bool = tr::is_binop<Op>>
+struct scan_op {
+    using type = K::noid_op<std::decay_t<Op>>;
+};
+template <typename Op>
+struct scan_op<Op, true> {
+    using type = builtin_op_t<Op>;
+};
+
 inline hipStream_t stream_of(compute::hip::target const& t) { return reinterpret_cast<hipStream_t>(t.stream()); }
 
 inline void* scratch(compute::hip::target const& t, std::size_t bytes, char const* what) {
@@ -155,8 +166,13 @@ struct scan_conv {
 template <typename V, typename X, typename Cv, typename Op, bool INCL, bool ALIGNED>
 void scan_launch(compute::hip::target const& t, V const* in, V* out, uint64_t n, Cv cv, Op op, X init) {
     namespace S = K::scan_detail;
-    // opt<V> values take twice the registers: 8 rounds (aligned) / 4
-    constexpr int R = std::is_same<X, V>::value ? S::rounds_for<V, ALIGNED>() : (ALIGNED ? 8 : 4);
+    // a user operator scans plain values (noid_op, no identity needed): the
+    // built-in kinds' tile shape, except 14 rounds for aligned 8-byte
+    // integers (the identity-free wave scan's selects: 16 rounds spill 12
+    // VGPRs, 14 fit in 120)
+    constexpr bool noid = K::is_noid_op<Op>::value;
+    constexpr int R = (noid && ALIGNED && sizeof(V) == 8 && std::is_integral<V>::value) ? 14
+                                                                                           : S::rounds_for<V, ALIGNED>();
     constexpr uint64_t tile = S::tile_elems<V, R>();
     const uint64_t ntiles = (n + tile - 1) / tile;
     const std::size_t state = (256 + ntiles * K::tile_state<X>::bytes_per_tile() + 255) / 256 * 256;
@@ -174,18 +190,19 @@ void scan(compute::hip::target const& t, V const* in, V* out, uint64_t n, Op con
           bool inclusive) {
     static_assert(sizeof(V) == 4 || sizeof(V) == 8, "scan (device closure): 4- or 8-byte element types");
     if (n == 0) return;
+    // A user operator has no known identity: round 3 lifted it to opt<V>
+    // (flag + padding per element: 8 rounds instead of 16, 2^30 int64 3.43
+    // vs 2.66 ms, profiles/r04_closure_timing_first.log); the kernel now runs
+    // it on plain values with the identity-free scan (K::noid_op).
     constexpr bool lift = !tr::is_binop<Op>;
-    using X = std::conditional_t<lift, K::opt<V>, V>;
+    using X = V;
     using Cv = scan_conv<V, X, std::decay_t<Conv>>;
-    using OpD = typename dev_op<Op>::type;
+    using OpD = typename scan_op<Op>::type;
     const OpD opd = [&] {
         if constexpr (lift) return OpD{op};
         else return OpD{};
     }();
-    const X iv = [&] {
-        if constexpr (lift) return X{static_cast<V>(init), 1u};
-        else return static_cast<V>(init);
-    }();
+    const X iv = static_cast<V>(init);
     const bool aligned = (reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) % 16 == 0;
     Cv cv{conv};
     if (inclusive) {

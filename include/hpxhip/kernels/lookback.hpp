@@ -219,6 +219,31 @@ struct tile_state {
         if (tile == first && lane == 0) publish(tile, excl, TILE_INCLUSIVE);
         return excl;
     }
+
+    // The same for an operator without identity (noid_op): the cnt >= 1
+    // aggregates are folded by an identity-free wave scan read at lane
+    // cnt - 1 (lanes past cnt hold any value and are not read).
+    template <typename Op>
+    __device__ __forceinline__ T exclusive_prefix_fixed_noid(uint64_t tile, Op op) const {
+        const int lane = lane_id();
+        const uint64_t first = tile / kGroup * kGroup;
+        const uint64_t base = tile == first ? first - kGroup : first;
+        const uint64_t cnt = tile == first ? kGroup : tile - first;
+        uint32_t spins = 0;
+        T a{};
+        bool ok = true;
+        if (static_cast<uint64_t>(lane) < cnt) ok = wait_slot(base + lane, TILE_AGGREGATE, &a, spins);
+        T e{};
+        if (ok) ok = wait_slot(base, TILE_INCLUSIVE, &e, spins);
+        if (!__all(ok)) {
+            if (lane == 0 && err)
+                __hip_atomic_store(err, HPXHIP_DEVERR_LOOKBACK_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return e;
+        }
+        const T excl = op(readlane(e, 0), readlane(wave_inclusive_scan_noid(a, op), static_cast<int>(cnt - 1)));
+        if (tile == first && lane == 0) publish(tile, excl, TILE_INCLUSIVE);
+        return excl;
+    }
 };
 
 }  // namespace hpxhip

@@ -60,8 +60,30 @@ constexpr uint64_t tile_elems() {
 template <typename T, typename Op, int WAVES, bool LOOKBACK, int LBK = 1, bool FIXED = false>
 __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& st, Op op, const T* prefix_dev, T init,
                                             T* s_wave_total) {
-    const T id = Op::template identity<T>();
+    constexpr bool NOID = is_noid_op<Op>::value;
     const int lane = lane_id();
+    if constexpr (NOID) {
+        // lanes >= WAVES pad with any value: they only feed lanes >= WAVES
+        static_assert(FIXED && LOOKBACK, "an operator without identity takes the fixed look-back");
+        const T wt = s_wave_total[lane < WAVES ? lane : 0];
+        const T wi = wave_inclusive_scan_noid(wt, op);
+        const T agg = readlane(wi, WAVES - 1);
+        const T wex = dpp<DPP_WAVE_SHR1>(wi, wi);  // lane 0: nothing before wave 0
+        T p;
+        if (tile == 0) {
+            p = prefix_dev ? *prefix_dev : init;
+            if (lane == 0) {
+                st.publish(0, agg, TILE_AGGREGATE);
+                st.publish(0, p, TILE_INCLUSIVE);  // E(0)
+            }
+        } else {
+            if (lane == 0) st.publish(tile, agg, TILE_AGGREGATE);
+            p = st.exclusive_prefix_fixed_noid(tile, op);
+        }
+        if (lane < WAVES) s_wave_total[lane] = lane == 0 ? p : op(p, wex);
+        return;
+    } else {
+    const T id = Op::template identity<T>();
     const T wt = lane < WAVES ? s_wave_total[lane] : id;
     const T wi = wave_inclusive_scan(wt, op);
     const T agg = readlane(wi, WAVES - 1);
@@ -91,6 +113,7 @@ __device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& 
         }
     }
     if (lane < WAVES) s_wave_total[lane] = op(p, wex);
+    }
 }
 
 // T: element type of in/out; X: the scanned value type (T for the built-in
@@ -118,7 +141,18 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
     const uint64_t tile = DYN_ID ? s_tile : blockIdx.x;
     const int wave = threadIdx.x / kWave;
     const int lane = lane_id();
-    const X id = Op::template identity<X>();
+    // NOID (noid_op, a user operator): no identity -- out-of-range elements
+    // hold X{} (they only feed outputs that are not stored), and the one
+    // position with nothing before it (lane 0's first element of an
+    // exclusive scan: in every round with DEFER, in round 0 without) is
+    // handled by index at the store.
+    constexpr bool NOID = is_noid_op<Op>::value;
+    constexpr bool DEF = DEFER;
+    static_assert(!(NOID && EARLY), "EARLY needs an identity");
+    const X id = [] {
+        if constexpr (NOID) return X{};
+        else return Op::template identity<X>();
+    }();
 
     const uint64_t tile_base = tile * TILE;
     const uint64_t wbase = tile_base + wave * WAVE_ELEMS;
@@ -174,31 +208,65 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
     // Default for double only: int64 measured the same either way (2.68-2.70
     // ms), float at 12 rounds spills 4 VGPRs with it and none without.
     X carry = id;
-    X tr[DEFER ? ROUNDS : 1];
+    X tr[DEF ? ROUNDS : 1];
 #pragma unroll
     for (int r = 0; r < ROUNDS; ++r) {
         X local[V];
-        X run = id;
+        if constexpr (NOID) {
+            // lane-local scan from the first element; x[r][e] becomes the
+            // wave-local value, except (lane 0, e = 0) of an exclusive scan,
+            // which has none (its output is the carry alone)
+            X run = x[r][0];
+            local[0] = x[r][0];
 #pragma unroll
-        for (int e = 0; e < V; ++e) {
-            const X nxt = op(run, x[r][e]);
-            local[e] = INCL ? nxt : run;
-            run = nxt;
-        }
-        const X incl = wave_inclusive_scan(run, op);
-        const X excl = wave_shift_right<X, Op>(incl);
-        if constexpr (DEFER) {
+            for (int e = 1; e < V; ++e) {
+                const X nxt = op(run, x[r][e]);
+                local[e] = INCL ? nxt : run;
+                run = nxt;
+            }
+            const X incl = wave_inclusive_scan_noid(run, op);
+            const X excl = dpp<DPP_WAVE_SHR1>(incl, incl);  // lane 0: nothing before it in the round
+            const X tot = readlane(incl, kWave - 1);
+            if (DEF || r == 0) {
 #pragma unroll
-            for (int e = 0; e < V; ++e) x[r][e] = op(excl, local[e]);
-            tr[r] = readlane(incl, kWave - 1);
+                for (int e = 0; e < V; ++e) {
+                    if (!INCL && e == 0) x[r][e] = excl;  // lane 0: unused (index rule at the store)
+                    else x[r][e] = lane == 0 ? local[e] : op(excl, local[e]);
+                }
+            } else {
+                const X pre = lane == 0 ? carry : op(carry, excl);
+#pragma unroll
+                for (int e = 0; e < V; ++e) x[r][e] = (!INCL && e == 0) ? pre : op(pre, local[e]);
+            }
+            if constexpr (DEF) tr[r] = tot;
+            else carry = r == 0 ? tot : op(carry, tot);
         } else {
-            const X pre = op(carry, excl);
+            X run = id;
 #pragma unroll
-            for (int e = 0; e < V; ++e) x[r][e] = op(pre, local[e]);
-            carry = op(carry, readlane(incl, kWave - 1));
+            for (int e = 0; e < V; ++e) {
+                const X nxt = op(run, x[r][e]);
+                local[e] = INCL ? nxt : run;
+                run = nxt;
+            }
+            const X incl = wave_inclusive_scan(run, op);
+            const X excl = wave_shift_right<X, Op>(incl);
+            if constexpr (DEF) {
+#pragma unroll
+                for (int e = 0; e < V; ++e) x[r][e] = op(excl, local[e]);
+                tr[r] = readlane(incl, kWave - 1);
+            } else {
+                const X pre = op(carry, excl);
+#pragma unroll
+                for (int e = 0; e < V; ++e) x[r][e] = op(pre, local[e]);
+                carry = op(carry, readlane(incl, kWave - 1));
+            }
         }
     }
-    if constexpr (DEFER) {
+    if constexpr (NOID && DEF) {
+        carry = tr[0];
+#pragma unroll
+        for (int r = 1; r < ROUNDS; ++r) carry = op(carry, tr[r]);
+    } else if constexpr (!NOID && DEF) {
 #pragma unroll
         for (int r = 0; r < ROUNDS; ++r) carry = op(carry, tr[r]);
     }
@@ -212,14 +280,22 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
 
     // ---- store (DEFER: round r adds the carry of rounds < r here)
     X rc = pre;
+    // NOID: lane 0's first element of an exclusive scan has nothing before it
+    // in its round -- its output is the carry
+    auto value = [&](const X& c, int r, int e) -> T {
+        if constexpr (NOID && !INCL) {
+            if (e == 0 && lane == 0 && (DEF || r == 0)) return unwrap_value(c);
+        }
+        return unwrap_value(op(c, x[r][e]));
+    };
     if (ALIGNED && full) {
         VT* dst = reinterpret_cast<VT*>(out + wbase);
 #pragma unroll
         for (int r = 0; r < ROUNDS; ++r) {
             VT y;
 #pragma unroll
-            for (int e = 0; e < V; ++e) y.v[e] = unwrap_value(op(DEFER ? rc : pre, x[r][e]));
-            if constexpr (DEFER) rc = op(rc, tr[r]);
+            for (int e = 0; e < V; ++e) y.v[e] = value(DEF ? rc : pre, r, e);
+            if constexpr (DEF) rc = op(rc, tr[r]);
             if constexpr (NT_STORE) st_stream(&dst[r * kWave + lane], y);
             else dst[r * kWave + lane] = y;
         }
@@ -229,9 +305,9 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
 #pragma unroll
             for (int e = 0; e < V; ++e) {
                 const uint64_t i = wbase + (static_cast<uint64_t>(r) * kWave + lane) * V + e;
-                if (i < n) out[i] = unwrap_value(op(DEFER ? rc : pre, x[r][e]));
+                if (i < n) out[i] = value(DEF ? rc : pre, r, e);
             }
-            if constexpr (DEFER) rc = op(rc, tr[r]);
+            if constexpr (DEF) rc = op(rc, tr[r]);
         }
     }
 }

@@ -453,17 +453,13 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 // PERSIST (device-planned sort, BOUNDS only): a fixed grid strides over the
 // planned buckets (bucket b by workgroup b mod gridDim), so a launch the plan
 // skips costs one gate read per workgroup instead of one dispatch per bucket.
-// LIST (with PERSIST): the buckets to sort are list[0, *list_n) -- the ones
-// k_seg_sort_keys left (runs too long for its insertion step).
 template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16, typename VAL = uint32_t,
-          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false, bool LIST = false>
+          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false>
 __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
     void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf,
                        VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr,
-                       const int32_t* __restrict__ ctl = nullptr, uint32_t first_bucket = 0,
-                       const uint32_t* __restrict__ list = nullptr, const uint32_t* __restrict__ list_n = nullptr) {
+                       const int32_t* __restrict__ ctl = nullptr, uint32_t first_bucket = 0) {
     static_assert(!PERSIST || BOUNDS, "the persistent form strides over bucket bounds");
-    static_assert(!LIST || PERSIST, "the list form strides over the list");
     // device-planned sort: ctl = {on, buckets, top_single}; the grid covers
     // the largest bucket count (or strides over it), blocks past the planned
     // count return
@@ -744,13 +740,7 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     };
     // first_bucket: a launch may cover the buckets from there on (a plain
     // launch sized for the typical plan, then a striding one for the rest)
-    if constexpr (LIST) {
-        const uint32_t cnt = *list_n;
-        for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-            one(list[i]);
-            __syncthreads();
-        }
-    } else if constexpr (PERSIST) {
+    if constexpr (PERSIST) {
         for (uint32_t bk = first_bucket + blockIdx.x; bk < nbk; bk += gridDim.x) {
             one(bk);
             __syncthreads();  // s_keys / s_vals read out before the next bucket's passes
@@ -758,233 +748,6 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     } else if (first_bucket + blockIdx.x < nbk) {
         one(first_bucket + blockIdx.x);
     }
-}
-
-// ------------------------------------------------ keys-only segment sort (r04)
-// One workgroup sorts one bucket of a keys-only sort in LDS with ONE counting
-// pass instead of two stable 8-bit passes:
-//   1. every key adds one to the LDS counter of its DBITS-bit digit under
-//      `top` (ds_add_rtn on 16-bit counters packed two per word); the value
-//      the atomic returns is the key's rank among its digit's keys -- in no
-//      particular order, which a keys-only sort does not need: keys equal on
-//      every bit are identical, and the runs below restore the order of keys
-//      that differ under the digit;
-//   2. one exclusive scan of the 2^DBITS counters, the keys scattered to
-//      offset + rank;
-//   3. each run of keys equal on every bit from the digit up (2.1 keys on
-//      average for 8192-key buckets and 12-bit digits) is sorted by
-//      insertion by the thread that owns its first position.
-// The two stable passes ranked every key twice by wave match (8 ballots,
-// ~40 VALU per key per pass) and kept 47 % of the LDS cycles in bank
-// conflicts (profiles/r03_pmc_sort.txt); one atomic add per key replaces both.
-// A bucket over this kernel's LDS capacity, or with a run over kRunMax keys
-// (skewed low bits), is left as it is -- a permutation of its keys -- and
-// its id is appended to `relist`, for k_bucket_sort (LIST form) to sort it
-// completely.  ctl = {on, buckets, top_single} as for k_bucket_sort.
-template <typename U, typename X, int THREADS = 512, int ITEMS = 17, int DBITS = 12>
-__global__ __launch_bounds__(THREADS, 4) void k_seg_sort_keys(U* __restrict__ keys, const uint64_t* __restrict__ seg,
-                                                              X xf, uint32_t* __restrict__ relist,
-                                                              uint32_t* __restrict__ relist_n,
-                                                              const int32_t* __restrict__ ctl) {
-    if (!ctl[0]) return;
-    const uint32_t bk = blockIdx.x;
-    if (bk >= static_cast<uint32_t>(ctl[1])) return;
-    const int top_planned = ctl[2];
-    constexpr int WAVES = THREADS / kWave;
-    constexpr int CHUNK = ITEMS * kWave;
-    constexpr int BITS = static_cast<int>(sizeof(U) * 8);
-    constexpr int NCNT = 1 << DBITS;       // digit counters
-    constexpr int NWORD = NCNT / 2;        // two 16-bit counters per word
-    constexpr int WPT = NWORD / THREADS;   // words per thread in the scan
-    static_assert(NWORD % THREADS == 0 && WPT >= 1 && WPT <= 4, "scan: 1-4 counter words per thread");
-    static_assert(THREADS * ITEMS < 65536, "16-bit counters");
-    __shared__ alignas(16) U s_keys[THREADS * ITEMS];
-    __shared__ alignas(16) uint32_t s_cnt[NWORD];
-    __shared__ uint32_t s_wsum[WAVES];
-    __shared__ U s_ends[2];
-    __shared__ int s_long;
-
-    const int t = threadIdx.x;
-    const int lane = lane_id();
-    const int wave = t / kWave;
-    const uint64_t b = seg[bk];
-    const uint64_t mm = seg[bk + 1] - b;
-    if (mm > static_cast<uint64_t>(THREADS) * ITEMS) {
-        // over this kernel's capacity: k_bucket_sort (LIST) takes it, and
-        // raises *oversized if it is over that kernel's capacity too
-        if (t == 0) {
-            const uint32_t slot = __hip_atomic_fetch_add(relist_n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            relist[slot] = bk;
-        }
-        return;
-    }
-    const uint32_t m = static_cast<uint32_t>(mm);
-    if (m < 2) return;
-
-    const uint32_t wbase = static_cast<uint32_t>(wave) * CHUNK;
-    const uint32_t have = m > wbase ? m - wbase : 0u;
-    const int nfull = static_cast<int>(have >= static_cast<uint32_t>(CHUNK) ? ITEMS : have / kWave);
-    const uint64_t tail_mask = (have % kWave) ? (~0ull >> (kWave - have % kWave)) : 0ull;
-    auto active = [&](int r) -> uint64_t { return r < nfull ? ~0ull : (r == nfull ? tail_mask : 0ull); };
-    U* gkeys = keys + b;
-
-    U k[ITEMS];
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-        const bool on = (active(r) >> lane) & 1u;
-        k[r] = on ? ld_stream(&gkeys[wbase + r * kWave + lane]) : U(0);
-    }
-    if constexpr (WPT == 4) {
-        reinterpret_cast<uint4*>(s_cnt)[t] = make_uint4(0, 0, 0, 0);
-    } else {
-#pragma unroll
-        for (int i = 0; i < WPT; ++i) s_cnt[t * WPT + i] = 0;
-    }
-    if (t == 0) s_long = 0;
-    {
-        const uint32_t last = m - 1;
-        const uint32_t lw = last / CHUNK, lo = last % CHUNK;
-        if (t == 0) s_ends[0] = k[0];
-        if (static_cast<uint32_t>(wave) == lw && static_cast<uint32_t>(lane) == lo % kWave) {
-            U x = k[0];
-#pragma unroll
-            for (int r = 1; r < ITEMS; ++r)
-                if (static_cast<uint32_t>(r) == lo / kWave) x = k[r];
-            s_ends[1] = x;
-        }
-        __syncthreads();
-    }
-    const U diff = xf(s_ends[0]) ^ xf(s_ends[1]);
-    int top = top_planned;
-    if (diff) {
-        const int hb = BITS - (sizeof(U) == 8 ? __builtin_clzll(static_cast<uint64_t>(diff))
-                                               : __builtin_clz(static_cast<uint32_t>(diff)));
-        top = hb > top ? hb : top;
-    }
-    if (top <= 0) return;  // all keys equal: nothing moves
-    const int lo = top > DBITS ? top - DBITS : 0;
-    auto digit = [&](U x) -> uint32_t { return static_cast<uint32_t>(xf(x) >> lo) & (NCNT - 1); };
-
-    // ---- 1. count: the atomic's old value is the key's rank in its digit
-    uint32_t rank2[(ITEMS + 1) / 2];
-#pragma unroll
-    for (int r = 0; r < (ITEMS + 1) / 2; ++r) rank2[r] = 0;
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-        if ((active(r) >> lane) & 1u) {
-            const uint32_t d = digit(k[r]);
-            const uint32_t sh = 16u * (d & 1u);
-            const uint32_t old = atomicAdd(&s_cnt[d >> 1], 1u << sh);
-            rank2[r / 2] |= ((old >> sh) & 0xffffu) << (16 * (r & 1));
-        }
-    }
-    __syncthreads();
-
-    // ---- 2. exclusive scan of the counters (thread t: words [t*WPT, (t+1)*WPT))
-    {
-        uint32_t w[WPT], sum = 0;
-        if constexpr (WPT == 4) {  // one 16-B LDS access per thread
-            const uint4 q = reinterpret_cast<const uint4*>(s_cnt)[t];
-            w[0] = q.x;
-            w[1] = q.y;
-            w[2] = q.z;
-            w[3] = q.w;
-        } else {
-#pragma unroll
-            for (int i = 0; i < WPT; ++i) w[i] = s_cnt[t * WPT + i];
-        }
-#pragma unroll
-        for (int i = 0; i < WPT; ++i) sum += (w[i] & 0xffffu) + (w[i] >> 16);
-        const uint32_t incl = wave_inclusive_scan(sum, op_plus{});
-        if (lane == kWave - 1) s_wsum[wave] = incl;
-        __syncthreads();
-        uint32_t pre = incl - sum;
-#pragma unroll
-        for (int x = 0; x < WAVES; ++x)
-            if (x < wave) pre += s_wsum[x];
-#pragma unroll
-        for (int i = 0; i < WPT; ++i) {
-            const uint32_t c0 = w[i] & 0xffffu, c1 = w[i] >> 16;
-            w[i] = pre | ((pre + c0) << 16);
-            pre += c0 + c1;
-        }
-        if constexpr (WPT == 4) {
-            reinterpret_cast<uint4*>(s_cnt)[t] = make_uint4(w[0], w[1], w[2], w[3]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < WPT; ++i) s_cnt[t * WPT + i] = w[i];
-        }
-    }
-    __syncthreads();
-
-    // ---- scatter to offset + rank
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-        if ((active(r) >> lane) & 1u) {
-            const uint32_t d = digit(k[r]);
-            const uint32_t off = (s_cnt[d >> 1] >> (16u * (d & 1u))) & 0xffffu;
-            s_keys[off + ((rank2[r / 2] >> (16 * (r & 1))) & 0xffffu)] = k[r];
-        }
-    }
-    __syncthreads();
-
-    // ---- 3. runs of keys equal from the digit up: insertion by the thread
-    // owning the run's first position (positions t*ITEMS .. t*ITEMS+ITEMS-1)
-    if (lo > 0) {
-        auto pre = [&](const U& x) { return xf(x) >> lo; };
-        const uint32_t p0 = static_cast<uint32_t>(t) * ITEMS;
-        uint32_t starts = 0;
-        if (p0 + 1 < m) {
-            U prev = p0 ? s_keys[p0 - 1] : U(0);
-            U cur = s_keys[p0];
-#pragma unroll
-            for (int j = 0; j < ITEMS; ++j) {
-                const uint32_t i = p0 + j;
-                if (i + 1 < m) {
-                    const U nxt = s_keys[i + 1];
-                    if (pre(cur) == pre(nxt) && (i == 0 || pre(prev) != pre(cur))) starts |= 1u << j;
-                    prev = cur;
-                    cur = nxt;
-                }
-            }
-        }
-        __syncthreads();  // detection reads done before any run moves
-        int long_run = 0;
-        while (starts) {
-            const int j = __builtin_ctz(starts);
-            starts &= starts - 1;
-            const uint32_t s = p0 + static_cast<uint32_t>(j);
-            const U r0 = pre(s_keys[s]);
-            uint32_t e = s + 2;  // the detection saw s + 1 in the run
-            while (e < m && e - s <= kRunMax && pre(s_keys[e]) == r0) ++e;
-            if (e - s > kRunMax) {
-                long_run = 1;
-                break;
-            }
-            for (uint32_t p = s + 1; p < e; ++p) {
-                const U x = s_keys[p];
-                const U xo = xf(x);
-                uint32_t q = p;
-                while (q > s && xf(s_keys[q - 1]) > xo) {
-                    s_keys[q] = s_keys[q - 1];
-                    --q;
-                }
-                if (q != p) s_keys[q] = x;
-            }
-        }
-        if (long_run) s_long = 1;
-        __syncthreads();
-        if (s_long) {
-            // skewed low bits: the bucket stays as loaded (a permutation of
-            // its keys) and is sorted completely by k_bucket_sort (LIST)
-            if (t == 0) {
-                const uint32_t slot = __hip_atomic_fetch_add(relist_n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                relist[slot] = bk;
-            }
-            return;
-        }
-    }
-    for (uint32_t i = t; i < m; i += THREADS) st_stream(&gkeys[i], s_keys[i]);
 }
 
 }  // namespace sort_detail

@@ -4,14 +4,10 @@ the top byte and the 9 bits under it (17-bit form) or the two top live bytes
 (16-bit form) --, bucket bounds by lower_bound over buckets of the top byte
 plus b2 bits, b2 chosen from the histograms, one LDS-resident sort per
 bucket (512- or 1024-thread segments); a bucket over its segment's capacity
-sends the whole sort to the LSD over the live digits.  Keys-only buckets of
-the 17-bit form are sorted by k_seg_sort_keys (one atomic counting pass on 12
-bits + insertion of the runs; r04), which hands buckets with long runs or over
-its capacity to k_bucket_sort (two stable LDS passes); HPXHIP_SORT_SEG=stable
-runs k_bucket_sort for every bucket.  Checked element for element against the
-oracle on the distributions that steer it down each branch, in every form
-(HPXHIP_SORT_HYBRID=17 with either segment kernel, and 16).  Sizes start at
-the hybrid's 2^22-key threshold.
+sends the whole sort to the LSD over the live digits.  Checked element for
+element against the oracle on the distributions that steer it down each
+branch, in both forms (HPXHIP_SORT_HYBRID=17 / 16).  Sizes start at the
+hybrid's 2^22-key threshold.
 
 Parity: std::sort's order for integer keys (sort.hpp:78-229, restated by the
 oracle's O.sort as std::sort on the keys' ordered bits, oracle/oracle.cpp) and
@@ -32,10 +28,9 @@ def pol(gpu_target):
     return ex.par.on(hpx.default_executor(gpu_target))
 
 
-@pytest.fixture(params=["17", "17-stable", "16"], autouse=True)
+@pytest.fixture(params=["17", "16"], autouse=True)
 def form(request, monkeypatch):
-    monkeypatch.setenv("HPXHIP_SORT_HYBRID", request.param.split("-")[0])
-    monkeypatch.setenv("HPXHIP_SORT_SEG", "stable" if request.param.endswith("stable") else "atomic")
+    monkeypatch.setenv("HPXHIP_SORT_HYBRID", request.param)
     return request.param
 
 
@@ -128,13 +123,12 @@ def test_buckets_past_the_typical_grid(pol, gpu_target):
 
 @pytest.mark.parametrize("choices", [1, 2, 8, 64])
 def test_equal_prefix_runs(pol, gpu_target, choices):
-    """Runs of keys equal on every bit the segment sort's LDS passes order
-    (k_bucket_sort step 2 / k_seg_sort_keys step 3: each run sorted by
-    insertion by the thread that finds its start; a run over kRunMax = 16 keys
-    goes on to the odd-even rounds, and past OE_MAX rounds to the LSD -- in
-    k_seg_sort_keys, to k_bucket_sort through the relist): bits [20, 47) take
-    one of `choices` values, so the keys sharing a 17-bit prefix split into
-    runs of about 64 / choices keys (2^23 keys) with random low 20 bits."""
+    """Runs of keys equal on every bit the segment sort's two LDS passes order
+    (k_bucket_sort step 2: each run sorted by insertion by the thread that
+    finds its start; a run over kRunMax = 16 keys goes on to the odd-even
+    rounds, and past OE_MAX rounds to the LSD): bits [20, 47) take one of
+    `choices` values, so the keys sharing a 17-bit prefix split into runs of
+    about 64 / choices keys (2^23 keys) with random low 20 bits."""
     rng = np.random.default_rng(0x5EED + choices)
     n = 1 << 23
     mids = rng.integers(0, 1 << 27, choices, dtype=np.uint64)
@@ -144,11 +138,10 @@ def test_equal_prefix_runs(pol, gpu_target, choices):
     check(pol, gpu_target, h, True)
 
 
-def test_bucket_over_the_atomic_segment_capacity(pol, gpu_target):
-    """A bucket the plan accepts (<= 9216 keys) but over k_seg_sort_keys'
-    capacity (512 x 17 = 8704): 4800 extra keys on the prefix (0x12, 0b101)
-    make the plan take b2 = 3 (buckets of ~4096 keys) with that one bucket at
-    ~8900 keys, which goes through the relist to k_bucket_sort."""
+def test_bucket_near_the_segment_capacity(pol, gpu_target):
+    """A bucket close to the 512 x 18 = 9216-key segment capacity the plan
+    sizes against: 4800 extra keys on the prefix (0x12, 0b101) make the plan
+    take b2 = 3 (buckets of ~4096 keys) with that one bucket at ~8900 keys."""
     rng = np.random.default_rng(0xCAB)
     n = 1 << 23
     h = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
