@@ -58,6 +58,14 @@ inline kernel_error check_noexcept(int status) {
 
 // ------------------------------------------------------------------ future
 namespace lcos { namespace detail {
+// A completion a waiting get() may run itself (target::async_result): it
+// waits on a HIP event recorded behind the work instead of for the host
+// callback, whose hand-off costs ~30 us (profiles/r03_cxx_call_overhead.log).
+struct early_completion {
+    virtual void wait_and_complete() = 0;
+    virtual ~early_completion() = default;
+};
+
 template <typename T>
 struct shared_state {
     std::mutex mtx;
@@ -76,6 +84,7 @@ struct shared_state {
     // reported as the algorithm's error (bad_alloc or hpx::exception_list,
     // hpx/parallel/exception_list.hpp:81-111), set by parallel::detail::guarded.
     bool algorithm_result = false;
+    std::shared_ptr<early_completion> early;  // set by target::async_result
 
     void set_ready(int status) {
         std::vector<std::function<void()>> conts;
@@ -90,6 +99,11 @@ struct shared_state {
         for (auto& c : conts) c();
     }
     void wait() {
+        {
+            std::lock_guard<std::mutex> lk(mtx);
+            if (ready) return;
+        }
+        if (early) early->wait_and_complete();
         std::unique_lock<std::mutex> lk(mtx);
         cv.wait(lk, [&] { return ready; });
     }
@@ -316,6 +330,25 @@ public:
         host_free_[b.cls].push_back(b.idx);
     }
 
+    // HIP events for the early completion of futures (target::async_result)
+    hpxhip_event take_event() {
+        {
+            std::lock_guard<std::mutex> lk(mtx_);
+            if (!events_.empty()) {
+                hpxhip_event e = events_.back();
+                events_.pop_back();
+                return e;
+            }
+        }
+        hpxhip_event e = nullptr;
+        if (hpxhip_event_create(&e) != HPXHIP_SUCCESS) return nullptr;
+        return e;
+    }
+    void give_event(hpxhip_event e) {
+        std::lock_guard<std::mutex> lk(mtx_);
+        events_.push_back(e);
+    }
+
     hpxhip_stream take_stream() {
         {
             std::lock_guard<std::mutex> lk(mtx_);
@@ -364,6 +397,7 @@ private:
     std::vector<std::pair<void*, void*>> chunks_;  // (device, pinned host) per chunk
     std::vector<unsigned> free_;
     std::vector<hpxhip_stream> streams_;
+    std::vector<hpxhip_event> events_;
     std::vector<void*> blocks_, host_blocks_;
     std::vector<unsigned> block_free_[64], host_free_[64];
 };
@@ -451,12 +485,44 @@ class target {
     };
     std::shared_ptr<handle> h_;
 
+    // Completion of an async_result future: run once, by the stream callback
+    // or -- earlier -- by a get() that waited on the event recorded behind the
+    // work.  The callback returns the slot to the pool; the event goes back
+    // when the future's state lets go of this object.
     template <typename S>
-    struct completion {
-        std::shared_ptr<S> st;
+    struct completion final : lcos::detail::early_completion {
+        S* st = nullptr;  // kept alive by the future and by the callback's reference
         detail::device_pool* pool = nullptr;
         detail::device_pool::slot_ref slot{};
         std::function<void(unsigned char const*)> on_ready;
+        hpxhip_event ev = nullptr;
+        int device = 0;
+        std::mutex m;
+        bool done = false, released = false;
+
+        void complete(int status) {
+            bool first = false;
+            {
+                std::lock_guard<std::mutex> lk(m);
+                if (!done) {
+                    done = first = true;
+                    if (pool && !released) std::memcpy(st->raw, slot.host, sizeof(st->raw));
+                    if (status == 0 && on_ready) on_ready(st->raw);
+                }
+            }
+            if (first) st->set_ready(status);
+        }
+        void wait_and_complete() override {
+            if (ev && hpxhip_event_synchronize(ev) == HPXHIP_SUCCESS) complete(0);
+        }
+        void release_slot() {
+            std::lock_guard<std::mutex> lk(m);
+            if (pool && !released) pool->release(slot.id);
+            released = true;
+        }
+        ~completion() override {
+            if (ev) detail::device_pool::get(device).give_event(ev);
+        }
     };
 
     explicit target(std::shared_ptr<handle> h) noexcept : h_(std::move(h)) {}
@@ -526,13 +592,17 @@ public:
         return async_result<void>([](unsigned char const*) {});
     }
 
-    // A future completed from a stream callback once all work queued so far
-    // is done.  With a result slot, the callback copies the slot's bytes into
-    // the shared state and releases the slot; then on_ready(bytes) runs (still
-    // on the callback thread, no HIP calls: e.g. a for_loop reduction folding
-    // its view into the live-out variable, for_loop_reduction.hpp:60-66) and
-    // the state becomes ready.  value(bytes) runs on the first get(), after
-    // the device error word is checked.
+    // A future completed once all work queued so far is done -- by a stream
+    // callback, or by a get() that waits first: get() waits on a HIP event
+    // recorded behind the work and completes the state itself (r04: the
+    // callback's hand-off had cost ~30 us per par(task) + get(),
+    // profiles/r03_cxx_call_overhead.log).  Completion copies the result
+    // slot's bytes into the shared state, then on_ready(bytes) runs (no HIP
+    // calls: it may run on the callback thread; e.g. a for_loop reduction
+    // folding its view into the live-out variable, for_loop_reduction.hpp:
+    // 60-66) and the state becomes ready.  value(bytes) runs on the first
+    // get(), after the device error word is checked.  The slot returns to
+    // its pool from the callback, which always runs.
     template <typename R>
     future<R> async_result(std::function<R(unsigned char const*)> value, result_slot slot = {},
                            std::function<void(unsigned char const*)> on_ready = {}) const {
@@ -547,30 +617,40 @@ public:
             return value(self->raw);
         };
         hpxhip_stream s = stream();
-        auto* c = new completion<S>{st, nullptr, {}, std::move(on_ready)};
+        auto c = std::make_shared<completion<S>>();
+        c->st = st.get();
+        c->on_ready = std::move(on_ready);
+        c->device = dev;
         if (slot) {
             auto d = slot.detach();
             c->pool = d.first;
             c->slot = d.second;
         }
+        c->ev = detail::device_pool::get(dev).take_event();
+        if (c->ev && hpxhip_event_record(c->ev, s) != HPXHIP_SUCCESS) {
+            detail::device_pool::get(dev).give_event(c->ev);
+            c->ev = nullptr;  // no early path: the callback completes it
+        }
+        struct box {
+            std::shared_ptr<S> st;
+            std::shared_ptr<completion<S>> c;
+        };
+        auto* b = new box{st, c};
         int rc = hpxhip_stream_add_callback(
             s,
             [](void* p, int status) {
-                auto* cp = static_cast<completion<S>*>(p);
-                if (cp->pool) {
-                    std::memcpy(cp->st->raw, cp->slot.host, sizeof(cp->st->raw));
-                    cp->pool->release(cp->slot.id);
-                }
-                if (status == 0 && cp->on_ready) cp->on_ready(cp->st->raw);
-                cp->st->set_ready(status);
-                delete cp;
+                auto* bp = static_cast<box*>(p);
+                bp->c->complete(status);
+                bp->c->release_slot();
+                delete bp;
             },
-            c);
+            b);
         if (rc != HPXHIP_SUCCESS) {
-            if (c->pool) c->pool->release(c->slot.id);
-            delete c;
+            c->release_slot();
+            delete b;
             detail::check(rc, "hpxhip_stream_add_callback");
         }
+        st->early = c;
         return future<R>(st);
     }
 
