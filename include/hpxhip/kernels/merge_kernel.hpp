@@ -138,8 +138,10 @@ __global__ __launch_bounds__(kThreads) void k_merge(const T* __restrict__ a, uin
     const uint64_t total = na + nb;
     const uint64_t d0 = t * kTile;
     const uint64_t d1 = d0 + kTile < total ? d0 + kTile : total;
-    const uint64_t a0 = splits[t], a1 = splits[t + 1];
-    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
+    // clamped as in k_pass_merge: consistent splits pass unchanged
+    const uint64_t a1 = min(splits[t + 1], min(na, d1));
+    const uint64_t a0 = min(splits[t], min(a1, d0));
+    const uint64_t b0 = min(d0 - a0, nb), b1 = max(b0, min(d1 - a1, nb));
     const int la = static_cast<int>(a1 - a0), lb = static_cast<int>(b1 - b0);
     const int len = la + lb;
     stage<T, VEC>(a, a0, a1, s);
@@ -253,9 +255,12 @@ __global__ __launch_bounds__(kThreads) void k_pass_merge(const T* __restrict__ s
     const uint64_t nb = n - p0 - na < w ? n - p0 - na : w;
     const uint64_t dl0 = d0 - p0;                                   // diagonal in the pair
     const uint64_t dl1 = dl0 + kTile < na + nb ? dl0 + kTile : na + nb;
-    const uint64_t a0 = splits[t];
-    const uint64_t a1 = dl1 == na + nb ? na : splits[t + 1];  // tile t + 1 is in the same pair
-    const uint64_t b0 = dl0 - a0, b1 = dl1 - a1;
+    // splits come from k_pass_partition over the same data; the clamps keep
+    // every access inside the run pair even if the data changed in between
+    // (a caller racing the sort: garbage order, but no stray access)
+    const uint64_t a1 = min(dl1 == na + nb ? na : splits[t + 1], min(na, dl1));  // tile t + 1 is in the same pair
+    const uint64_t a0 = min(splits[t], min(a1, dl0));
+    const uint64_t b0 = min(dl0 - a0, nb), b1 = max(b0, min(dl1 - a1, nb));
     const int la = static_cast<int>(a1 - a0), lb = static_cast<int>(b1 - b0);
     const int len = la + lb;
     const T* a = src + p0;

@@ -352,8 +352,10 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             if (full || i < n) {
                 const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
                 const uint64_t dst = s_adj[d] + s_whist[wave][d] + rank[r];
-                kout[dst] = k[r];
-                if constexpr (HAS_VAL) vout[dst] = v[r];
+                if (dst < n) {  // see the write-out below
+                    kout[dst] = k[r];
+                    if constexpr (HAS_VAL) vout[dst] = v[r];
+                }
             }
         }
         return false;
@@ -368,8 +370,15 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             const U key = s_keys[i];
             const uint32_t d = static_cast<uint32_t>(xf(key) >> shift) & DMASK;
             const uint64_t dst = s_adj[d] + i;
-            kout[dst] = key;
-            if constexpr (HAS_VAL) vout[dst] = s_vals[i];
+            // Destinations come from the histogram taken before the pass: they
+            // stay below n unless the keys were changed during the sort (a
+            // caller racing the sort on another stream).  Then the result is
+            // garbage, but no store leaves the output buffer (it would
+            // overwrite the plan words in the scratch that follows it).
+            if (dst < n) {
+                kout[dst] = key;
+                if constexpr (HAS_VAL) vout[dst] = s_vals[i];
+            }
         }
     }
     return true;

@@ -12,7 +12,7 @@
 //   sort              2^28 u64: radix sort (std::less) vs a lambda comparator
 //                     (merge sort), sort.hpp:364
 //
-// Device time per call from HIP events on the executor's stream, best of 5
+// Device time per call from HIP events on the policy's stream, best of 5
 // after one warm-up; GB/s on the algorithmic bytes (8 B/elem reduce, 16 B/elem
 // scan, 12 B/elem copy_if at 50 %).  Each result is also checked against the
 // kind path's.  usage: closure_timing [logn=30] [reduce|sort|all]
@@ -77,7 +77,10 @@ void reductions(hip::default_executor& exec, std::size_t n, char const* tn) {
     else
         hip::detail::check(hpxhip_generate(hip::dtype_of<T>::value, HPXHIP_GEN_UNIT, 0x5eed, 0, 0, d.data(), n,
                                            exec.target().stream()), "generate");
-    timer tm(exec.target().stream());
+    // the policy holds a copy of exec, whose target has a stream of its own
+    // (cuda_target.cpp:203-211): time on that stream, after the generate
+    exec.target().synchronize();
+    timer tm(pol.executor().target().stream());
     T kind_v{}, l1{}, l2{};
     double kind = tm.best_ms([&] { kind_v = hpx::parallel::transform_reduce(pol, d.begin(), d.end(), T(0), std::plus<T>(), fn::identity{}); });
     double conv = tm.best_ms([&] {
@@ -126,10 +129,12 @@ void reductions(hip::default_executor& exec, std::size_t n, char const* tn) {
 void sorts(hip::default_executor& exec, std::size_t n) {
     auto pol = ex::par.on(exec);
     dvec<uint64_t> d(n, hip::allocator<uint64_t>(exec.target()));
-    timer tm(exec.target().stream());
+    // keys generated and sorted on the policy's stream (a copy of exec has a
+    // stream of its own: generating on exec's would race the sort)
+    const hpxhip_stream ps = pol.executor().target().stream();
+    timer tm(ps);
     auto regen = [&] {
-        hip::detail::check(hpxhip_generate(HPXHIP_U64, HPXHIP_GEN_BITS, 0xabc, 0, 0, d.data(), n, exec.target().stream()),
-                           "generate");
+        hip::detail::check(hpxhip_generate(HPXHIP_U64, HPXHIP_GEN_BITS, 0xabc, 0, 0, d.data(), n, ps), "generate");
     };
     double gen = tm.best_ms(regen);
     double radix = tm.best_ms([&] {
