@@ -1,0 +1,11 @@
+# round 4, lease d: comparator-sort timing (race fixed), C++ call overhead (event get), full suite, smoke, bench
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 300 tests/cxx/bin/closure_timing 30 sort > gpurun_out/r4d_closure_sort.log 2>&1 || exit $?
+timeout -k 10 300 tests/cxx/bin/call_overhead > gpurun_out/r4d_call_overhead.log 2>&1 || exit $?
+timeout -k 10 1200 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/r4d_tests.log 2>&1
+rc=$?; echo "suite rc=$rc" >> gpurun_out/r4d_status.log
+if [ $rc -gt 1 ]; then exit $rc; fi
+timeout -k 10 200 python -u __graft_entry__.py smoke > gpurun_out/r4d_smoke.log 2>&1 || exit $?
+timeout -k 10 500 python -u bench.py > gpurun_out/r4d_bench.log 2>&1 || exit $?
+echo "bench ok" >> gpurun_out/r4d_status.log
