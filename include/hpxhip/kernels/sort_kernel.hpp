@@ -24,6 +24,15 @@ __device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 
 // into both halves of the peer mask with one v_bitop3 each (acc & ~(m ^ x),
 // truth table 0x90): 4 VALU per bit where the select/xor/and form took 9
 // (scripts/ubench/bucket.hip; the ranking is the VALU-bound part of a pass).
+// r04: the ballot is the compiler's (__builtin_amdgcn_ballot_w64), not an
+// inline-asm v_cmp: the asm form wrote every bit's mask into one SGPR pair,
+// so each ballot waited on the previous bit's bitop3 reads (and an s_nop for
+// the VALU-writes-SGPR hazard); the builtin lets the compiler give each
+// ballot its own SGPRs and interleave the ranks of neighbouring keys.
+// HPXHIP_MATCH_ASM=1 builds the round-3 form (A/B).
+#ifndef HPXHIP_MATCH_ASM
+#define HPXHIP_MATCH_ASM 0
+#endif
 template <int BITS = 8>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
     uint32_t lo = static_cast<uint32_t>(active), hi = static_cast<uint32_t>(active >> 32);
@@ -31,7 +40,11 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
     for (int b = 0; b < BITS; ++b) {
         const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(d), b, 1));
         uint64_t m;
+#if HPXHIP_MATCH_ASM
         asm("v_cmp_ne_u32_e64 %0, 0, %1" : "=s"(m) : "v"(x));
+#else
+        m = __builtin_amdgcn_ballot_w64(x != 0);
+#endif
         lo = __builtin_amdgcn_bitop3_b32(lo, static_cast<uint32_t>(m), x, 0x90);
         hi = __builtin_amdgcn_bitop3_b32(hi, static_cast<uint32_t>(m >> 32), x, 0x90);
     }
