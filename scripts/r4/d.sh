@@ -20,3 +20,4 @@ if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 200 python -u __graft_entry__.py smoke > gpurun_out/r4d_smoke.log 2>&1 || exit $?
 timeout -k 10 500 python -u bench.py > gpurun_out/r4d_bench.log 2>&1 || exit $?
 echo "bench ok" >> gpurun_out/r4d_status.log
+for c in u64corr u64hot; do SORT_ONLY=$c timeout -k 10 300 python -u scripts/sort_probe.py 28 >> gpurun_out/r4d_cliff.log 2>&1 || exit $?; done

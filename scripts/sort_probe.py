@@ -2,7 +2,12 @@
 keys at 2^20..2^30, device time from HIP events (best of 3, generation
 subtracted), host time of the call itself, and an is_sorted + checksum
 check of every result.  usage: python scripts/sort_probe.py [maxlog]
-(SORT_ONLY=u64|u32|pairs|u64r16|u64r24: that case at 2^maxlog only)."""
+(SORT_ONLY=u64|u32|pairs|u64r16|u64r24|u64corr|u64hot: that case at 2^maxlog
+only; u64corr: the 9-bit field under the top byte is a function of the top
+byte -- uniform marginal histograms, 256 populated buckets of n/256 keys, so
+every bucket is oversized and the plan falls back to the full LSD after the
+prefix passes; u64hot: uniform keys plus one prefix holding
+n/64 extra keys -- one oversized bucket sends the whole sort to the LSD)."""
 import ctypes
 import os
 import sys
@@ -36,7 +41,23 @@ def ms(a, b):
     return f.value
 
 
-def run(dt, logn, kv=False, reps=3, key_range=None):
+def correlate(k, n, hot=False):
+    """u64corr: bits [47, 56) := bits [56, 64) << 1 (a function of the top
+    byte); u64hot: keys [0, n/64) moved onto one 17-bit prefix."""
+    from hpx_amd import functional as F  # noqa: F401
+    import numpy as np_
+    h = k.to_host()
+    if hot:
+        m = n // 64
+        h[:m] = (np_.uint64(0x1234B) << np_.uint64(47)) | (h[:m] & np_.uint64((1 << 47) - 1))
+    else:
+        top = h >> np_.uint64(56)
+        h = (h & ~np_.uint64(0x1FF << 47)) | ((top << np_.uint64(48)) & np_.uint64(0x1FF << 47))
+    L.call("hpxhip_memcpy_async", ctypes.c_void_p(k.data()), h.ctypes.data_as(ctypes.c_void_p), 8 * n, L.H2D, S)
+    t.synchronize()
+
+
+def run(dt, logn, kv=False, reps=3, key_range=None, shape=None):
     n = 1 << logn
     k = hpx.vector(n, dtype=dt, tgt=t)
     v = hpx.vector(n, dtype=np.uint64, tgt=t) if kv else None
@@ -46,6 +67,8 @@ def run(dt, logn, kv=False, reps=3, key_range=None):
             P.generate(pol, k.begin(), k.end(), "range", 7 + r, 0, key_range - 1)
         else:
             P.generate(pol, k.begin(), k.end(), "bits", 7 + r)
+        if shape:
+            correlate(k, n, hot=shape == "hot")
         if kv:
             P.generate(pol, v.begin(), v.end(), "iota", 0, 0, 0)
         t.synchronize()
@@ -77,8 +100,10 @@ if only:
     # u64r16 / u64r24: keys below 2^16 / 2^24 (two / three live digits)
     dt, kv, kr = {"u64": (np.uint64, False, None), "u32": (np.uint32, False, None),
                   "pairs": (np.uint64, True, None), "u64r16": (np.uint64, False, 1 << 16),
-                  "u64r24": (np.uint64, False, 1 << 24)}[only]
-    d, h, ok = run(dt, maxlog, kv, reps=2, key_range=kr)
+                  "u64r24": (np.uint64, False, 1 << 24), "u64corr": (np.uint64, False, None),
+                  "u64hot": (np.uint64, False, None)}[only]
+    shape = {"u64corr": "corr", "u64hot": "hot"}.get(only)
+    d, h, ok = run(dt, maxlog, kv, reps=2, key_range=kr, shape=shape)
     print(f"{only + ' 2^' + str(maxlog):28s} {d:9.3f} {(1 << maxlog) / d / 1e6:8.2f} {h:8.3f} {ok}", flush=True)
     sys.exit(0)
 for logn in range(20, maxlog + 1, 2):
