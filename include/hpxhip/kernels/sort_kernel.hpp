@@ -24,14 +24,15 @@ __device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 
 // into both halves of the peer mask with one v_bitop3 each (acc & ~(m ^ x),
 // truth table 0x90): 4 VALU per bit where the select/xor/and form took 9
 // (scripts/ubench/bucket.hip; the ranking is the VALU-bound part of a pass).
-// r04: the ballot is the compiler's (__builtin_amdgcn_ballot_w64), not an
-// inline-asm v_cmp: the asm form wrote every bit's mask into one SGPR pair,
-// so each ballot waited on the previous bit's bitop3 reads (and an s_nop for
-// the VALU-writes-SGPR hazard); the builtin lets the compiler give each
-// ballot its own SGPRs and interleave the ranks of neighbouring keys.
-// HPXHIP_MATCH_ASM=1 builds the round-3 form (A/B).
+// The ballot stays an inline-asm v_cmp into one SGPR pair.  r04 A/B
+// (profiles/r04_sort_ab_ballot.log): the compiler's ballot
+// (__builtin_amdgcn_ballot_w64) gives every bit its own SGPRs and interleaves
+// neighbouring keys, but the full sort got slower (2^30 u64 18.9-19.0 vs
+// 18.3-18.5 ms, u32 14.1 vs 13.5): the extra SGPR pairs spill into VGPR
+// lanes in the segment sort and lengthen the onesweep passes.
+// HPXHIP_MATCH_ASM=0 builds the builtin form.
 #ifndef HPXHIP_MATCH_ASM
-#define HPXHIP_MATCH_ASM 0
+#define HPXHIP_MATCH_ASM 1
 #endif
 template <int BITS = 8>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
