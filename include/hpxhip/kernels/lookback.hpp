@@ -40,6 +40,10 @@
 
 #include <hpxhip/kernels/common.hpp>
 
+#ifndef HPXHIP_LB_GROUP_K
+#define HPXHIP_LB_GROUP_K 1
+#endif
+
 namespace hpxhip {
 
 enum : uint32_t { TILE_INVALID = 0, TILE_AGGREGATE = 1, TILE_INCLUSIVE = 2 };
@@ -168,7 +172,55 @@ struct tile_state {
     // waits are on lower tile ids only (dispatch-order forward progress, as
     // above) and bounded.  Tile 0 publishes its aggregate and E(0) = the
     // scan's initial prefix.
-    static constexpr uint64_t kGroup = kWave;
+    // Group = 64 x kGroupK tiles: lane l folds the aggregates of tiles
+    // base + l*kGroupK .. base + l*kGroupK + kGroupK - 1 (in order), the
+    // wave reduction then folds the lanes in order.  The E(first) hand-offs
+    // form a chain, one link per group; kGroupK > 1 shortens it (A/B knob
+    // HPXHIP_LB_GROUP_K).
+    static constexpr int kGroupK = HPXHIP_LB_GROUP_K;
+    static constexpr uint64_t kGroup = static_cast<uint64_t>(kWave) * kGroupK;
+
+    // Loads the aggregates [base + lane*K, ...) < base + cnt of this lane,
+    // all in flight together, re-polling the unpublished ones; v[j] valid for
+    // lane*K + j < cnt.  False on timeout.
+    __device__ __forceinline__ bool wait_aggregates(uint64_t base, uint64_t cnt, T (&v)[kGroupK],
+                                                    uint32_t& spins) const {
+        const uint64_t l0 = static_cast<uint64_t>(lane_id()) * kGroupK;
+        bool pending[kGroupK];
+#pragma unroll
+        for (int j = 0; j < kGroupK; ++j) pending[j] = l0 + j < cnt;
+        while (true) {
+            uint64_t a[kGroupK][G];
+#pragma unroll
+            for (int j = 0; j < kGroupK; ++j)
+                if (pending[j]) {
+                    const uint64_t* p = slots + (base + l0 + j) * 2 * G;
+#pragma unroll
+                    for (int g = 0; g < G; ++g) a[j][g] = __hip_atomic_load(&p[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < kGroupK; ++j)
+                if (pending[j]) {
+                    bool ok = true;
+                    uint32_t w[G];
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        ok = ok && static_cast<uint32_t>(a[j][g] >> 32) == TILE_AGGREGATE;
+                        w[g] = static_cast<uint32_t>(a[j][g]);
+                    }
+                    if (ok) {
+                        v[j] = from_words<T>(w);
+                        pending[j] = false;
+                    } else {
+                        any = true;
+                    }
+                }
+            if (!any) return true;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kSpinLimit) return false;
+        }
+    }
 
     // Lane-uniform; waits until slot (j, status) is published.
     __device__ __forceinline__ bool wait_slot(uint64_t j, uint32_t status, T* v, uint32_t& spins) const {
@@ -200,14 +252,22 @@ struct tile_state {
         const T id = Op::template identity<T>();
         const int lane = lane_id();
         const uint64_t first = tile / kGroup * kGroup;
-        // the aggregates to fold: the previous group's 64 (a group's first
+        // the aggregates to fold: the previous group's (a group's first
         // tile) or this group's tiles before this one
         const uint64_t base = tile == first ? first - kGroup : first;
         const uint64_t cnt = tile == first ? kGroup : tile - first;
         uint32_t spins = 0;
         T a = id;
         bool ok = true;
-        if (static_cast<uint64_t>(lane) < cnt) ok = wait_slot(base + lane, TILE_AGGREGATE, &a, spins);
+        if constexpr (kGroupK == 1) {
+            if (static_cast<uint64_t>(lane) < cnt) ok = wait_slot(base + lane, TILE_AGGREGATE, &a, spins);
+        } else {
+            T v[kGroupK];
+            ok = wait_aggregates(base, cnt, v, spins);
+#pragma unroll
+            for (int j = 0; j < kGroupK; ++j)
+                if (static_cast<uint64_t>(lane) * kGroupK + j < cnt) a = op(a, v[j]);
+        }
         T e = id;
         if (ok) ok = wait_slot(base, TILE_INCLUSIVE, &e, spins);  // E(base): base is a group's first tile
         if (!__all(ok)) {
@@ -232,7 +292,16 @@ struct tile_state {
         uint32_t spins = 0;
         T a{};
         bool ok = true;
-        if (static_cast<uint64_t>(lane) < cnt) ok = wait_slot(base + lane, TILE_AGGREGATE, &a, spins);
+        if constexpr (kGroupK == 1) {
+            if (static_cast<uint64_t>(lane) < cnt) ok = wait_slot(base + lane, TILE_AGGREGATE, &a, spins);
+        } else {
+            T v[kGroupK];
+            ok = wait_aggregates(base, cnt, v, spins);
+            a = v[0];  // lanes with no aggregate hold any value: not read
+#pragma unroll
+            for (int j = 1; j < kGroupK; ++j)
+                if (static_cast<uint64_t>(lane) * kGroupK + j < cnt) a = op(a, v[j]);
+        }
         T e{};
         if (ok) ok = wait_slot(base, TILE_INCLUSIVE, &e, spins);
         if (!__all(ok)) {
@@ -240,7 +309,8 @@ struct tile_state {
                 __hip_atomic_store(err, HPXHIP_DEVERR_LOOKBACK_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return e;
         }
-        const T excl = op(readlane(e, 0), readlane(wave_inclusive_scan_noid(a, op), static_cast<int>(cnt - 1)));
+        const T excl = op(readlane(e, 0), readlane(wave_inclusive_scan_noid(a, op),
+                                                   static_cast<int>((cnt - 1) / kGroupK)));
         if (tile == first && lane == 0) publish(tile, excl, TILE_INCLUSIVE);
         return excl;
     }
