@@ -40,8 +40,8 @@
 
 #include <hpxhip/kernels/common.hpp>
 
-#ifndef HPXHIP_LB_GROUP_K
-#define HPXHIP_LB_GROUP_K 1
+#ifndef HPXHIP_LB_GROUP
+#define HPXHIP_LB_GROUP 64
 #endif
 
 namespace hpxhip {
@@ -172,13 +172,18 @@ struct tile_state {
     // waits are on lower tile ids only (dispatch-order forward progress, as
     // above) and bounded.  Tile 0 publishes its aggregate and E(0) = the
     // scan's initial prefix.
-    // Group = 64 x kGroupK tiles: lane l folds the aggregates of tiles
-    // base + l*kGroupK .. base + l*kGroupK + kGroupK - 1 (in order), the
-    // wave reduction then folds the lanes in order.  The E(first) hand-offs
-    // form a chain, one link per group; kGroupK > 1 shortens it (A/B knob
-    // HPXHIP_LB_GROUP_K).
-    static constexpr int kGroupK = HPXHIP_LB_GROUP_K;
-    static constexpr uint64_t kGroup = static_cast<uint64_t>(kWave) * kGroupK;
+    // Group = kGroup tiles (HPXHIP_LB_GROUP, an A/B knob): lane l folds the
+    // aggregates of tiles base + l*kGroupK .. base + l*kGroupK + kGroupK - 1
+    // (in order; kGroupK = 1 up to 64 tiles), the wave reduction then folds
+    // the lanes in order.  The E(first) hand-offs form a chain, one link per
+    // group; a tile waits for up to kGroup - 1 aggregates.  r04 A/B at 2^30
+    // (profiles/r04_ab_lookback_group.log): 256 tiles (4 per lane) 2.89 vs
+    // 2.59 ms int64 scan, 2.87 vs 2.18 copy_if -- the per-tile fold, not the
+    // chain, is what the group size trades.
+    static constexpr uint64_t kGroup = HPXHIP_LB_GROUP;
+    static constexpr int kGroupK = kGroup > static_cast<uint64_t>(kWave) ? static_cast<int>(kGroup / kWave) : 1;
+    static_assert(kGroup % kGroupK == 0 && (kGroup <= static_cast<uint64_t>(kWave) || kGroup % kWave == 0),
+                  "group: up to 64 tiles, or a multiple of 64");
 
     // Loads the aggregates [base + lane*K, ...) < base + cnt of this lane,
     // all in flight together, re-polling the unpublished ones; v[j] valid for
