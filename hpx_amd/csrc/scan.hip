@@ -67,7 +67,7 @@ int launch_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init, const
     static_assert(tile_elems<T, R, TH>() >= tile_elems<T, 8>(), "scratch is sized for 1024 x 8-round tiles");
     const uint64_t ntiles = ntiles_for<T, R, TH>(n);
     HPXHIP_CHECK(hipMemsetAsync(ws, 0, align_up(kSlotsOff + ntiles * tile_state<T>::bytes_per_tile(), 256), s));
-    tile_state<T> st{reinterpret_cast<uint64_t*>(ws + kSlotsOff), device_error_word(s)};
+    scan_detail::scan_state<T> st{reinterpret_cast<uint64_t*>(ws + kSlotsOff), device_error_word(s)};
     hipLaunchKernelGGL((k_scan<T, Conv, Op, INCL, ALIGNED, R, TH, true, TH == kThreads ? 1 : 4>),
                        dim3(static_cast<unsigned>(ntiles)), dim3(TH), 0, s, in, out, n, conv, op, init, prefix_dev,
                        reinterpret_cast<uint32_t*>(ws), st);

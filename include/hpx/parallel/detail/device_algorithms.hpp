@@ -178,7 +178,7 @@ void scan_launch(compute::hip::target const& t, V const* in, V* out, uint64_t n,
     const std::size_t state = (256 + ntiles * K::tile_state<X>::bytes_per_tile() + 255) / 256 * 256;
     char* ws = static_cast<char*>(scratch(t, state, "scan scratch"));
     compute::hip::detail::check(hpxhip_memset_async(ws, 0, state, t.stream()), "scan scratch");
-    K::tile_state<X> st{reinterpret_cast<uint64_t*>(ws + 256), error_word(t)};
+    K::scan_detail::scan_state<X> st{reinterpret_cast<uint64_t*>(ws + 256), error_word(t)};
     hipLaunchKernelGGL((S::k_scan<V, Cv, Op, INCL, ALIGNED, R, S::kThreads, true, 1, false, 1, false, true, X>),
                        dim3(static_cast<unsigned>(ntiles)), dim3(S::kThreads), 0, stream_of(t), in, out, n, cv, op,
                        init, static_cast<X const*>(nullptr), reinterpret_cast<uint32_t*>(ws), st);

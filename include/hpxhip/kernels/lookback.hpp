@@ -48,7 +48,8 @@ namespace hpxhip {
 
 enum : uint32_t { TILE_INVALID = 0, TILE_AGGREGATE = 1, TILE_INCLUSIVE = 2 };
 
-template <typename T>
+// GROUP: tiles per group of the fixed-association look-back (below).
+template <typename T, int GROUP = HPXHIP_LB_GROUP>
 struct tile_state {
     static constexpr int G = sizeof(T) / 4;  // granules per value (1 or 2; up to 8 for opt<T> values)
     static_assert(sizeof(T) % 4 == 0 && sizeof(T) <= 32, "tile values of whole 32-bit words");
@@ -172,7 +173,7 @@ struct tile_state {
     // waits are on lower tile ids only (dispatch-order forward progress, as
     // above) and bounded.  Tile 0 publishes its aggregate and E(0) = the
     // scan's initial prefix.
-    // Group = kGroup tiles (HPXHIP_LB_GROUP, an A/B knob): lane l folds the
+    // Group = kGroup tiles (GROUP; HPXHIP_LB_GROUP sets the default): lane l folds the
     // aggregates of tiles base + l*kGroupK .. base + l*kGroupK + kGroupK - 1
     // (in order; kGroupK = 1 up to 64 tiles), the wave reduction then folds
     // the lanes in order.  The E(first) hand-offs form a chain, one link per
@@ -180,7 +181,7 @@ struct tile_state {
     // (profiles/r04_ab_lookback_group.log): 256 tiles (4 per lane) 2.89 vs
     // 2.59 ms int64 scan, 2.87 vs 2.18 copy_if -- the per-tile fold, not the
     // chain, is what the group size trades.
-    static constexpr uint64_t kGroup = HPXHIP_LB_GROUP;
+    static constexpr uint64_t kGroup = GROUP;
     static constexpr int kGroupK = kGroup > static_cast<uint64_t>(kWave) ? static_cast<int>(kGroup / kWave) : 1;
     static_assert(kGroup % kGroupK == 0 && (kGroup <= static_cast<uint64_t>(kWave) || kGroup % kWave == 0),
                   "group: up to 64 tiles, or a multiple of 64");

@@ -28,6 +28,18 @@ namespace scan_detail {
 constexpr int kThreads = 1024;
 constexpr int kRounds = 16;
 
+// Tiles per group of the fixed-association look-back (lookback.hpp).  A
+// tile folds up to GROUP - 1 published aggregates, and the groups' first
+// tiles form a chain of hand-offs: r04 at 2^30 int64 / f64 (16384-element
+// tiles, profiles/r04_ab_lookback_group.log): 64 tiles 2.62 ms, 32 tiles
+// 2.55, 16 tiles 3.2 (the chain binds).
+#ifndef HPXHIP_SCAN_LB_GROUP
+#define HPXHIP_SCAN_LB_GROUP 32
+#endif
+constexpr int kScanGroup = HPXHIP_SCAN_LB_GROUP;
+template <typename X>
+using scan_state = tile_state<X, kScanGroup>;
+
 // Rounds per launch variant: 16 for aligned integer and double scans (r03:
 // double had spilled at 16 and ran 12 rounds -- 2.83 ms for 2^30 f64 --
 // until the deferred round carry (DEFER below) cut its temporaries: 121
@@ -57,8 +69,8 @@ constexpr uint64_t tile_elems() {
 // profiles/r03_ubench_scan7_fixed.log): every tile reads 64 aggregates
 // published right after their loads plus one group word, instead of walking
 // a variable window and publishing an inclusive value of its own.
-template <typename T, typename Op, int WAVES, bool LOOKBACK, int LBK = 1, bool FIXED = false>
-__device__ __forceinline__ void tile_prefix(uint64_t tile, const tile_state<T>& st, Op op, const T* prefix_dev, T init,
+template <typename T, typename Op, int WAVES, bool LOOKBACK, int LBK = 1, bool FIXED = false, typename ST>
+__device__ __forceinline__ void tile_prefix(uint64_t tile, const ST& st, Op op, const T* prefix_dev, T init,
                                             T* s_wave_total) {
     constexpr bool NOID = is_noid_op<Op>::value;
     const int lane = lane_id();
@@ -123,7 +135,7 @@ template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED, int R
           int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false, int LBK = 1,
           bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = true, typename X = T, bool DEFER = std::is_floating_point_v<X> && sizeof(X) == 8, bool FIXED = true>
 __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, X init,
-                                                   const X* prefix_dev, uint32_t* counter, tile_state<X> st) {
+                                                   const X* prefix_dev, uint32_t* counter, scan_state<X> st) {
     constexpr int V = 16 / sizeof(T);
     constexpr int WAVES = THREADS / kWave;
     constexpr uint64_t TILE = tile_elems<T, ROUNDS, THREADS>();
