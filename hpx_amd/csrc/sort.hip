@@ -61,17 +61,11 @@ constexpr int kHistBlocksPerCU = 4;  // 4 lane copies x 8 KiB per pass histogram
 // each digit's thread loads 4 predecessors per step (4.88 ms/pass vs 5.00 at
 // 8 and 5.48 at 16; rocPRIM's radix_sort_keys takes 50.2 ms for the whole
 // 2^30 u64 sort on the same GPU, the plain LSD here 40 ms, the hybrid 21 ms).
-// HPXHIP_SORT_LBFIX = G > 0: the onesweep passes take the fixed-group
-// look-back (groups of G tiles, k_onesweep LBFIX) instead of the walk.
-#ifndef HPXHIP_SORT_LBFIX
-#define HPXHIP_SORT_LBFIX 0
-#endif
 template <bool HAS_VAL>
 struct tile_shape {
     static constexpr int threads = HAS_VAL ? 256 : 512;
     static constexpr int items = 16;
     static constexpr int lbb = 4;
-    static constexpr int lbfix = HPXHIP_SORT_LBFIX;
     static constexpr int tile = threads * items;
 };
 
@@ -107,8 +101,7 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     L.counter = off;  // counter (16 B) immediately followed by lb: one zero fill per pass
     off += 256;
     L.lb = off;
-    // room for a 9-bit pass, and the group prefixes of the fixed-group look-back
-    L.lb_bytes = (L.ntiles + L.ntiles / 16 + 1) * kXBins * (L.wide ? 8 : 4);
+    L.lb_bytes = L.ntiles * kXBins * (L.wide ? 8 : 4);  // room for a 9-bit pass
     off = align_up(off + L.lb_bytes, 256);
     L.total = off;
     return L;
@@ -368,8 +361,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     auto pass = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, int rb, const int32_t* word,
                     bool persist) -> int {
         const uint64_t nt = L.ntiles;
-        const uint64_t ngr = TS::lbfix > 0 ? nt / TS::lbfix + 1 : 0;  // group prefixes (LBFIX)
-        const uint64_t zbytes = align_up(256 + (nt + ngr) * (uint64_t(1) << rb) * (L.wide ? 8 : 4), 16);
+        const uint64_t zbytes = align_up(256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), 16);
         hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
                            reinterpret_cast<uint4*>(counter), zbytes / 16, word);
         HPXHIP_CHECK_LAUNCH();
@@ -386,14 +378,13 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             constexpr bool DYN = sizeof(U) == 8;
             if (persist)
                 hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB, true, true,
-                                               true, TS::lbfix>),
+                                               true>),
                                    grid, block, 0, s, kin, kout, vin, vout, n, 0, RB == 9 ? xstart : start,
                                    reinterpret_cast<G*>(base + L.lb), counter, err, X{}, word, nt);
             else
-                hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB, true, DYN,
-                                               false, TS::lbfix>),
+                hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB, true, DYN>),
                                    grid, block, 0, s, kin, kout, vin, vout, n, 0, RB == 9 ? xstart : start,
-                                   reinterpret_cast<G*>(base + L.lb), counter, err, X{}, word, nt);
+                                   reinterpret_cast<G*>(base + L.lb), counter, err, X{}, word);
         };
         using R8 = std::integral_constant<int, 8>;
         using R9 = std::integral_constant<int, 9>;

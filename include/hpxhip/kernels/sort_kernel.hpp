@@ -182,8 +182,7 @@ __global__ __launch_bounds__(R) void k_bin_offsets(const unsigned long long* __r
 // gate and left (~0.1 ms each, ~0.9 ms per sort over the skipped second-byte
 // and LSD passes); a persistent grid leaves after one read per workgroup.
 template <typename U, typename VAL, bool HAS_VAL, typename G, typename X, int THREADS = 512, int ITEMS = 16,
-          int LBB = 8, int RB = 8, bool STAGE = true, bool DYN_ID = HPXHIP_TILE_DYN_ID, bool PERSIST = false,
-          int LBFIX = 0>
+          int LBB = 8, int RB = 8, bool STAGE = true, bool DYN_ID = HPXHIP_TILE_DYN_ID, bool PERSIST = false>
 __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin, U* __restrict__ kout,
                                                        const VAL* __restrict__ vin, VAL* __restrict__ vout,
                                                        uint64_t n, int shift,
@@ -281,8 +280,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             tile_count += c;
         }
         // publish this tile's aggregate for digit t as early as possible
-        // (LBFIX: tile 0's too -- its group's tiles fold it)
-        if ((tile != 0 || LBFIX > 0) && (LBB > 0 || LBFIX > 0))
+        if (tile != 0 && LBB > 0)
             __hip_atomic_store(&my[t], enc_agg<G>(tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         count_incl = wave_inclusive_scan(tile_count, op_plus{});
         if (lane == kWave - 1) s_wsum[wave] = count_incl;
@@ -319,55 +317,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     // ---- per-digit look-back across tiles (thread t < R owns digit t)
     if (t < R) {
         uint64_t excl = 0;
-        if constexpr (LBFIX > 0) {
-            // Fixed groups of LBFIX tiles (lookback.hpp's scheme, per digit):
-            // E(first), the digit's count in the tiles before a group's first
-            // tile, is published by that tile in eg; tile t folds E(first) and
-            // the aggregates of first .. t - 1 -- all loads in flight at once,
-            // one round trip instead of a walk of several steps.
-            G* eg = lb + ntiles * R;
-            const uint64_t first = tile / LBFIX * LBFIX;
-            if (tile == 0) {
-                __hip_atomic_store(&eg[t], enc_incl<G>(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                const uint64_t base = tile == first ? first - LBFIX : first;
-                const uint32_t cnt = static_cast<uint32_t>(tile == first ? LBFIX : tile - first);
-                G g[LBFIX];
-                G e = __hip_atomic_load(&eg[(base / LBFIX) * R + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-                for (int j = 0; j < LBFIX; ++j)
-                    g[j] = static_cast<uint32_t>(j) < cnt
-                               ? __hip_atomic_load(&lb[(base + j) * R + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : enc_agg<G>(0);
-                uint32_t spins = 0;
-                while (true) {
-                    bool ok = e != 0;
-#pragma unroll
-                    for (int j = 0; j < LBFIX; ++j) ok = ok && g[j] != 0;
-                    if (ok) break;
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > kSpinLimit) {
-                        if (err)
-                            __hip_atomic_store(err, HPXHIP_DEVERR_LOOKBACK_TIMEOUT, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    if (e == 0)
-                        e = __hip_atomic_load(&eg[(base / LBFIX) * R + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-                    for (int j = 0; j < LBFIX; ++j)
-                        if (g[j] == 0)
-                            g[j] = __hip_atomic_load(&lb[(base + j) * R + t], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                }
-                excl = static_cast<uint64_t>(e >> 1);
-#pragma unroll
-                for (int j = 0; j < LBFIX; ++j) excl += static_cast<uint64_t>(g[j] >> 1) - 1;
-                if (tile == first)
-                    __hip_atomic_store(&eg[(first / LBFIX) * R + t], enc_incl<G>(excl), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
-        } else if (tile == 0) {
+        if (tile == 0) {
             if (LBB > 0) __hip_atomic_store(&my[t], enc_incl<G>(tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if constexpr (LBB > 0) {
             int64_t pred = static_cast<int64_t>(tile) - 1;
