@@ -61,8 +61,13 @@ namespace lcos { namespace detail {
 // A completion a waiting get() may run itself (target::async_result): it
 // waits on a HIP event recorded behind the work instead of for the host
 // callback, whose hand-off costs ~30 us (profiles/r03_cxx_call_overhead.log).
+// r04: the host callback is registered only when something must be told
+// without asking (a continuation, when_all); get() and is_ready() use the
+// event directly.
 struct early_completion {
     virtual void wait_and_complete() = 0;
+    virtual bool try_complete() = 0;                          // non-blocking
+    virtual void arm(std::shared_ptr<void> keep_state) = 0;  // ensure a completion callback
     virtual ~early_completion() = default;
 };
 
@@ -136,6 +141,11 @@ public:
     explicit future(std::shared_ptr<state> s) : st_(std::move(s)) {}
     bool valid() const { return static_cast<bool>(st_); }
     bool is_ready() const {
+        {
+            std::lock_guard<std::mutex> lk(st_->mtx);
+            if (st_->ready) return true;
+        }
+        if (st_->early) st_->early->try_complete();
         std::lock_guard<std::mutex> lk(st_->mtx);
         return st_->ready;
     }
@@ -171,6 +181,11 @@ public:
             std::unique_lock<std::mutex> lk(parent->mtx);
             if (!parent->ready) {
                 parent->continuations.push_back([raw] { raw->set_ready(0); });
+                lk.unlock();
+                if (parent->early) {
+                    parent->early->arm(parent);
+                    nst->early = parent->early;  // a get() on the continuation may complete the parent itself
+                }
                 return future<R>(nst);
             }
         }
@@ -228,6 +243,8 @@ future<std::vector<future<T>>> when_all(std::vector<future<T>>&& fs) {
             count_down();
         } else {
             in->continuations.push_back(count_down);
+            lk.unlock();
+            if (in->early) in->early->arm(in);
         }
     }
     count_down();
@@ -267,6 +284,7 @@ public:
 
     slot_ref acquire() {
         std::lock_guard<std::mutex> lk(mtx_);
+        if (free_.empty()) reap();
         if (free_.empty()) grow();
         unsigned id = free_.back();
         free_.pop_back();
@@ -278,6 +296,20 @@ public:
     void release(unsigned id) {
         std::lock_guard<std::mutex> lk(mtx_);
         free_.push_back(id);
+    }
+    // The device's callback stream: a completion armed after its work was
+    // queued waits there on its event (the stream that queued the work may
+    // have gone back to the pool, or been destroyed, by then).
+    hpxhip_stream callback_stream() {
+        std::lock_guard<std::mutex> lk(mtx_);
+        if (!cb_stream_) check(hpxhip_stream_create(device_, &cb_stream_), "hpxhip_stream_create");
+        return cb_stream_;
+    }
+    // A slot whose future was dropped before its work completed: freed (and
+    // its event returned) once the event shows the work done.
+    void defer_release(unsigned id, hpxhip_event ev) {
+        std::lock_guard<std::mutex> lk(mtx_);
+        deferred_.emplace_back(id, ev);
     }
 
     // Device blocks of 2^cls bytes (cls >= 8) for the small per-call arrays of
@@ -378,6 +410,18 @@ public:
 
 private:
     explicit device_pool(int device) : device_(device) {}
+    void reap() {  // called with mtx_ held
+        for (std::size_t i = 0; i < deferred_.size();) {
+            if (hpxhip_event_query(deferred_[i].second) == HPXHIP_SUCCESS) {
+                free_.push_back(deferred_[i].first);
+                events_.push_back(deferred_[i].second);
+                deferred_[i] = deferred_.back();
+                deferred_.pop_back();
+            } else {
+                ++i;
+            }
+        }
+    }
     void grow() {  // called with mtx_ held
         void* d = nullptr;
         void* h = nullptr;
@@ -398,6 +442,8 @@ private:
     std::vector<unsigned> free_;
     std::vector<hpxhip_stream> streams_;
     std::vector<hpxhip_event> events_;
+    std::vector<std::pair<unsigned, hpxhip_event>> deferred_;
+    hpxhip_stream cb_stream_ = nullptr;
     std::vector<void*> blocks_, host_blocks_;
     std::vector<unsigned> block_free_[64], host_free_[64];
 };
@@ -485,20 +531,24 @@ class target {
     };
     std::shared_ptr<handle> h_;
 
-    // Completion of an async_result future: run once, by the stream callback
-    // or -- earlier -- by a get() that waited on the event recorded behind the
-    // work.  The callback returns the slot to the pool; the event goes back
-    // when the future's state lets go of this object.
+    // Completion of an async_result future, run once: by a get() that
+    // waited on the event recorded behind the work, by is_ready() finding
+    // the event complete, or by the stream callback -- registered only when
+    // a continuation needs it (arm).  Completion copies the result slot's
+    // bytes into the state and returns the slot to its pool (the work is
+    // done by then); a future dropped before completion hands its slot and
+    // event to the pool, which frees them once the event has fired.
     template <typename S>
-    struct completion final : lcos::detail::early_completion {
-        S* st = nullptr;  // kept alive by the future and by the callback's reference
+    struct completion final : lcos::detail::early_completion, std::enable_shared_from_this<completion<S>> {
+        S* st = nullptr;  // kept alive by the future, and by an armed callback's reference
         detail::device_pool* pool = nullptr;
         detail::device_pool::slot_ref slot{};
         std::function<void(unsigned char const*)> on_ready;
         hpxhip_event ev = nullptr;
+        hpxhip_stream stream = nullptr;
         int device = 0;
         std::mutex m;
-        bool done = false, released = false;
+        bool done = false, armed = false;
 
         void complete(int status) {
             bool first = false;
@@ -506,21 +556,77 @@ class target {
                 std::lock_guard<std::mutex> lk(m);
                 if (!done) {
                     done = first = true;
-                    if (pool && !released) std::memcpy(st->raw, slot.host, sizeof(st->raw));
+                    if (pool) {
+                        std::memcpy(st->raw, slot.host, sizeof(st->raw));
+                        pool->release(slot.id);
+                        pool = nullptr;
+                    }
                     if (status == 0 && on_ready) on_ready(st->raw);
                 }
             }
             if (first) st->set_ready(status);
         }
         void wait_and_complete() override {
+            {
+                std::lock_guard<std::mutex> lk(m);
+                if (done) return;
+            }
             if (ev && hpxhip_event_synchronize(ev) == HPXHIP_SUCCESS) complete(0);
+            else arm(nullptr);  // no event: the callback completes it
         }
-        void release_slot() {
-            std::lock_guard<std::mutex> lk(m);
-            if (pool && !released) pool->release(slot.id);
-            released = true;
+        bool try_complete() override {
+            {
+                std::lock_guard<std::mutex> lk(m);
+                if (done) return true;
+            }
+            if (ev && hpxhip_event_query(ev) == HPXHIP_SUCCESS) {
+                complete(0);
+                return true;
+            }
+            return false;
+        }
+        void arm(std::shared_ptr<void> keep) override {
+            {
+                std::lock_guard<std::mutex> lk(m);
+                if (done || armed) return;
+                armed = true;
+            }
+            struct box {
+                std::shared_ptr<void> keep;  // the state the completion writes
+                std::shared_ptr<completion> c;
+            };
+            auto* b = new box{std::move(keep), this->shared_from_this()};
+            hpxhip_stream cs = stream;  // no event: armed at creation, on the stream of the work
+            if (ev) {
+                cs = detail::device_pool::get(device).callback_stream();
+                int rw = hpxhip_stream_wait_event(cs, ev);
+                if (rw != HPXHIP_SUCCESS) {
+                    delete b;
+                    detail::check(rw, "hpxhip_stream_wait_event");
+                }
+            }
+            int rc = hpxhip_stream_add_callback(
+                cs,
+                [](void* p, int status) {
+                    auto* bp = static_cast<box*>(p);
+                    bp->c->complete(status);
+                    delete bp;
+                },
+                b);
+            if (rc != HPXHIP_SUCCESS) {
+                delete b;
+                detail::check(rc, "hpxhip_stream_add_callback");
+            }
         }
         ~completion() override {
+            if (pool) {  // never completed: the work may still write the slot
+                if (ev) {
+                    pool->defer_release(slot.id, ev);
+                    ev = nullptr;
+                } else {
+                    pool->release(slot.id);  // no event was recorded: the callback path completed or never queued
+                }
+            }
             if (ev) detail::device_pool::get(device).give_event(ev);
         }
     };
@@ -592,17 +698,18 @@ public:
         return async_result<void>([](unsigned char const*) {});
     }
 
-    // A future completed once all work queued so far is done -- by a stream
-    // callback, or by a get() that waits first: get() waits on a HIP event
-    // recorded behind the work and completes the state itself (r04: the
-    // callback's hand-off had cost ~30 us per par(task) + get(),
-    // profiles/r03_cxx_call_overhead.log).  Completion copies the result
-    // slot's bytes into the shared state, then on_ready(bytes) runs (no HIP
-    // calls: it may run on the callback thread; e.g. a for_loop reduction
-    // folding its view into the live-out variable, for_loop_reduction.hpp:
-    // 60-66) and the state becomes ready.  value(bytes) runs on the first
-    // get(), after the device error word is checked.  The slot returns to
-    // its pool from the callback, which always runs.
+    // A future completed once all work queued so far is done.  A HIP event
+    // is recorded behind the work; get() waits on it and completes the state
+    // itself, is_ready() queries it, and only a continuation (then,
+    // when_all) registers a host callback (r04: registering one per call and
+    // waiting for its hand-off had cost ~20 of the ~31 us of a par(task) +
+    // get(), profiles/r03_cxx_call_overhead.log).  Completion copies the
+    // result slot's bytes into the shared state, returns the slot, then
+    // on_ready(bytes) runs (no HIP calls: it may run on the callback thread;
+    // e.g. a for_loop reduction folding its view into the live-out variable,
+    // for_loop_reduction.hpp:60-66) and the state becomes ready.
+    // value(bytes) runs on the first get(), after the device error word is
+    // checked.
     template <typename R>
     future<R> async_result(std::function<R(unsigned char const*)> value, result_slot slot = {},
                            std::function<void(unsigned char const*)> on_ready = {}) const {
@@ -621,6 +728,7 @@ public:
         c->st = st.get();
         c->on_ready = std::move(on_ready);
         c->device = dev;
+        c->stream = s;
         if (slot) {
             auto d = slot.detach();
             c->pool = d.first;
@@ -629,27 +737,9 @@ public:
         c->ev = detail::device_pool::get(dev).take_event();
         if (c->ev && hpxhip_event_record(c->ev, s) != HPXHIP_SUCCESS) {
             detail::device_pool::get(dev).give_event(c->ev);
-            c->ev = nullptr;  // no early path: the callback completes it
+            c->ev = nullptr;
         }
-        struct box {
-            std::shared_ptr<S> st;
-            std::shared_ptr<completion<S>> c;
-        };
-        auto* b = new box{st, c};
-        int rc = hpxhip_stream_add_callback(
-            s,
-            [](void* p, int status) {
-                auto* bp = static_cast<box*>(p);
-                bp->c->complete(status);
-                bp->c->release_slot();
-                delete bp;
-            },
-            b);
-        if (rc != HPXHIP_SUCCESS) {
-            c->release_slot();
-            delete b;
-            detail::check(rc, "hpxhip_stream_add_callback");
-        }
+        if (!c->ev) c->arm(st);  // no event: only the callback can complete it
         st->early = c;
         return future<R>(st);
     }
