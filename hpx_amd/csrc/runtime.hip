@@ -375,8 +375,13 @@ int hpxhip_event_record(hpxhip_event event, hpxhip_stream stream) {
     return static_cast<int>(
         hipEventRecord(reinterpret_cast<hipEvent_t>(event), reinterpret_cast<hipStream_t>(stream)));
 }
+// The event calls return their status and clear HIP's last error, so a
+// failure the caller handles (a completion falling back to its callback) is
+// not reported again by the next launch's hipGetLastError().
 int hpxhip_event_synchronize(hpxhip_event event) {
-    return static_cast<int>(hipEventSynchronize(reinterpret_cast<hipEvent_t>(event)));
+    hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(event));
+    if (e != hipSuccess) (void)hipGetLastError();
+    return static_cast<int>(e);
 }
 int hpxhip_event_query(hpxhip_event event) {
     hipError_t e = hipEventQuery(reinterpret_cast<hipEvent_t>(event));
@@ -384,6 +389,7 @@ int hpxhip_event_query(hpxhip_event event) {
         (void)hipGetLastError();
         return HPXHIP_ERROR_NOT_READY;
     }
+    if (e != hipSuccess) (void)hipGetLastError();
     return static_cast<int>(e);
 }
 int hpxhip_event_elapsed_ms(hpxhip_event start, hpxhip_event stop, float* ms) {

@@ -264,7 +264,7 @@ namespace detail {
 // a completion callback may still run during static destruction).
 class device_pool {
 public:
-    static constexpr unsigned kChunkSlots = 256, kSlotBytes = 64, kMaxIdleStreams = 32;
+    static constexpr unsigned kChunkSlots = 256, kSlotBytes = 64;
 
     static device_pool& get(int device) {
         static std::mutex m;
@@ -397,15 +397,14 @@ public:
     // A stream handed back may still have queued work: whoever takes it next
     // is ordered behind that work, which is at least as strong as the
     // reference's destroy-while-busy (cudaStreamDestroy returns at once).
+    // Pooled streams are never destroyed: a completion's event may be queried
+    // or waited on long after the stream it was recorded on went back to the
+    // pool, and HIP reads that stream's state then (a destroyed one reported
+    // "event last recorded in a capturing stream").  The pool holds at most as
+    // many streams as targets were ever alive at once.
     void give_stream(hpxhip_stream s) {
-        {
-            std::lock_guard<std::mutex> lk(mtx_);
-            if (streams_.size() < kMaxIdleStreams) {
-                streams_.push_back(s);
-                return;
-            }
-        }
-        hpxhip_stream_destroy(s);
+        std::lock_guard<std::mutex> lk(mtx_);
+        streams_.push_back(s);
     }
 
 private:

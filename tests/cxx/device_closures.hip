@@ -169,10 +169,11 @@ void test_executor(Executor& exec, hip::target const& t, std::mt19937& gen, char
     std::iota(big.begin(), big.end(), 3);
     hpx::compute::vector<int, hip::allocator<int>> bo(big.size(), -1, alloc);
     {
-        // ~10^11 device iterations: not done when the call returns (the
-        // concurrent executor's one-future-per-element result takes a few ms
-        // to build); checked on a sample of the elements
-        constexpr int slow = 100000;
+        // ~10^12 device iterations (tens of ms): not done when the call
+        // returns, even after the concurrent executor has built its
+        // one-future-per-element result (a few ms; 10^11 iterations raced it);
+        // checked on a sample of the elements
+        constexpr int slow = 1000000;
         auto fs = ex::bulk_async_execute(exec, bulk_slow{bo.data(), slow}, big);
         bool pending = false;
         for (auto& f : fs) pending = pending || !f.is_ready();
@@ -180,7 +181,7 @@ void test_executor(Executor& exec, hip::target const& t, std::mt19937& gen, char
         big.assign(big.size(), 0);  // the caller's shape may go away at once
         hpx::when_all(std::move(fs)).get();
         std::vector<int> hb = to_host(bo);
-        for (std::size_t i = 0; i < hb.size(); i += 997)
+        for (std::size_t i = 0; i < hb.size(); i += 9973)
             if (!HPX_TEST_EQ(hb[i], bulk_slow::expect(int(i) + 3, slow))) break;
         HPX_TEST_EQ(hb.back(), bulk_slow::expect(int(hb.size()) + 2, slow));
     }
