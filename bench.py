@@ -304,17 +304,27 @@ def main(argv=None, comm_tgt=None):
 
 
 def timed(L, tgt, fn, reps=3):
+    """Best of `reps` HIP-event intervals on the target's stream around fn().
+    A task-policy call returns its future once the work is enqueued, so the
+    interval is the device time of the call; the future is taken after the
+    stop event (a sync call's interval would also hold the host round trip
+    that returns its result)."""
     ev = Events(L, 2 * reps + 2)
-    fn()
+    _take(fn())
     tgt.synchronize()
     best = 1e30
     for _ in range(reps):
         e0 = ev.record(tgt.stream)
-        fn()
+        r = fn()
         e1 = ev.record(tgt.stream)
         tgt.synchronize()
+        _take(r)
         best = min(best, ev.ms(e0, e1))
     return best
+
+
+def _take(r):
+    return r.get() if hasattr(r, "get") else r
 
 
 def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
@@ -322,11 +332,15 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
     res = {}
     xv, yv = x.local, y.local
     n = n_local
-    ms = timed(L, tgt, lambda: P.copy_if(pol, xv.begin(), xv.end(), yv.begin(), F.not_less_than(0)))
+    # timed as the step is: par(task), device events around the enqueue
+    tpol = ex.par(ex.task).on(hpx.default_executor(tgt))
+    ms = timed(L, tgt, lambda: P.copy_if(tpol, xv.begin(), xv.end(), yv.begin(), F.not_less_than(0)))
+    hits = int(P.copy_if(tpol, xv.begin(), xv.end(), yv.begin(), F.not_less_than(0)).get()[1] - yv.begin())
     res["copy_if_int64"] = {"ms": round(ms, 4), "gbs_model_12B": round(12 * n / ms / 1e6, 1),
-                            "pct_peak": pct(12 * n / ms / 1e6)}
+                            "pct_peak": pct(12 * n / ms / 1e6), "hits": hits,
+                            "gbs_actual_bytes": round((8 * n + 8 * hits) / ms / 1e6, 1)}
     res["segmented_reduce_int64"] = seg_reduce_row(S, F, comm, tgt, pol, x)
-    res["double_reduce_scan"] = double_row(hpx, L, P, F, tgt, pol, n)
+    res["double_reduce_scan"] = double_row(hpx, L, P, F, tgt, pol, tpol, n)
     res["stream_2p30"] = stream_row(hpx, L, P, F, tgt, pol, n)
     # sort of 2^30 uint64 keys (8 GiB + 8 GiB workspace)
     keys = hpx.vector(n, dtype=np.uint64, tgt=tgt)
@@ -439,7 +453,7 @@ def stream_row(hpx, L, P, F, tgt, pol, n, iterations=10, scalar=3.0):
     return out
 
 
-def double_row(hpx, L, P, F, tgt, pol, n):
+def double_row(hpx, L, P, F, tgt, pol, tpol, n):
     """configs[1]'s double leg: transform_reduce and inclusive_scan over 2^30
     doubles in [0, 1) (53-bit mantissas, so the sums round).  Check: the last
     inclusive value against the reduce within the FP-scan tolerance of
@@ -447,8 +461,8 @@ def double_row(hpx, L, P, F, tgt, pol, n):
     xd = hpx.vector(n, dtype=np.float64, tgt=tgt)
     yd = hpx.vector(n, dtype=np.float64, tgt=tgt)
     P.generate(pol, xd.begin(), xd.end(), "unit", 3)
-    ms_r = timed(L, tgt, lambda: P.reduce(pol, xd.begin(), xd.end(), 0.0, F.plus))
-    ms_s = timed(L, tgt, lambda: P.inclusive_scan(pol, xd.begin(), xd.end(), yd.begin(), F.plus, 0.0))
+    ms_r = timed(L, tgt, lambda: P.reduce(tpol, xd.begin(), xd.end(), 0.0, F.plus))
+    ms_s = timed(L, tgt, lambda: P.inclusive_scan(tpol, xd.begin(), xd.end(), yd.begin(), F.plus, 0.0))
     r = float(P.reduce(pol, xd.begin(), xd.end(), 0.0, F.plus))
     last = float(yd[n - 1])
     ntiles = -(-n // (1024 * 12 * 2))

@@ -78,7 +78,11 @@ int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev,
     // at the old bound (4 waves per SIMD) and ran one workgroup per CU:
     // int32 2^31 2.77 -> 2.38 ms (profiles/r02_ubench_copyif_occupancy.log).
     constexpr int kMinWaves = (std::is_same_v<SV, uint32_t> && ALIGNED) ? 8 : 4;
-    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId, false, kRpb, kFixed>), dim3(static_cast<unsigned>(ntiles)),
+    // r04: nontemporal output stores for 8-byte elements, 2.182-2.199 ->
+    // 2.175-2.176 ms at 2^30 int64 (profiles/r04_ubench_copyif8.log; round 2
+    // had measured them slower under counter-ordered tiles)
+    constexpr bool kNtStore = sizeof(T) == 8 && ALIGNED;
+    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId, kNtStore, kRpb, kFixed>), dim3(static_cast<unsigned>(ntiles)),
                        dim3(kThreads), 0, s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles,
                        prefix0);
     HPXHIP_CHECK_LAUNCH();

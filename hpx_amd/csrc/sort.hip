@@ -173,9 +173,9 @@ __device__ inline bool fits(double est, double cap) { return est + 5.0 * sqrt(es
 
 __device__ inline int top_bit_d(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
 
-// Planner, one thread.  stage 0 runs on the first histogram (the two top
-// digits and the 9-bit field under the top byte; every digit for small
-// sorts); stage 1 (after the gated count of the remaining digits) decides a
+// Planner, one thread.  stage 0 runs on the first histogram (the top digit
+// and the 9-bit field under it for the 17-bit form, the two top digits for
+// the 16-bit form; every digit for small sorts); stage 1 (after the gated count of the remaining digits) decides a
 // plan stage 0 left pending.
 //   17-bit form: the top two digits live, the 9-bit field's histogram known:
 //     prefix passes on the 9-bit field then the top byte, buckets = top byte +
@@ -323,10 +323,13 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     constexpr int kField17Shift = field17_shift<U>();
     int mode = n >= kHybridMin ? hybrid_mode() : 0;
     if (HAS_VAL && mode > 16) mode = 16;  // no 9-bit pass with values
-    // a sort that may take the hybrid counts only the two top digits (and the
-    // 9-bit field under the top byte) first -- the LDS atomics, not the read,
-    // bound k_hist -- and the rest only when the plan needs them
-    const int first = mode ? passes - 2 : 0;
+    // a sort that may take the hybrid counts only the digits its plan reads
+    // first -- the LDS atomics, not the read, bound k_hist -- and the rest
+    // only when the plan needs them: the 17-bit form reads the top byte and
+    // the 9-bit field under it (r04: the second byte's count, which only the
+    // 16-bit form reads, moved to the gated count; one LDS atomic per key
+    // fewer), the 16-bit form the two top bytes
+    const int first = mode == 17 ? passes - 1 : (mode ? passes - 2 : 0);
     const bool xfield = mode == 17;
 
     U* kc = static_cast<U*>(keys);

@@ -405,6 +405,10 @@ __device__ __forceinline__ void order_after_poll() { __builtin_amdgcn_fence(__AT
 // Bounded spin: every look-back wait gives up after this many polls and
 // raises the device error word instead of hanging the GPU.
 constexpr uint32_t kSpinLimit = 1u << 24;
+// s_sleep argument between polls (units of 64 clocks)
+#ifndef HPXHIP_LB_SLEEP
+#define HPXHIP_LB_SLEEP 1
+#endif
 
 // Device error word (per library instance); set by a kernel that gave up a
 // spin, read back by hpxhip_device_error().

@@ -128,7 +128,7 @@ struct tile_state {
 #pragma unroll
                 for (int k = 0; k < K; ++k) ok = ok && f[k] != TILE_INVALID;
                 if (__all(ok)) break;
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(HPXHIP_LB_SLEEP);
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (f[k] == TILE_INVALID) f[k] = read(static_cast<uint64_t>(pred - lane - k * kWave), &v[k]);
@@ -223,7 +223,7 @@ struct tile_state {
                     }
                 }
             if (!any) return true;
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(HPXHIP_LB_SLEEP);
             if (++spins > kSpinLimit) return false;
         }
     }
@@ -246,7 +246,7 @@ struct tile_state {
                 *v = from_words<T>(w);
                 return true;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(HPXHIP_LB_SLEEP);
             if (++spins > kSpinLimit) return false;
         }
     }

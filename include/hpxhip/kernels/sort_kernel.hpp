@@ -71,7 +71,11 @@ __device__ __forceinline__ uint32_t peers_below(uint64_t peers) {
 // the 9-bit field at bits [xshift, xshift + 9) into xhist (512 bins; the
 // hybrid sort's 9-bit prefix pass).
 constexpr int kXBins = 512;
-template <typename U, typename X, int THREADS = 256, int COPIES = 4>
+// r04 (scripts/ubench/hist3.hip, profiles/r04_ubench_hist_context.log): LDS
+// sized for the one or two counted digits with 8-16 lane copies measured the
+// same (1.43-1.50 ms back to back, 1.60-1.69 right after the keys were
+// written) as this shape; a plain 16-B read of the keys takes 1.22 / 1.29 ms.
+template <typename U, typename X, int THREADS = 256, int COPIES = 4, int D = static_cast<int>(sizeof(U))>
 __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, uint64_t n, int first, int passes, X xf,
                                                    unsigned long long* __restrict__ hist,
                                                    unsigned long long* __restrict__ bits, int xshift,
@@ -79,9 +83,10 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
                                                    const int32_t* __restrict__ gate = nullptr) {
     if (gate && *gate == 0) return;  // device-planned sort: this count is not needed
     constexpr int P = static_cast<int>(sizeof(U));
-    __shared__ uint32_t h[P * kRadix * COPIES];
+    static_assert(D >= 1 && D <= P, "digit slots");
+    __shared__ uint32_t h[D * kRadix * COPIES];
     __shared__ uint32_t hx[kXBins * COPIES];
-    for (int i = threadIdx.x; i < P * kRadix * COPIES; i += THREADS) h[i] = 0;
+    for (int i = threadIdx.x; i < D * kRadix * COPIES; i += THREADS) h[i] = 0;
     for (int i = threadIdx.x; i < kXBins * COPIES; i += THREADS) hx[i] = 0;
     __syncthreads();
     constexpr int V = 16 / sizeof(U);
@@ -103,7 +108,8 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
         all &= b;
 #pragma unroll
         for (int p = 0; p < P; ++p)
-            if (p >= first && p < passes) atomicAdd(&h[(p * kRadix + ((b >> (8 * p)) & 0xff)) * COPIES + copy], 1u);
+            if (p >= first && p < passes && p - first < D)
+                atomicAdd(&h[((p - first) * kRadix + ((b >> (8 * p)) & 0xff)) * COPIES + copy], 1u);
         if (xshift >= 0) atomicAdd(&hx[static_cast<uint32_t>((b >> xshift) & (kXBins - 1)) * COPIES + copy], 1u);
     };
     for (uint64_t i = tid; i < nvec; i += stride * 4) {
@@ -127,11 +133,12 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
         atomicAnd(&bits[1], static_cast<unsigned long long>(all) | (sizeof(U) == 8 ? 0ull : ~0ull << 32));
     }
     __syncthreads();
-    for (int i = threadIdx.x + first * kRadix; i < passes * kRadix; i += THREADS) {
+    const int counted = (passes - first < D ? passes - first : D) * kRadix;
+    for (int i = threadIdx.x; i < counted; i += THREADS) {
         uint32_t c = 0;
 #pragma unroll
         for (int k = 0; k < COPIES; ++k) c += h[i * COPIES + k];
-        if (c) atomicAdd(&hist[i], static_cast<unsigned long long>(c));
+        if (c) atomicAdd(&hist[first * kRadix + i], static_cast<unsigned long long>(c));
     }
     if (xshift >= 0)
         for (int i = threadIdx.x; i < kXBins; i += THREADS) {
@@ -345,7 +352,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
                 }
                 pred -= used;
                 if (!done && used < LBB) {
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(HPXHIP_LB_SLEEP);
                     if (++spins > kSpinLimit) {
                         if (err)
                             __hip_atomic_store(err, HPXHIP_DEVERR_LOOKBACK_TIMEOUT, __ATOMIC_RELAXED,
@@ -477,8 +484,8 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 // planned buckets (bucket b by workgroup b mod gridDim), so a launch the plan
 // skips costs one gate read per workgroup instead of one dispatch per bucket.
 template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16, typename VAL = uint32_t,
-          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false>
-__global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
+          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false, int MINW = 4>
+__global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
     void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf,
                        VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr,
                        const int32_t* __restrict__ ctl = nullptr, uint32_t first_bucket = 0) {
@@ -496,6 +503,7 @@ __global__ __launch_bounds__(THREADS, 4)  // 4 waves per SIMD: one 1024- or two 
     constexpr int CHUNK = ITEMS * kWave;
     constexpr int BITS = static_cast<int>(sizeof(U) * 8);
     static_assert(THREADS * ITEMS < 65536, "16-bit LDS counters");
+    static_assert(THREADS >= kRadix, "one thread per digit in the offset scan");
     __shared__ alignas(16) U s_keys[THREADS * ITEMS];
     __shared__ alignas(16) VAL s_vals[HAS_VAL ? THREADS * ITEMS : 1];
     __shared__ uint16_t s_whist[WAVES][kRadix];
