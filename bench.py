@@ -324,7 +324,8 @@ def timed(L, tgt, fn, reps=3):
 
 
 def _take(r):
-    return r.get() if hasattr(r, "get") else r
+    from hpx_amd.future import future
+    return r.get() if isinstance(r, future) else r
 
 
 def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):

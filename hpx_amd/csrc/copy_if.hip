@@ -82,7 +82,11 @@ int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev,
     // 2.175-2.176 ms at 2^30 int64 (profiles/r04_ubench_copyif8.log; round 2
     // had measured them slower under counter-ordered tiles)
     constexpr bool kNtStore = sizeof(T) == 8 && ALIGNED;
-    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId, kNtStore, kRpb, kFixed>), dim3(static_cast<unsigned>(ntiles)),
+    // r04, 8-byte elements: 16-B output stores and the one-hop look-back
+    // (copy_if_kernel.hpp): 2.18-2.20 -> 2.13-2.15 ms at 2^30 int64
+    constexpr bool kWide = sizeof(T) == 8 && ALIGNED;
+    constexpr bool kOneHop = sizeof(T) == 8;
+    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId, kNtStore, kRpb, kFixed, kThreads, kWide, kOneHop>), dim3(static_cast<unsigned>(ntiles)),
                        dim3(kThreads), 0, s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles,
                        prefix0);
     HPXHIP_CHECK_LAUNCH();

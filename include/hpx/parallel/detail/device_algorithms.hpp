@@ -233,7 +233,10 @@ void copy_if_launch(compute::hip::target const& t, T const* in, T* out, uint64_t
     K::tile_state<SV> st{reinterpret_cast<uint64_t*>(ws + 256), error_word(t)};
     // blockIdx tile order with the fixed-association look-back (the shipped
     // choice for copy_if, copy_if.hip); 4 waves per SIMD: a user predicate
-    // may need more than 64 VGPRs
+    // may need more than 64 VGPRs.  r04: the shipped kernel's 8-byte
+    // write-out (nt 16-B stores, 4 rounds per LDS batch) and one-hop
+    // look-back took the lambda copy_if from 1.0x to 1.23x of the kind path
+    // here (profiles/r04_closure_timing_copyif.log), so this form keeps them off.
     hipLaunchKernelGGL((C::k_copy_if<T, P, ALIGNED, R, 4, 0, SV, false, false, 1, true>),
                        dim3(static_cast<unsigned>(ntiles)),
                        dim3(C::kThreads), 0, stream_of(t), in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws),

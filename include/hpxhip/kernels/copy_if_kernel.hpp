@@ -32,10 +32,12 @@ using hit_word = std::conditional_t<(BITS <= 32), uint32_t, uint64_t>;
 //   1 = no look-back (tile prefix 0), 2 = hits stored straight from
 //   registers at their ranks (no LDS compaction), 4 = no write-out at all.
 // SV: tile-state value type (uint32_t halves the look-back granules; valid
-// while n < 2^32).
+// while n < 2^32).  WIDE: 8-byte elements stored as 16-B pairs (r04,
+// 2.191-2.196 -> 2.183-2.185 ms at 2^30 int64, profiles/r04_ubench_copyif8_wide.log).
+// ONEHOP: the one-hop fixed look-back (lookback.hpp).
 template <typename T, typename Pred, bool ALIGNED, int ROUNDS, int MINW = 4, int ABL = 0, typename SV = uint64_t,
           bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = false, int RPB = 1, bool FIXED = false,
-          int THREADS = kThreads>
+          int THREADS = kThreads, bool WIDE = false, bool ONEHOP = false>
 __global__ __launch_bounds__(THREADS, MINW) void k_copy_if(const T* in, T* out, uint64_t n, Pred pred,
                                                        uint64_t* count_dev, uint32_t* counter,
                                                        tile_state<SV> st, uint64_t ntiles,
@@ -117,7 +119,12 @@ __global__ __launch_bounds__(THREADS, MINW) void k_copy_if(const T* in, T* out, 
         } else if constexpr ((ABL & 1) == 0) {
             if (lane == 0) st.publish(tile, static_cast<SV>(agg), TILE_AGGREGATE);
             if constexpr (FIXED) {
-                p = st.exclusive_prefix_fixed(tile, op_plus{});
+                // ONEHOP (lookback.hpp): 8-byte elements 2.176-2.184 -> 2.138-2.146
+                // ms at 2^30 int64; 4-byte ones spill 35 VGPRs with it (14 without)
+                // and slow down, 2.27 -> 2.58 ms at 2^31 int32; the int64 scan
+                // measured 2.544 -> 2.576 and keeps the two-hop form
+                // (profiles/r04_ubench_lookback_onehop.log)
+                p = st.template exclusive_prefix_fixed<ONEHOP>(tile, op_plus{});
             } else {
                 p = st.exclusive_prefix(tile, op_plus{});
                 if (lane == 0) st.publish(tile, static_cast<SV>(p + agg), TILE_INCLUSIVE);
@@ -181,12 +188,33 @@ __global__ __launch_bounds__(THREADS, MINW) void k_copy_if(const T* in, T* out, 
         // LDS is in order within a wave; the wait + clobber keep the compiler
         // from hoisting the reads above the writes of other lanes.
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (WIDE && sizeof(T) == 8) {
+            // 16-B stores: one element up to the output's next 16-B boundary,
+            // then element pairs, then an odd last element
+            using V2 = vec<T, 2>;
+            T* o = out + base + out_base;
+            const uint32_t head = bcnt ? static_cast<uint32_t>((reinterpret_cast<uintptr_t>(o) >> 3) & 1u) : 0u;
+            const uint32_t npairs = (bcnt - head) / 2;
+            if (lane == 0 && head) st_stream(&o[0], stage[0]);
+            if (lane == 0 && ((bcnt - head) & 1u)) st_stream(&o[bcnt - 1], stage[bcnt - 1]);
 #pragma unroll
-        for (int k = 0; k < V * RPB; ++k) {
-            const uint32_t j = k * kWave + lane;
-            if (j < bcnt) {
-                if constexpr (NT_STORE) st_stream(&out[base + out_base + j], stage[j]);
-                else out[base + out_base + j] = stage[j];
+            for (int k = 0; k < (V * RPB + 1) / 2; ++k) {
+                const uint32_t q = k * kWave + lane;
+                if (q < npairs) {
+                    V2 w;
+                    w.v[0] = stage[head + 2 * q];
+                    w.v[1] = stage[head + 2 * q + 1];
+                    st_stream(reinterpret_cast<V2*>(o + head + 2 * q), w);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < V * RPB; ++k) {
+                const uint32_t j = k * kWave + lane;
+                if (j < bcnt) {
+                    if constexpr (NT_STORE) st_stream(&out[base + out_base + j], stage[j]);
+                    else out[base + out_base + j] = stage[j];
+                }
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next batch's writes

@@ -43,6 +43,11 @@
 #ifndef HPXHIP_LB_GROUP
 #define HPXHIP_LB_GROUP 64
 #endif
+// Default of the fixed-association look-back's one-hop form (below); the
+// kernels choose it per call (copy_if: one-hop, scans: two-hop).
+#ifndef HPXHIP_LB_ONEHOP
+#define HPXHIP_LB_ONEHOP 0
+#endif
 
 namespace hpxhip {
 
@@ -251,13 +256,83 @@ struct tile_state {
         }
     }
 
+    // ---- one-hop form (r04) ----------------------------------------------
+    // A tile of group g >= 1 that is not the group's first takes
+    //   E(g) = E(g-1) (op) fold(aggregate(64(g-1)) .. aggregate(64g-1))
+    // itself, from E(g-1) (published a whole group earlier) and the previous
+    // group's aggregates, instead of waiting for the group's first tile to
+    // publish E(g): the only fresh waits left are on the aggregates of its
+    // nearest predecessors, one hand-off instead of two.  The association --
+    // and so every bit of a floating-point result -- is the two-hop form's:
+    // E(g) is folded the same way by every tile of the group, and the group's
+    // first tile still publishes it.  Lane l polls the previous group's
+    // aggregate l, its own group's aggregate l (l < pos) and E(g-1), all in
+    // flight together.
+    __device__ __forceinline__ bool wait_onehop(uint64_t first, uint64_t pos, T* prev_agg, T* own_agg, T* e,
+                                                uint32_t& spins) const {
+        const uint64_t lane = static_cast<uint64_t>(lane_id());
+        const uint64_t* p1 = slots + (first - kGroup + lane) * 2 * G;  // aggregate slot
+        const uint64_t* p2 = slots + (first + lane) * 2 * G;           // aggregate slot
+        const uint64_t* p3 = slots + ((first - kGroup) * 2 + 1) * G;   // inclusive slot: E(g-1)
+        bool w1 = lane < kGroup, w2 = lane < pos, w3 = true;
+        while (true) {
+            uint64_t a1[G], a2[G], a3[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                if (w1) a1[g] = __hip_atomic_load(&p1[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (w2) a2[g] = __hip_atomic_load(&p2[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (w3) a3[g] = __hip_atomic_load(&p3[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            auto take = [&](bool& w, const uint64_t (&a)[G], uint32_t status, T* v) {
+                if (!w) return;
+                bool ok = true;
+                uint32_t x[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    ok = ok && static_cast<uint32_t>(a[g] >> 32) == status;
+                    x[g] = static_cast<uint32_t>(a[g]);
+                }
+                if (ok) {
+                    *v = from_words<T>(x);
+                    w = false;
+                }
+            };
+            take(w1, a1, TILE_AGGREGATE, prev_agg);
+            take(w2, a2, TILE_AGGREGATE, own_agg);
+            take(w3, a3, TILE_INCLUSIVE, e);
+            if (!(w1 || w2 || w3)) return true;
+            __builtin_amdgcn_s_sleep(HPXHIP_LB_SLEEP);
+            if (++spins > kSpinLimit) return false;
+        }
+    }
+
     // Called by ALL 64 lanes of one wave, tile > 0.  Returns the exclusive
     // prefix on every lane; a group's first tile also publishes it.
-    template <typename Op>
+    template <bool ONEHOP = HPXHIP_LB_ONEHOP, typename Op>
     __device__ __forceinline__ T exclusive_prefix_fixed(uint64_t tile, Op op) const {
         const T id = Op::template identity<T>();
         const int lane = lane_id();
         const uint64_t first = tile / kGroup * kGroup;
+        if constexpr (ONEHOP && kGroupK == 1) {
+            if (first > 0) {
+                const uint64_t pos = tile - first;
+                uint32_t spins = 0;
+                T a1 = id, a2 = id, e = id;
+                const bool ok = wait_onehop(first, pos, &a1, &a2, &e, spins);
+                if (!__all(ok)) {
+                    if (lane == 0 && err)
+                        __hip_atomic_store(err, HPXHIP_DEVERR_LOOKBACK_TIMEOUT, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    return id;
+                }
+                const T eg = op(readlane(e, 0), wave_reduce(a1, op));  // E(g)
+                if (pos == 0) {
+                    if (lane == 0) publish(tile, eg, TILE_INCLUSIVE);
+                    return eg;
+                }
+                return op(eg, wave_reduce(a2, op));
+            }
+        }
         // the aggregates to fold: the previous group's (a group's first
         // tile) or this group's tiles before this one
         const uint64_t base = tile == first ? first - kGroup : first;
@@ -289,10 +364,31 @@ struct tile_state {
     // The same for an operator without identity (noid_op): the cnt >= 1
     // aggregates are folded by an identity-free wave scan read at lane
     // cnt - 1 (lanes past cnt hold any value and are not read).
-    template <typename Op>
+    template <bool ONEHOP = HPXHIP_LB_ONEHOP, typename Op>
     __device__ __forceinline__ T exclusive_prefix_fixed_noid(uint64_t tile, Op op) const {
         const int lane = lane_id();
         const uint64_t first = tile / kGroup * kGroup;
+        if constexpr (ONEHOP && kGroupK == 1) {
+            if (first > 0) {
+                const uint64_t pos = tile - first;
+                uint32_t spins = 0;
+                T a1{}, a2{}, e{};
+                const bool ok = wait_onehop(first, pos, &a1, &a2, &e, spins);
+                if (!__all(ok)) {
+                    if (lane == 0 && err)
+                        __hip_atomic_store(err, HPXHIP_DEVERR_LOOKBACK_TIMEOUT, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    return e;
+                }
+                // lanes past the counts hold any value and are not read
+                const T eg = op(readlane(e, 0), readlane(wave_inclusive_scan_noid(a1, op), static_cast<int>(kGroup - 1)));
+                if (pos == 0) {
+                    if (lane == 0) publish(tile, eg, TILE_INCLUSIVE);
+                    return eg;
+                }
+                return op(eg, readlane(wave_inclusive_scan_noid(a2, op), static_cast<int>(pos - 1)));
+            }
+        }
         const uint64_t base = tile == first ? first - kGroup : first;
         const uint64_t cnt = tile == first ? kGroup : tile - first;
         uint32_t spins = 0;

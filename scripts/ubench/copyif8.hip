@@ -1,6 +1,7 @@
 // Microbenchmark (round 4, copyif8): phase split of the shipped 2^30 int64
 // copy_if (ABL ablations: 1 no look-back, 4 no write-out, 2 direct scatter)
-// and nt stores, for the PMC passes of scripts/r4/l.sh.
+// and nt stores, for the PMC passes of scripts/r4/l.sh; then (after nt stores
+// shipped) 16-B output stores (WIDE).
 // (copyif7, round 3:) copy_if with the fixed-association look-back
 // (FIXED: tiles read their group's published aggregates plus one group
 // prefix word, lookback.hpp exclusive_prefix_fixed) against the shipped
@@ -37,7 +38,7 @@ struct harness {
   using P = pred_fn<HPXHIP_P_NOT_LT, T>;
   uint64_t N; T *in, *out, *ref_out; char* ws; uint32_t* err; uint64_t* cnt; unsigned long long* bad;
   hipEvent_t e0, e1; uint64_t ref = 0;
-  template <bool DYN, bool FIXED, int R = 8, bool NTS = false, int RPB = 1, int TH = kThreads, int MINW = 8, int ABL = 0>
+  template <bool DYN, bool FIXED, int R = 8, bool NTS = false, int RPB = 1, int TH = kThreads, int MINW = 8, int ABL = 0, bool WIDE = false>
   void run(const char* name) {
     using SV = uint32_t;
     const uint64_t ntiles = (N + tile_elems<T, R, TH>() - 1) / tile_elems<T, R, TH>();
@@ -45,7 +46,7 @@ struct harness {
     tile_state<SV> st{reinterpret_cast<uint64_t*>(ws + 256), err};
     auto launch = [&] {
       CK(hipMemsetAsync(ws, 0, total, 0));
-      k_copy_if<T, P, true, R, MINW, ABL, SV, DYN, NTS, RPB, FIXED, TH><<<ntiles, TH>>>(in, out, N, P{0}, cnt,
+      k_copy_if<T, P, true, R, MINW, ABL, SV, DYN, NTS, RPB, FIXED, TH, WIDE><<<ntiles, TH>>>(in, out, N, P{0}, cnt,
           reinterpret_cast<uint32_t*>(ws), st, ntiles);
     };
     launch(); CK(hipDeviceSynchronize());
@@ -79,16 +80,14 @@ int main(int argc, char** argv) {
   for (int rep = 0; rep < 2; ++rep) {
     harness<int64_t> h{1ull << 30, (int64_t*)in, (int64_t*)out, (int64_t*)ref_out, ws, err, cnt, bad, e0, e1};
     k_fill<int64_t><<<((1ull << 30) + 255) / 256, 256>>>(h.in, h.N); CK(hipDeviceSynchronize());
-    h.run<false, true, 8, false, 4>("T1024 R8 RPB4 2/CU (shipped)");
+    h.run<false, true, 8, true, 4>("T1024 R8 RPB4 2/CU nt (shipped r04)");
     if (only[0]) continue;
-    h.run<false, true, 8, true, 4>("nt stores");
-    h.run<false, true, 8, false, 4, kThreads, 8, 1>("ABL1 no look-back");
-    h.run<false, true, 8, false, 4, kThreads, 8, 4>("ABL4 no write-out");
-    h.run<false, true, 8, false, 4, kThreads, 8, 5>("ABL5 read + predicate only");
-    h.run<false, true, 8, false, 4, kThreads, 8, 2>("ABL2 direct scatter");
-    h.run<false, true, 8, true, 4, 768, 9>("T768 R8 RPB4 3/CU nt");
-    h.run<false, true, 6, true, 3, 1024, 12>("T1024 R6 RPB3 3/CU nt");
-    h.run<false, true, 4, true, 4, 1024, 16>("T1024 R4 RPB4 4/CU nt");
+    h.run<false, true, 8, true, 4, kThreads, 8, 0, true>("16-B stores");
+    h.run<false, true, 8, true, 2, kThreads, 8, 0, true>("16-B stores RPB2");
+    h.run<false, true, 8, true, 8, kThreads, 8, 0, true>("16-B stores RPB8");
+    harness<int64_t> h2{(1ull << 30) - 3, (int64_t*)in, (int64_t*)out + 1, (int64_t*)ref_out, ws, err, cnt, bad, e0, e1};
+    h2.run<false, true, 8, true, 4>("out at 8 B mod 16, n - 3: 8-B stores (reference)");
+    h2.run<false, true, 8, true, 4, kThreads, 8, 0, true>("out at 8 B mod 16, n - 3: 16-B stores");
   }
   uint32_t e = 0; CK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost)); printf("deverr %u\n", e);
   return 0;

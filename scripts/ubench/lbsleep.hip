@@ -63,7 +63,7 @@ int main() {
         for (; i <= probe; ++i) s += h[i];
         int64_t g; CK(hipMemcpy(&g, out + probe, 8, hipMemcpyDeviceToHost)); ok = ok && g == s;
       }
-      printf("sleep %2d group %3d  scan i64    min %7.3f ms med %7.3f ms  %7.1f GB/s %s\n", HPXHIP_LB_SLEEP,
+      printf("onehop %d sleep %2d group %3d  scan i64    min %7.3f ms med %7.3f ms  %7.1f GB/s %s\n", HPXHIP_LB_ONEHOP, HPXHIP_LB_SLEEP,
              scan_detail::kScanGroup, t, med, 16.0 * N / t / 1e6, ok ? "ok" : "MISMATCH");
     }
     {  // copy_if, shipped shape
@@ -77,7 +77,7 @@ int main() {
       float med;
       double t = best([&] {
         CK(hipMemsetAsync(ws, 0, total, 0));
-        k_copy_if<T, P, true, R, 8, 0, SV, false, false, 4, true><<<ntiles, kThreads>>>(in, out, N, P{0}, cnt,
+        k_copy_if<T, P, true, R, 8, 0, SV, false, true, 4, true, kThreads, true><<<ntiles, kThreads>>>(in, out, N, P{0}, cnt,
             reinterpret_cast<uint32_t*>(ws), st, ntiles);
       }, e0, e1, &med);
       uint64_t c = 0; CK(hipMemcpy(&c, cnt, 8, hipMemcpyDeviceToHost));
@@ -86,8 +86,34 @@ int main() {
       int64_t last[2]; int k = 1;
       for (uint64_t i = N; i-- > 0 && k >= 0;) if (h[i] >= 0) last[k--] = h[i];
       const bool ok = c == hc && g[0] == last[0] && g[1] == last[1];
-      printf("sleep %2d group %3d  copy_if i64 min %7.3f ms med %7.3f ms  %7.1f GB/s %s\n", HPXHIP_LB_SLEEP,
+      printf("onehop %d sleep %2d group %3d  copy_if i64 min %7.3f ms med %7.3f ms  %7.1f GB/s %s\n", HPXHIP_LB_ONEHOP, HPXHIP_LB_SLEEP,
              (int)tile_state<SV>::kGroup, t, med, (8.0 * N + 8.0 * c) / t / 1e6, ok ? "ok" : "MISMATCH");
+    }
+    {  // copy_if int32 at 2^31 (the same bytes): two-hop vs one-hop
+      using T = int32_t; using SV = uint32_t;
+      using P = pred_fn<HPXHIP_P_NOT_LT, T>;
+      using namespace copy_if_detail;
+      constexpr int R = 8;
+      const uint64_t N32 = 2 * N;
+      const T* in32 = reinterpret_cast<const T*>(in);
+      T* out32 = reinterpret_cast<T*>(out);
+      const uint64_t ntiles = (N32 + tile_elems<T, R>() - 1) / tile_elems<T, R>();
+      const size_t total = align_up(256 + ntiles * tile_state<SV>::bytes_per_tile(), 256);
+      tile_state<SV> st{reinterpret_cast<uint64_t*>(ws + 256), err};
+      uint64_t c[2];
+      for (int oh = 0; oh < 2; ++oh) {
+        float med;
+        double t = best([&] {
+          CK(hipMemsetAsync(ws, 0, total, 0));
+          if (oh) k_copy_if<T, P, true, R, 8, 0, SV, false, false, 1, true, kThreads, false, true><<<ntiles, kThreads>>>(in32, out32, N32, P{0}, cnt,
+              reinterpret_cast<uint32_t*>(ws), st, ntiles);
+          else k_copy_if<T, P, true, R, 8, 0, SV, false, false, 1, true, kThreads, false, false><<<ntiles, kThreads>>>(in32, out32, N32, P{0}, cnt,
+              reinterpret_cast<uint32_t*>(ws), st, ntiles);
+        }, e0, e1, &med);
+        CK(hipMemcpy(&c[oh], cnt, 8, hipMemcpyDeviceToHost));
+        printf("onehop %d             int32 copy_if 2^31 min %7.3f ms med %7.3f ms  %7.1f GB/s hits %llu %s\n", oh, t, med,
+               (4.0 * N32 + 4.0 * c[oh]) / t / 1e6, (unsigned long long)c[oh], (oh && c[1] != c[0]) ? "COUNT MISMATCH" : "");
+      }
     }
     fflush(stdout);
   }
