@@ -59,16 +59,24 @@ size_t scratch_total(uint64_t n) {
     return carry_off<T>(n) + 256;
 }
 
-template <typename T, bool INCL, bool ALIGNED, typename Conv, typename Op>
+// SHIFTED (ALIGNED only): the output is 16-B aligned and the input is not
+// (scan_kernel.hpp)
+template <typename T, bool INCL, bool ALIGNED, bool SHIFTED = false, typename Conv, typename Op>
 int launch_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, T init, const T* prefix_dev, char* ws,
                 hipStream_t s) {
+    static_assert(ALIGNED || !SHIFTED, "a shifted input needs the vector kernel");
+    // SHIFTED keeps the aligned shape (512 x 16 for 8-byte values, 4-10
+    // spilled VGPRs): 2^30 int64 in+1/out+0 2.56 ms, in+0/out+3 2.61, against
+    // 2.76 / 2.86 with 1024 x 8-round tiles (profiles/r04_unaligned_probe.log)
     constexpr int R = rounds_for<T, ALIGNED>();
     constexpr int TH = threads_for<T, ALIGNED>();
     static_assert(tile_elems<T, R, TH>() >= tile_elems<T, 8>(), "scratch is sized for 1024 x 8-round tiles");
     const uint64_t ntiles = ntiles_for<T, R, TH>(n);
     HPXHIP_CHECK(hipMemsetAsync(ws, 0, align_up(kSlotsOff + ntiles * tile_state<T>::bytes_per_tile(), 256), s));
     scan_detail::scan_state<T> st{reinterpret_cast<uint64_t*>(ws + kSlotsOff), device_error_word(s)};
-    hipLaunchKernelGGL((k_scan<T, Conv, Op, INCL, ALIGNED, R, TH, true, TH == kThreads ? 1 : 4>),
+    hipLaunchKernelGGL((k_scan<T, Conv, Op, INCL, ALIGNED, R, TH, true, TH == kThreads ? 1 : 4, false, 1,
+                               HPXHIP_TILE_DYN_ID, true, T, std::is_floating_point_v<T> && sizeof(T) == 8, true,
+                               SHIFTED>),
                        dim3(static_cast<unsigned>(ntiles)), dim3(TH), 0, s, in, out, n, conv, op, init, prefix_dev,
                        reinterpret_cast<uint32_t*>(ws), st);
     HPXHIP_CHECK_LAUNCH();
@@ -96,17 +104,19 @@ __global__ void k_scan_head(const T* in, T* out, uint64_t h, Conv conv, Op op, T
     *carry = acc;
 }
 
-// Misaligned input and output with the same offset inside 16 B: split off a
-// head that brings the output to a 1-KiB boundary (whole-line stores for
-// every wave) and scan the rest with the vector kernel seeded by the head's
-// carry.  int64 offset by one element: 3.8 -> ~2.7 ms at 2^30
-// (profiles/r02_unaligned_ranges.log).  Returns -1 when the split does not
-// apply (the element-wise kernel takes the range).
+// Misaligned input and output: split off a head that brings the output to a
+// 1-KiB boundary (whole-line stores for every wave) and scan the rest with
+// the vector kernel seeded by the head's carry.  Same offset inside 16 B:
+// int64 offset by one element 3.8 -> ~2.7 ms at 2^30
+// (profiles/r02_unaligned_ranges.log).  Different offsets (r04): the input
+// is read shifted across lanes (k_scan SHIFTED) instead of by the
+// element-wise kernel.  Returns -1 when the split does not apply (the
+// element-wise kernel takes the range).
 template <typename T, bool INCL, typename Conv, typename Op>
 int launch_scan_split(const T* in, T* out, uint64_t n, Conv conv, Op op, T init, const T* prefix_dev, char* ws,
                       hipStream_t s) {
     const uintptr_t ia = reinterpret_cast<uintptr_t>(in), oa = reinterpret_cast<uintptr_t>(out);
-    if (ia % 16 != oa % 16 || ia % sizeof(T) != 0) return -1;
+    if (ia % sizeof(T) != 0 || oa % sizeof(T) != 0) return -1;
     uint64_t h = head_to_align16(out, sizeof(T));
     const uintptr_t v = oa + h * sizeof(T);
     h += ((1024 - v % 1024) % 1024) / sizeof(T);
@@ -115,7 +125,8 @@ int launch_scan_split(const T* in, T* out, uint64_t n, Conv conv, Op op, T init,
     hipLaunchKernelGGL((k_scan_head<T, INCL, Conv, Op>), dim3(1), dim3(64), 0, s, in, out, h, conv, op, init,
                        prefix_dev, carry);
     HPXHIP_CHECK_LAUNCH();
-    return launch_scan<T, INCL, true>(in + h, out + h, n - h, conv, op, init, carry, ws, s);
+    if (ia % 16 == oa % 16) return launch_scan<T, INCL, true>(in + h, out + h, n - h, conv, op, init, carry, ws, s);
+    return launch_scan<T, INCL, true, true>(in + h, out + h, n - h, conv, op, init, carry, ws, s);
 }
 
 template <typename T, typename F>

@@ -133,7 +133,8 @@ __device__ __forceinline__ void tile_prefix(uint64_t tile, const ST& st, Op op, 
 // layer's device closures): conv maps T -> X, unwrap_value X -> T.
 template <typename T, typename Conv, typename Op, bool INCL, bool ALIGNED, int ROUNDS = kRounds,
           int THREADS = kThreads, bool LOOKBACK = true, int MINW = 1, bool EARLY = false, int LBK = 1,
-          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = true, typename X = T, bool DEFER = std::is_floating_point_v<X> && sizeof(X) == 8, bool FIXED = true>
+          bool DYN_ID = HPXHIP_TILE_DYN_ID, bool NT_STORE = true, typename X = T, bool DEFER = std::is_floating_point_v<X> && sizeof(X) == 8, bool FIXED = true,
+          bool SHIFTED = false>
 __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uint64_t n, Conv conv, Op op, X init,
                                                    const X* prefix_dev, uint32_t* counter, scan_state<X> st) {
     constexpr int V = 16 / sizeof(T);
@@ -168,11 +169,46 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
 
     const uint64_t tile_base = tile * TILE;
     const uint64_t wbase = tile_base + wave * WAVE_ELEMS;
-    const bool full = tile_base + TILE <= n;
+    // SHIFTED reads one vector past the wave's block (below)
+    const bool full = tile_base + TILE + (SHIFTED ? V : 0) <= n;
 
     // ---- load (all rounds in flight) and convert
     X x[ROUNDS][V];
-    if (ALIGNED && full) {
+    if constexpr (SHIFTED) {
+        // (r04) The output is 16-B aligned, the input s elements past a
+        // 16-B boundary (ranges whose offsets differ inside 16 B; they took
+        // the element-wise kernel before).  Each lane loads the aligned
+        // vector A under its output vector; the output vector is A's last
+        // V - s elements and the first s of the next aligned vector, which
+        // the next lane holds (DPP wave_shl:1), lane 63 takes from the next
+        // round's lane 0, and the last round's lane 63 from one extra vector
+        // past the wave's block.  One 16-B load per lane per round, as in the
+        // aligned kernel.
+        if (full) {
+            const int sh = static_cast<int>((reinterpret_cast<uintptr_t>(in) % 16) / sizeof(T));
+            const VT* src = reinterpret_cast<const VT*>(in + wbase - sh);
+            VT raw[ROUNDS];
+#pragma unroll
+            for (int r = 0; r < ROUNDS; ++r) raw[r] = ld_stream(&src[r * kWave + lane]);
+            const VT tail = src[ROUNDS * kWave];
+#pragma unroll
+            for (int r = 0; r < ROUNDS; ++r) {
+                const VT nx = r + 1 < ROUNDS ? readlane(raw[r + 1], 0) : tail;
+                const VT nb = dpp<DPP_WAVE_SHL1>(nx, raw[r]);
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    T v = raw[r].v[0];
+#pragma unroll
+                    for (int k = 1; k < 2 * V; ++k)
+                        if (k == e + sh) v = k < V ? raw[r].v[k] : nb.v[k - V];
+                    x[r][e] = conv(v);
+                }
+            }
+        }
+    }
+    if (SHIFTED && full) {
+        // loaded above
+    } else if (ALIGNED && full) {
         const VT* src = reinterpret_cast<const VT*>(in + wbase);
         VT raw[ROUNDS];
 #pragma unroll

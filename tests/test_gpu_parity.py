@@ -553,13 +553,19 @@ def test_roctx_annotation_path():
 # with the same offset inside 16 B -> one-thread head scan to a 1-KiB output
 # boundary, vector kernel seeded with its carry; copy_if: misaligned input ->
 # head compacted first, vector kernel seeded with its count) and through the
-# element-wise kernels (mutually misaligned), against the oracle.
-@pytest.mark.parametrize("dt", [np.int64, np.int32, np.uint32])
-@pytest.mark.parametrize("oin,oout", [(1, 1), (2, 2), (3, 3), (1, 0), (0, 3), (5, 5)])
+# element-wise kernels, against the oracle.  r04: mutually misaligned
+# ranges (offsets that differ inside 16 B) take the vector kernel with the
+# input shifted across lanes (k_scan SHIFTED) after the same head split.
+@pytest.mark.parametrize("dt", [np.int64, np.int32, np.uint32, np.float64])
+@pytest.mark.parametrize("oin,oout", [(1, 1), (2, 2), (3, 3), (1, 0), (0, 3), (5, 5), (0, 1), (2, 1), (3, 0),
+                                      (1, 2), (6, 1)])
 @pytest.mark.parametrize("incl", [True, False])
 def test_scan_misaligned_subranges(pol, gpu_target, dt, oin, oout, incl):
     n = 300007
-    a = rnd(dt, n, 31, *((-1000, 1000) if np.dtype(dt).kind == "i" else (0, 1000)))
+    if np.dtype(dt).kind == "f":  # small integers in doubles: exact sums in any association
+        a = rnd(np.int64, n, 31, -1000, 1000).astype(dt)
+    else:
+        a = rnd(dt, n, 31, *((-1000, 1000) if np.dtype(dt).kind == "i" else (0, 1000)))
     d = dev(a, gpu_target)
     o = hpx.vector(n, dtype=dt, tgt=gpu_target)
     m = n - max(oin, oout) - 11
@@ -568,6 +574,19 @@ def test_scan_misaligned_subranges(pol, gpu_target, dt, oin, oout, incl):
     else:
         P.exclusive_scan(pol, d.begin() + oin, d.begin() + oin + m, o.begin() + oout, 7)
     np.testing.assert_array_equal(o.to_host()[oout:oout + m], O.scan(a[oin:oin + m], 7, incl))
+
+
+@pytest.mark.parametrize("dt,oin,oout", [(np.int64, 1, 0), (np.int64, 0, 1), (np.int32, 3, 1), (np.float64, 1, 0)])
+def test_scan_shifted_input_large(pol, gpu_target, dt, oin, oout):
+    # 2^24 + 5 elements: many tiles of the shifted vector kernel, the last
+    # one partial; int64/int32 exact, doubles hold small integers
+    n = (1 << 24) + 5
+    a = rnd(np.int64, n, 41, -50, 50).astype(dt)
+    d = dev(a, gpu_target)
+    o = hpx.vector(n, dtype=dt, tgt=gpu_target)
+    m = n - max(oin, oout) - 3
+    P.inclusive_scan(pol, d.begin() + oin, d.begin() + oin + m, o.begin() + oout, F.plus, 3)
+    np.testing.assert_array_equal(o.to_host()[oout:oout + m], O.scan(a[oin:oin + m], 3, True))
 
 
 @pytest.mark.parametrize("off", [1, 3])
