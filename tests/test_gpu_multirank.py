@@ -3,8 +3,9 @@ range searches, merge, heat steps, reduce/scan/fold kernels) driven by the
 multi-rank orchestration of hpx_amd.segmented, with both processes on
 cuda:0.  RCCL refuses two ranks on one device, so the collectives here go
 through a host-staged gloo test double (device -> host -> gloo -> device);
-TorchComm's RCCL calls themselves are covered on a one-rank group in
-tests/test_gpu_merge_sort.py.  Results are checked against the oracle."""
+TorchComm's RCCL calls themselves run the same body on a one-rank RCCL
+group (and tests/test_gpu_merge_sort.py's wrapper test).  Results are
+checked against the oracle."""
 import ctypes
 import os
 import socket
@@ -17,17 +18,22 @@ from staged_comm import HostStagedComm
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, size, port, q):
+def _worker(rank, size, port, q, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=size)
+    if backend == "nccl":  # one rank: the product's TorchComm over RCCL
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=size, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=size)
     try:
         import hpx_amd as hpx
         from hpx_amd import execution as ex, functional as F
         from hpx_amd import segmented as S
         tgt = hpx.target(0)
         pol = ex.par.on(hpx.default_executor(tgt))
-        comm = HostStagedComm(tgt)
+        comm = S.TorchComm(tgt) if backend == "nccl" else HostStagedComm(tgt)
         alg = S.segmented()
         res = {}
         n = (1 << 20) + 12345
@@ -76,14 +82,19 @@ def _free_port():
     return p
 
 
-def test_two_ranks_on_gpu_segmented_sort_reduce_scan_stencil(gpu_target):
+@pytest.mark.parametrize("size,backend", [(2, "gloo"), (1, "nccl")])
+def test_ranks_on_gpu_segmented_sort_reduce_scan_stencil(gpu_target, size, backend):
+    """size 2: two processes on cuda:0, collectives host-staged over gloo;
+    size 1 over RCCL: the same orchestration through the product's
+    TorchComm (RCCL all-gathers on device buffers, all_to_all_single into
+    destination views, the halo ring's batch_isend_irecv to itself) -- the
+    N > 1 code path of the 8-GPU run, on the one GPU this box has."""
     import torch.multiprocessing as mp
     from oracle import oracle as O
-    size = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, size, port, q)) for r in range(size)]
+    procs = [ctx.Process(target=_worker, args=(r, size, port, q, backend)) for r in range(size)]
     for p in procs:
         p.start()
     results = dict(q.get(timeout=110) for _ in range(size))
