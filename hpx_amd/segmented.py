@@ -1101,7 +1101,9 @@ def init_distributed(tgt_from_local_rank: bool = True):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     tgt = target(local_rank if tgt_from_local_rank else 0)
-    if world <= 1:
+    # HPXHIP_RCCL_SELF=1 under torchrun: a one-rank RCCL group through
+    # TorchComm (rehearses the N > 1 code path on one GPU)
+    if world <= 1 and os.environ.get("HPXHIP_RCCL_SELF") != "1":
         return LocalComm(tgt), tgt
     import torch
     import torch.distributed as dist
