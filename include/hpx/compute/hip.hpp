@@ -223,31 +223,64 @@ future<T> make_exceptional_future(E const& e) {
 }
 
 // when_all over a vector of futures (hpx/lcos/when_all.hpp): ready once every
-// input is ready (counted down by continuations on the inputs' completions);
-// get() returns the input futures, whose values are then read with get().
+// input is ready; get() returns the input futures, whose values are then
+// read with get().  (r04) Like a single task future, the group completes
+// without host callbacks when it is waited on: a get() waits on each input
+// in turn (an event wait for a device input) and then readies the group;
+// is_ready() asks every input.  Only a continuation on the group (then) arms
+// it: each input then counts the group down from its own completion.
+namespace lcos { namespace detail {
+template <typename T>
+struct when_all_group final : early_completion {
+    using S = shared_state<std::vector<future<T>>>;
+    std::shared_ptr<std::vector<future<T>>> v;
+    S* st = nullptr;  // the group's state, which owns this object
+    std::once_flag armed;
+    void wait_and_complete() override {
+        for (auto& f : *v) f.shared()->wait();
+        st->set_ready(0);
+    }
+    bool try_complete() override {
+        for (auto& f : *v)
+            if (!f.is_ready()) return false;
+        st->set_ready(0);
+        return true;
+    }
+    void arm(std::shared_ptr<void> keep) override {
+        std::call_once(armed, [&] {
+            auto self = std::static_pointer_cast<S>(keep);
+            auto pending = std::make_shared<std::atomic<std::size_t>>(v->size() + 1);
+            auto count_down = [self, pending] {
+                if (pending->fetch_sub(1) == 1) self->set_ready(0);
+            };
+            for (auto& f : *v) {
+                auto const& in = f.shared();
+                std::unique_lock<std::mutex> lk(in->mtx);
+                if (in->ready) {
+                    lk.unlock();
+                    count_down();
+                } else {
+                    in->continuations.push_back(count_down);
+                    lk.unlock();
+                    if (in->early) in->early->arm(in);
+                }
+            }
+            count_down();
+        });
+    }
+};
+}}  // namespace lcos::detail
+
 template <typename T>
 future<std::vector<future<T>>> when_all(std::vector<future<T>>&& fs) {
     using S = lcos::detail::shared_state<std::vector<future<T>>>;
     auto st = std::make_shared<S>();
     auto v = std::make_shared<std::vector<future<T>>>(std::move(fs));
     st->value_fn = [v]() { return std::move(*v); };
-    auto pending = std::make_shared<std::atomic<std::size_t>>(v->size() + 1);
-    auto count_down = [st, pending] {
-        if (pending->fetch_sub(1) == 1) st->set_ready(0);
-    };
-    for (auto& f : *v) {
-        auto const& in = f.shared();
-        std::unique_lock<std::mutex> lk(in->mtx);
-        if (in->ready) {
-            lk.unlock();
-            count_down();
-        } else {
-            in->continuations.push_back(count_down);
-            lk.unlock();
-            if (in->early) in->early->arm(in);
-        }
-    }
-    count_down();
+    auto g = std::make_shared<lcos::detail::when_all_group<T>>();
+    g->v = v;
+    g->st = st.get();
+    st->early = g;
     return future<std::vector<future<T>>>(st);
 }
 
