@@ -387,6 +387,25 @@ def test_copy_if_predicates(pol, gpu_target, pred, name, arg):
     np.testing.assert_array_equal(o.to_host()[: exp.size], exp)
 
 
+@pytest.mark.parametrize("dt,n,sel", [(np.int64, (64 * 3 + 5) * 16384 + 777, 0.5), (np.float64, (64 * 2 + 40) * 16384, 0.5),
+                                      (np.int64, (64 * 2 + 1) * 16384 + 1, 0.97), (np.int64, 64 * 16384 * 2 + 3, 0.02),
+                                      (np.int32, (64 * 3 + 5) * 32768 + 9, 0.5)])
+def test_copy_if_lookback_groups(pol, gpu_target, dt, n, sel):
+    """Several 64-tile look-back groups and a partial last one (16384-element
+    8-byte tiles: the one-hop look-back and 16-B stores; 32768-element int32
+    tiles: the two-hop form), near-empty and near-full selections, and an
+    output that starts 8 B past a 16-B boundary."""
+    rng = np.random.default_rng(n)
+    a = (rng.random(n) < sel).astype(np.int64) * 2 - 1  # +1 selected, -1 not
+    a = (a * rng.integers(1, 1000, n)).astype(dt)
+    d, o = dev(a, gpu_target), hpx.vector(n + 1, dtype=dt, tgt=gpu_target)
+    exp = O.copy_if(a, "not_less_than", 0)
+    for off in (0, 1):
+        _, end = P.copy_if(pol, d.begin(), d.end(), o.begin() + off, F.not_less_than(0))
+        assert end - o.begin() == exp.size + off
+        np.testing.assert_array_equal(o.to_host()[off:off + exp.size], exp)
+
+
 def test_copy_if_golden(pol, gpu_target):
     case = golden_cases("copy_if")[0]
     g = load_golden(case)
