@@ -101,7 +101,11 @@ __global__ __launch_bounds__(kRwThreads) void k_binary(const TI* a, const TI* b,
 // i + 1 is the next lane's vector i, so the second read hits the cache.  The
 // caller moves the last vector to the scalar tail, so i + 1 stays inside the
 // range; head >= V keeps vector 0 at or after the range start (ld_shifted:
-// common.hpp).
+// common.hpp).  r04: taking vector i + 1 from the next lane over DPP instead
+// (shift_from_next_lane, as the scan's shifted input does) measured the same
+// or slower here -- triad b+1/c+0/a+0 3.98-3.99 ms both ways, b+0/c+1/a+3
+// 4.17 -> 4.26 (profiles/r04_unaligned_probe_dpp_elementwise.log): the
+// second load is a cache hit, the shuffles are not free.
 template <typename TI, typename C, typename TO, typename F, int V>
 __global__ __launch_bounds__(kRwThreads) void k_unary_sh(const TI* in, TO* out, span3 sp, F f, int sh) {
     using VO = vec<TO, V>;

@@ -296,6 +296,28 @@ enum : int {
     DPP_ROW_BCAST31 = 0x143,
 };
 
+// Elements [sh, sh + V) of the aligned vector pair (mine, the next lane's
+// aligned vector): the next lane's vector comes over DPP wave_shl:1, and
+// lane 63 (whose source is outside the wave) takes `after`, the aligned
+// vector that follows the wave's 64.  A range that starts sh elements past a
+// 16-B boundary is then read with one aligned 16-B load per lane (plus one
+// wave-uniform vector per wave) instead of two (ld_shifted).  All 64 lanes
+// must be active.
+template <typename T, int V>
+__device__ __forceinline__ vec<T, V> shift_from_next_lane(const vec<T, V>& mine, const vec<T, V>& after, int sh) {
+    const vec<T, V> nb = dpp<DPP_WAVE_SHL1>(after, mine);
+    vec<T, V> r;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+        T v = mine.v[0];
+#pragma unroll
+        for (int k = 1; k < 2 * V; ++k)
+            if (k == e + sh) v = k < V ? mine.v[k] : nb.v[k - V];
+        r.v[e] = v;
+    }
+    return r;
+}
+
 // Inclusive wave64 scan: lane l receives x_0 (+) ... (+) x_l, the lower
 // lanes always the left operand (a non-commutative associative op -- a user
 // operator of the C++ layer -- scans in lane order).

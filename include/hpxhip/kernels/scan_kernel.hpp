@@ -193,16 +193,9 @@ __global__ __launch_bounds__(THREADS, MINW) void k_scan(const T* in, T* out, uin
             const VT tail = src[ROUNDS * kWave];
 #pragma unroll
             for (int r = 0; r < ROUNDS; ++r) {
-                const VT nx = r + 1 < ROUNDS ? readlane(raw[r + 1], 0) : tail;
-                const VT nb = dpp<DPP_WAVE_SHL1>(nx, raw[r]);
+                const VT y = shift_from_next_lane<T, V>(raw[r], r + 1 < ROUNDS ? readlane(raw[r + 1], 0) : tail, sh);
 #pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    T v = raw[r].v[0];
-#pragma unroll
-                    for (int k = 1; k < 2 * V; ++k)
-                        if (k == e + sh) v = k < V ? raw[r].v[k] : nb.v[k - V];
-                    x[r][e] = conv(v);
-                }
+                for (int e = 0; e < V; ++e) x[r][e] = conv(y.v[e]);
             }
         }
     }

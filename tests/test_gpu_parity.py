@@ -637,11 +637,12 @@ def test_copy_if_misaligned_input(pol, gpu_target, dt, off, oout):
 # ---- mutually misaligned elementwise ranges (inputs offset from the output
 # inside 16 B): the shifted-vector kernels (aligned vectors i and i+1 of each
 # misaligned input, elements shifted in registers), bit-exact against the
-# oracle for every relative offset of 8-B and 4-B elements.
+# oracle for every relative offset of 8-B and 4-B elements, with partial
+# last waves.
 @pytest.mark.parametrize("dt", [np.float64, np.int64, np.int32, np.float32])
 @pytest.mark.parametrize("oa,ob,oo", [(1, 0, 0), (0, 1, 3), (1, 2, 0), (3, 1, 2), (2, 2, 1), (0, 0, 1)])
-def test_transform_binary_shifted(pol, gpu_target, dt, oa, ob, oo):
-    n = 100003
+@pytest.mark.parametrize("n", [100003, 3001])
+def test_transform_binary_shifted(pol, gpu_target, dt, oa, ob, oo, n):
     a, b = rnd(dt, n, 41, *((-1000, 1000) if np.dtype(dt).kind == "i" else ())), rnd(dt, n, 42, *((-1000, 1000) if np.dtype(dt).kind == "i" else ()))
     da, db = dev(a, gpu_target), dev(b, gpu_target)
     do = hpx.vector(n, dtype=dt, tgt=gpu_target)
