@@ -71,7 +71,8 @@ struct tile_shape {
 
 struct sort_layout {
     uint64_t ntiles;
-    size_t alt_keys, alt_vals, hist, xhist, bits, start, xstart, bounds, ctl, counter, lb, lb_bytes, total;
+    size_t alt_keys, alt_vals, hist, xhist, thist, bits, start, xstart, tstart, bounds, ctl, counter, lb, lb_bytes,
+        total;
     bool wide;  // 64-bit granules
 };
 
@@ -88,13 +89,17 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     off += 8 * kRadix * 8;
     L.xhist = off;  // the 9-bit prefix field's histogram
     off += kXBins * 8;
+    L.thist = off;  // the top 9 bits' histogram (18-bit form)
+    off += kXBins * 8;
     L.bits = off;  // OR / AND of the ordered keys
     off += 256;
     L.start = off;
     off += 8 * kRadix * 8;
     L.xstart = off;
     off += kXBins * 8;
-    L.bounds = off;  // hybrid: bucket bounds (up to 2^17 + 1)
+    L.tstart = off;
+    off += kXBins * 8;
+    L.bounds = off;  // hybrid: bucket bounds (up to 2^18 + 1)
     off = align_up(off + 8 * (kMaxBuckets + 1), 256);
     L.ctl = off;  // the device-side plan (ctl words below)
     off += 256;
@@ -116,8 +121,11 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
 //   16-bit prefix (the two top live bytes): the same 512-thread segments, or
 //     1024-thread segments of <= 18432 keys (one workgroup per CU) for
 //     buckets too large for both -- e.g. top bytes that are constant.
-// HPXHIP_SORT_HYBRID=0 / 16 turns the hybrid / its 17-bit form off (tests,
-// ablations).
+//   18-bit prefix (default, keys): the top 9 bits + the 9 bits under them,
+//     ~4096-key buckets in 512 x 9 segments (kCap18 below).
+// HPXHIP_SORT_HYBRID=0 / 16 / 17 selects the plain LSD / the 16-bit form /
+// the 17-bit form (tests, ablations); a plan whose buckets do not fit its
+// form's segments falls back to the 16-bit form, then to the LSD.
 constexpr int kSegThreads16 = 1024, kSegThreads17 = 512, kSegItems = 18;
 constexpr uint64_t kCap16 = static_cast<uint64_t>(kSegThreads16) * kSegItems;
 constexpr uint64_t kCap17 = static_cast<uint64_t>(kSegThreads17) * kSegItems;
@@ -126,14 +134,30 @@ constexpr uint64_t kCap17 = static_cast<uint64_t>(kSegThreads17) * kSegItems;
 // workgroup per CU).
 constexpr int kSegItemsKV = 9;
 constexpr uint64_t kCapKV = static_cast<uint64_t>(kSegThreads16) * kSegItemsKV;
+// 18-bit form (keys, HPXHIP_SORT_HYBRID=18): two 9-bit prefix passes (the
+// field [P-18, P-9), then the top 9 bits) and ~4096-key buckets sorted by
+// 512 x 9 workgroups, three per CU (2^30 u64: 5.26 ms against 6.43-6.59 for
+// the 8192-key 512 x 18 shape, profiles/r04_ubench_segment_occupancy.log).
+constexpr int kSegItems18 = 9;
+constexpr uint64_t kCap18 = static_cast<uint64_t>(kSegThreads17) * kSegItems18;
 // the 9-bit field under the top byte: bits [47, 56) of a 64-bit key, [15, 24) of a 32-bit one
 template <typename U>
 constexpr int field17_shift() { return static_cast<int>(8 * sizeof(U)) - 17; }
+// 18-bit form: the field under the top 9 bits, and the top 9 bits
+template <typename U>
+constexpr int field18_shift() { return static_cast<int>(8 * sizeof(U)) - 18; }
+template <typename U>
+constexpr int top9_shift() { return static_cast<int>(8 * sizeof(U)) - 9; }
 constexpr uint64_t kHybridMin = 1ull << 22;
 
+// Default form (r04): the 18-bit form -- 2^30 u64 17.81 vs 18.42 ms for the
+// 17-bit form, u32 12.84 vs 13.03, u32 2^28 3.39 vs 3.68
+// (profiles/r04_sort_probe_18bit.log): the 4096-key buckets' segment sort
+// (5.1-5.4 ms against 6.4-6.6) more than pays for the second pass being
+// 9-bit instead of 8-bit (5.3-5.6 against 4.7-4.9).
 int hybrid_mode() {
     const char* e = std::getenv("HPXHIP_SORT_HYBRID");
-    if (!e) return 17;
+    if (!e) return 18;
     return std::atoi(e);
 }
 
@@ -160,7 +184,9 @@ enum : int {
     C_NLSD = 27,       // live digits
     C_DIGITS = 28,     // [28, 36): live digits, least significant first
     C_FIRST = 36,      // the first histogram counted digits [first, passes)
-    C_WORDS = 40
+    C_B9 = 37,         // shift of the top-9-bit prefix pass (18-bit form), -1
+    C_SEGC = 38,       // {on, nb, top_single}: 512 x 9 segment sort (18-bit form)
+    C_WORDS = 44
 };
 static_assert(C_WORDS * 4 <= 256, "plan words fit their slot");
 
@@ -186,6 +212,7 @@ __device__ inline int top_bit_d(uint64_t x) { return x ? 64 - __builtin_clzll(x)
 //     segment, or the 1024-thread keys segment for b2 = 8 buckets over 9216;
 //   otherwise the LSD over the live digits.
 __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const unsigned long long* __restrict__ xhist,
+                            const unsigned long long* __restrict__ thist,
                             const unsigned long long* __restrict__ bits, uint64_t n, int passes, int first, int mode,
                             int has_val, int stage, int32_t* __restrict__ ctl) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -195,6 +222,7 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
     } else {
         for (int i = 0; i < C_WORDS; ++i) ctl[i] = 0;
         for (int i = 0; i < 11; ++i) ctl[i] = -1;
+        ctl[C_B9] = -1;
         ctl[C_FIRST] = first;
     }
     ctl[C_PENDING] = 0;
@@ -220,8 +248,8 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
         }
         return static_cast<double>(m);
     };
-    auto plan = [&](int s1, int s2, int b2, int seg) {
-        const uint32_t nb = 256u << b2;
+    auto plan = [&](int s1, int s2, int b2, int seg, int tbits = 8) {
+        const uint32_t nb = (1u << tbits) << b2;
         ctl[C_BOUNDS + 0] = 1;
         ctl[C_BOUNDS + 1] = static_cast<int32_t>(nb);
         ctl[C_BOUNDS + 2] = s1;
@@ -232,6 +260,17 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
         ctl[seg + 2] = top_bit_d(diff & ((uint64_t(1) << s2) - 1));
     };
     const bool top_two = live[0] == passes - 1 && live[1] == passes - 2;
+    if (mode == 18 && !has_val && stage == 0 && top_two) {
+        // top 9 bits [8P - 9, 8P), field [8P - 18, 8P - 9): b2 <= 9 bits of the field
+        const double m_top = bin_max(thist, kXBins, 1);
+        const int fs = 8 * passes - 18;
+        for (int b2 = 1; b2 <= 9; ++b2)
+            if (fits(m_top * bin_max(xhist, kXBins, 1 << (9 - b2)) / dn, kCap18)) {
+                ctl[C_A9] = fs;
+                ctl[C_B9] = 8 * passes - 9;
+                return plan(8 * passes - 9, fs + 9 - b2, b2, C_SEGC, 9);
+            }
+    }
     if (mode == 17 && !has_val && first > 0 && top_two) {
         const double m_top = bin_max(hist + live[0] * kRadix, kRadix, 1);
         const int fs = 8 * passes - 17;
@@ -329,8 +368,10 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     // the 9-bit field under it (r04: the second byte's count, which only the
     // 16-bit form reads, moved to the gated count; one LDS atomic per key
     // fewer), the 16-bit form the two top bytes
-    const int first = mode == 17 ? passes - 1 : (mode ? passes - 2 : 0);
-    const bool xfield = mode == 17;
+    const int first = mode == 18 ? passes : (mode == 17 ? passes - 1 : (mode ? passes - 2 : 0));
+    const bool xfield = mode == 17 || mode == 18;
+    auto* thist = reinterpret_cast<unsigned long long*>(base + L.thist);
+    auto* tstart = reinterpret_cast<unsigned long long*>(base + L.tstart);
 
     U* kc = static_cast<U*>(keys);
     U* ka = reinterpret_cast<U*>(base + L.alt_keys);
@@ -345,7 +386,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     // the remaining digits [0, first), iff *gate
     auto count_rest = [&](const int32_t* gate) -> int {
         hipLaunchKernelGGL((k_hist<U, X, kHistThreads>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n, 0, first,
-                           X{}, hist, bits, -1, xhist, gate);
+                           X{}, hist, bits, -1, xhist, gate, -1, static_cast<unsigned long long*>(nullptr), 1);
         HPXHIP_CHECK_LAUNCH();
         return offsets();
     };
@@ -362,7 +403,8 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     // segment sort and the prefix passes lose the dispatcher's overlap of a
     // leaving workgroup with a starting one; profiles/r03_sort_probe_persistent.log).
     auto pass = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, int rb, const int32_t* word,
-                    bool persist) -> int {
+                    bool persist, const unsigned long long* bs9 = nullptr) -> int {
+        const unsigned long long* b9 = bs9 ? bs9 : xstart;  // a 9-bit pass's bin starts
         const uint64_t nt = L.ntiles;
         const uint64_t zbytes = align_up(256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), 16);
         hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
@@ -382,11 +424,11 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             if (persist)
                 hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB, true, true,
                                                true>),
-                                   grid, block, 0, s, kin, kout, vin, vout, n, 0, RB == 9 ? xstart : start,
+                                   grid, block, 0, s, kin, kout, vin, vout, n, 0, RB == 9 ? b9 : start,
                                    reinterpret_cast<G*>(base + L.lb), counter, err, X{}, word, nt);
             else
                 hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, RB, true, DYN>),
-                                   grid, block, 0, s, kin, kout, vin, vout, n, 0, RB == 9 ? xstart : start,
+                                   grid, block, 0, s, kin, kout, vin, vout, n, 0, RB == 9 ? b9 : start,
                                    reinterpret_cast<G*>(base + L.lb), counter, err, X{}, word);
         };
         using R8 = std::integral_constant<int, 8>;
@@ -405,34 +447,47 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     };
 
     // ---- first histogram (+ OR / AND of the keys) and the plan
-    HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8 + kXBins * 8, s));  // hist and xhist
+    HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8 + 2 * kXBins * 8, s));  // hist, xhist, thist
     HPXHIP_CHECK(hipMemsetAsync(bits, 0, 8, s));
     HPXHIP_CHECK(hipMemsetAsync(bits + 1, 0xff, 8, s));
-    hipLaunchKernelGGL((k_hist<U, X, kHistThreads>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n, first, passes,
-                       X{}, hist, bits, xfield ? kField17Shift : -1, xhist, static_cast<const int32_t*>(nullptr));
+    if (mode == 18)  // the field and the top 9 bits; no byte digit
+        hipLaunchKernelGGL((k_hist<U, X, kHistThreads, 4, 2, true>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n,
+                           first, passes, X{}, hist, bits, field18_shift<U>(), xhist,
+                           static_cast<const int32_t*>(nullptr), top9_shift<U>(), thist);
+    else
+        hipLaunchKernelGGL((k_hist<U, X, kHistThreads>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n, first,
+                           passes, X{}, hist, bits, xfield ? kField17Shift : -1, xhist,
+                           static_cast<const int32_t*>(nullptr));
     HPXHIP_CHECK_LAUNCH();
     if ((rc = offsets())) return rc;
     if (xfield) {
         hipLaunchKernelGGL(k_bin_offsets<kXBins>, dim3(1), dim3(kXBins), 0, s, xhist, xstart);
         HPXHIP_CHECK_LAUNCH();
     }
-    hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, bits, n, passes, first, mode, HAS_VAL ? 1 : 0,
-                       0, ctl);
+    if (mode == 18) {
+        hipLaunchKernelGGL(k_bin_offsets<kXBins>, dim3(1), dim3(kXBins), 0, s, thist, tstart);
+        HPXHIP_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, thist, bits, n, passes, first, mode,
+                       HAS_VAL ? 1 : 0, 0, ctl);
     HPXHIP_CHECK_LAUNCH();
     if (first > 0) {
         if ((rc = count_rest(ctl + C_HIST_A))) return rc;
-        hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, bits, n, passes, first, mode,
+        hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, thist, bits, n, passes, first, mode,
                            HAS_VAL ? 1 : 0, 1, ctl);
         HPXHIP_CHECK_LAUNCH();
     }
 
     // ---- hybrid: prefix passes (keys -> alt -> keys), bucket bounds, per-bucket LDS sort
     if (mode) {
-        if (!HAS_VAL && mode == 17 && (rc = pass(kc, ka, nullptr, nullptr, 9, ctl + C_A9, false))) return rc;
+        if (!HAS_VAL && (mode == 17 || mode == 18) && (rc = pass(kc, ka, nullptr, nullptr, 9, ctl + C_A9, false)))
+            return rc;
         // the second-byte pass runs in the 16-bit form only (pairs; keys the
-        // 17-bit form does not fit)
-        if ((rc = pass(kc, ka, vc, va, 8, ctl + C_A8, mode == 17))) return rc;
-        if ((rc = pass(ka, kc, va, vc, 8, ctl + C_B, false))) return rc;
+        // 17-/18-bit form does not fit); the top-byte pass in the 16- and
+        // 17-bit forms, the top-9-bit pass in the 18-bit form
+        if ((rc = pass(kc, ka, vc, va, 8, ctl + C_A8, mode >= 17))) return rc;
+        if ((rc = pass(ka, kc, va, vc, 8, ctl + C_B, mode == 18))) return rc;
+        if (!HAS_VAL && mode == 18 && (rc = pass(ka, kc, nullptr, nullptr, 9, ctl + C_B9, false, tstart))) return rc;
         hipLaunchKernelGGL((k_bucket_bounds<U, X>), dim3((kMaxBuckets + 1 + 255) / 256), dim3(256), 0, s, kc, n, 0, 0,
                            0, 0u, X{}, bounds, ctl + C_BOUNDS);
         HPXHIP_CHECK_LAUNCH();
@@ -451,22 +506,45 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         // workgroup per CU.
         const unsigned cus = static_cast<unsigned>(current_device_info().cus);
         const uint64_t want = 2 * (n / 8192 + 1);
-        const uint32_t g0 = static_cast<uint32_t>(want > kMaxBuckets ? kMaxBuckets : want);
+        constexpr uint64_t kMax17 = uint64_t(1) << 17;  // a 16- or 17-bit plan's buckets
+        const uint32_t g0 = static_cast<uint32_t>(want > kMax17 ? kMax17 : want);
         if constexpr (HAS_VAL) {
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true, true>),
                                dim3(g0), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, vc, oversized,
                                ctl + C_SEGA, 0u);
             HPXHIP_CHECK_LAUNCH();
-            if (g0 < kMaxBuckets)
+            if (g0 < kMax17)
                 hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true, true, true>),
                                    dim3(cus), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, vc, oversized,
                                    ctl + C_SEGA, g0);
+        } else if (mode == 18) {
+            // the 18-bit form's ~4096-key buckets: one workgroup per expected
+            // bucket, then a striding grid; the 512 x 18 segment (a plan that
+            // fell back to the 16-bit form) strides over all of them
+            const uint64_t want18 = 2 * (n / 4096 + 1);
+            const uint32_t g18 = static_cast<uint32_t>(want18 > kMaxBuckets ? kMaxBuckets : want18);
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true>),
+                               dim3(g18), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
+                               ctl + C_SEGC, 0u);
+            HPXHIP_CHECK_LAUNCH();
+            if (g18 < kMaxBuckets)
+                hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true, true>),
+                                   dim3(3 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
+                                   oversized, ctl + C_SEGC, g18);
+            HPXHIP_CHECK_LAUNCH();
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true, true>),
+                               dim3(2 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
+                               oversized, ctl + C_SEGA, 0u);
+            HPXHIP_CHECK_LAUNCH();
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItems, 16, uint32_t, false, true, true>),
+                               dim3(cus), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, nullptr,
+                               oversized, ctl + C_SEGB, 0u);
         } else {
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true>),
                                dim3(g0), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
                                ctl + C_SEGA, 0u);
             HPXHIP_CHECK_LAUNCH();
-            if (g0 < kMaxBuckets)
+            if (g0 < kMax17)
                 hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true, true>),
                                    dim3(2 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
                                    oversized, ctl + C_SEGA, g0);

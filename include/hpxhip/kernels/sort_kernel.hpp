@@ -75,19 +75,39 @@ constexpr int kXBins = 512;
 // sized for the one or two counted digits with 8-16 lane copies measured the
 // same (1.43-1.50 ms back to back, 1.60-1.69 right after the keys were
 // written) as this shape; a plain 16-B read of the keys takes 1.22 / 1.29 ms.
-template <typename U, typename X, int THREADS = 256, int COPIES = 4, int D = static_cast<int>(sizeof(U))>
+// TF (the 18-bit form, sort.hip): also the top 9 bits, [tshift, tshift + 9),
+// into thist (512 bins).
+template <typename U, typename X, int THREADS = 256, int COPIES = 4, int D = static_cast<int>(sizeof(U)),
+          bool TF = false>
 __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, uint64_t n, int first, int passes, X xf,
                                                    unsigned long long* __restrict__ hist,
                                                    unsigned long long* __restrict__ bits, int xshift,
                                                    unsigned long long* __restrict__ xhist,
-                                                   const int32_t* __restrict__ gate = nullptr) {
+                                                   const int32_t* __restrict__ gate = nullptr, int tshift = -1,
+                                                   unsigned long long* __restrict__ thist = nullptr,
+                                                   int skip_constant = 0) {
     if (gate && *gate == 0) return;  // device-planned sort: this count is not needed
     constexpr int P = static_cast<int>(sizeof(U));
+    // skip_constant (a second count, after the first has left the keys' OR /
+    // AND in bits): digits on which every key agrees are not counted -- no
+    // plan reads them, and all 64 lanes adding into one bin serialise (r04:
+    // keys below 2^16 spent ~1 ms of their 2^30 sort counting six constant
+    // bytes)
+    uint32_t live = 0xffu;
+    if (skip_constant) {
+        const unsigned long long diff = bits[0] ^ bits[1];
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+            if (((diff >> (8 * p)) & 0xffu) == 0) live &= ~(1u << p);
+    }
     static_assert(D >= 1 && D <= P, "digit slots");
     __shared__ uint32_t h[D * kRadix * COPIES];
     __shared__ uint32_t hx[kXBins * COPIES];
+    __shared__ uint32_t ht[TF ? kXBins * COPIES : 1];
     for (int i = threadIdx.x; i < D * kRadix * COPIES; i += THREADS) h[i] = 0;
     for (int i = threadIdx.x; i < kXBins * COPIES; i += THREADS) hx[i] = 0;
+    if constexpr (TF)
+        for (int i = threadIdx.x; i < kXBins * COPIES; i += THREADS) ht[i] = 0;
     __syncthreads();
     constexpr int V = 16 / sizeof(U);
     using VT = vec<U, V>;
@@ -108,9 +128,10 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
         all &= b;
 #pragma unroll
         for (int p = 0; p < P; ++p)
-            if (p >= first && p < passes && p - first < D)
+            if (p >= first && p < passes && p - first < D && ((live >> p) & 1u))
                 atomicAdd(&h[((p - first) * kRadix + ((b >> (8 * p)) & 0xff)) * COPIES + copy], 1u);
         if (xshift >= 0) atomicAdd(&hx[static_cast<uint32_t>((b >> xshift) & (kXBins - 1)) * COPIES + copy], 1u);
+        if constexpr (TF) atomicAdd(&ht[static_cast<uint32_t>((b >> tshift) & (kXBins - 1)) * COPIES + copy], 1u);
     };
     for (uint64_t i = tid; i < nvec; i += stride * 4) {
         VT x[4];
@@ -146,6 +167,13 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
 #pragma unroll
             for (int k = 0; k < COPIES; ++k) c += hx[i * COPIES + k];
             if (c) atomicAdd(&xhist[i], static_cast<unsigned long long>(c));
+        }
+    if constexpr (TF)
+        for (int i = threadIdx.x; i < kXBins; i += THREADS) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int k = 0; k < COPIES; ++k) c += ht[i * COPIES + k];
+            if (c) atomicAdd(&thist[i], static_cast<unsigned long long>(c));
         }
 }
 
@@ -414,16 +442,17 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
 // ------------------------------------------------------- hybrid (MSD) tail
 // After two onesweep passes on the most significant live bits (the low
 // prefix field of b2 = 8 or 9 bits at s2, then the top live byte at s1) the
-// keys are ordered by a (8 + b2)-bit prefix; every prefix value is a
-// contiguous bucket.
-constexpr int kMaxBuckets = 1 << 17;
+// keys are ordered by a (8 + b2)-bit prefix (the 18-bit form: 9 + b2);
+// every prefix value is a contiguous bucket.
+constexpr int kMaxBuckets = 1 << 18;
 // longest run of equal-prefix keys the segment sort orders by insertion
 constexpr uint32_t kRunMax = 16;
 
+// tmask: the top digit's mask (0xff, or 0x1ff in the 18-bit form)
 template <typename U, typename X>
-__device__ __forceinline__ uint32_t bucket_of(U k, int s1, int s2, int b2, X xf) {
+__device__ __forceinline__ uint32_t bucket_of(U k, int s1, int s2, int b2, X xf, uint32_t tmask = 0xffu) {
     const U u = xf(k);
-    return (static_cast<uint32_t>(u >> s1) & 0xffu) << b2 | (static_cast<uint32_t>(u >> s2) & ((1u << b2) - 1u));
+    return (static_cast<uint32_t>(u >> s1) & tmask) << b2 | (static_cast<uint32_t>(u >> s2) & ((1u << b2) - 1u));
 }
 
 // off[v] = first index whose prefix is >= v (v = 0..nb): a lower_bound per
@@ -442,10 +471,12 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
     }
     const uint32_t v = blockIdx.x * 256 + threadIdx.x;
     if (v > nb) return;
+    // nb = 2^(top digit bits + b2): the top digit is 8 or 9 bits wide
+    const uint32_t tmask = (1u << (__builtin_ctz(nb) - b2)) - 1u;
     uint64_t lo = 0, hi = n;
     while (lo < hi) {
         const uint64_t mid = lo + (hi - lo) / 2;
-        if (bucket_of(keys[mid], s1, s2, b2, xf) < v) lo = mid + 1;
+        if (bucket_of(keys[mid], s1, s2, b2, xf, tmask) < v) lo = mid + 1;
         else hi = mid;
     }
     off[v] = lo;

@@ -6,7 +6,8 @@ plus b2 bits, b2 chosen from the histograms, one LDS-resident sort per
 bucket (512- or 1024-thread segments); a bucket over its segment's capacity
 sends the whole sort to the LSD over the live digits.  Checked element for
 element against the oracle on the distributions that steer it down each
-branch, in both forms (HPXHIP_SORT_HYBRID=17 / 16).  Sizes start at the
+branch, in every form (HPXHIP_SORT_HYBRID=17 / 16 / 18; 18: two 9-bit
+prefix passes and ~4096-key buckets).  Sizes start at the
 hybrid's 2^22-key threshold.
 
 Parity: std::sort's order for integer keys (sort.hpp:78-229, restated by the
@@ -28,7 +29,7 @@ def pol(gpu_target):
     return ex.par.on(hpx.default_executor(gpu_target))
 
 
-@pytest.fixture(params=["17", "16"], autouse=True)
+@pytest.fixture(params=["17", "16", "18"], autouse=True)
 def form(request, monkeypatch):
     monkeypatch.setenv("HPXHIP_SORT_HYBRID", request.param)
     return request.param
