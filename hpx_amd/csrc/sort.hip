@@ -69,10 +69,13 @@ struct tile_shape {
     static constexpr int tile = threads * items;
 };
 
+// tiles per k_hist_tiles workgroup (chunk of the per-tile offset scan)
+constexpr uint64_t kTileChunk = 256;
+
 struct sort_layout {
     uint64_t ntiles;
     size_t alt_keys, alt_vals, hist, xhist, thist, bits, start, xstart, tstart, bounds, ctl, counter, lb, lb_bytes,
-        total;
+        tcount, csum, nchunks, total;
     bool wide;  // 64-bit granules
 };
 
@@ -108,6 +111,13 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     L.lb = off;
     L.lb_bytes = L.ntiles * kXBins * (L.wide ? 8 : 4);  // room for a 9-bit pass
     off = align_up(off + L.lb_bytes, 256);
+    // 18-bit form, keys only: per-tile field counts -> offsets of the first
+    // prefix pass, and the chunk totals (k_hist_tiles)
+    L.nchunks = vsize ? 0 : (L.ntiles + kTileChunk - 1) / kTileChunk;
+    L.tcount = off;
+    off = align_up(off + (vsize ? 0 : L.ntiles * kXBins * 4), 256);
+    L.csum = off;
+    off = align_up(off + L.nchunks * kXBins * 4, 256);
     L.total = off;
     return L;
 }
@@ -403,13 +413,15 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     // segment sort and the prefix passes lose the dispatcher's overlap of a
     // leaving workgroup with a starting one; profiles/r03_sort_probe_persistent.log).
     auto pass = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, int rb, const int32_t* word,
-                    bool persist, const unsigned long long* bs9 = nullptr) -> int {
+                    bool persist, const unsigned long long* bs9 = nullptr, const uint32_t* pre = nullptr) -> int {
         const unsigned long long* b9 = bs9 ? bs9 : xstart;  // a 9-bit pass's bin starts
         const uint64_t nt = L.ntiles;
         const uint64_t zbytes = align_up(256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), 16);
-        hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
-                           reinterpret_cast<uint4*>(counter), zbytes / 16, word);
-        HPXHIP_CHECK_LAUNCH();
+        {  // (the PRE pass too: its tiles are claimed from the counter, which this zeroes)
+            hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
+                               reinterpret_cast<uint4*>(counter), zbytes / 16, word);
+            HPXHIP_CHECK_LAUNCH();
+        }
         const uint64_t cap = 2ull * static_cast<uint64_t>(current_device_info().cus);
         const dim3 grid(static_cast<unsigned>(persist && nt > cap ? cap : nt)), block(TS::threads);
         auto launch = [&](auto gtag, auto rbtag) {
@@ -433,7 +445,17 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         };
         using R8 = std::integral_constant<int, 8>;
         using R9 = std::integral_constant<int, 9>;
-        if (rb == 9) {
+        if (rb == 9 && pre) {
+            // precomputed tile offsets: no look-back.  Tile ids from the
+            // counter, as the look-back pass takes them: in blockIdx order
+            // the pass ran 8.4 ms against 5.1 (profiles/r04_sort_pre_blockidx.txt)
+            // -- the order in which tiles finish decides how the partial
+            // lines at the ends of their digit runs meet in the caches
+            if constexpr (!HAS_VAL)
+                hipLaunchKernelGGL((k_onesweep<U, VAL, false, uint32_t, X, TS::threads, TS::items, -1, 9, true, true>),
+                                   grid, block, 0, s, kin, kout, vin, vout, n, 0, b9,
+                                   reinterpret_cast<uint32_t*>(base + L.lb), counter, err, X{}, word, nt, pre);
+        } else if (rb == 9) {
             if constexpr (!HAS_VAL) {
                 if (L.wide) launch((unsigned long long)0, R9{});
                 else launch(uint32_t(0), R9{});
@@ -450,7 +472,18 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8 + 2 * kXBins * 8, s));  // hist, xhist, thist
     HPXHIP_CHECK(hipMemsetAsync(bits, 0, 8, s));
     HPXHIP_CHECK(hipMemsetAsync(bits + 1, 0xff, 8, s));
-    if (mode == 18)  // the field and the top 9 bits; no byte digit
+    // 18-bit form, keys, n < 2^32: the first count also leaves the field's
+    // per-tile counts for the first prefix pass (k_hist_tiles)
+    // (same-box A/B, profiles/r04_sort_ab_pre_offsets.log: 2^30 u64 17.99-18.05
+    // -> 17.58-17.68 ms, u32 13.17-13.26 -> 12.55-12.62 against the look-back pass)
+    const bool pre18 = mode == 18 && !HAS_VAL && n < (uint64_t(1) << 32) && TS::tile == 8192;
+    auto* tcount = reinterpret_cast<uint32_t*>(base + L.tcount);
+    auto* csum = reinterpret_cast<uint32_t*>(base + L.csum);
+    if (pre18)
+        hipLaunchKernelGGL((k_hist_tiles<U, X, 8192, kXBins>), dim3(static_cast<unsigned>(L.nchunks)), dim3(kXBins), 0,
+                           s, kc, n, L.ntiles, static_cast<uint32_t>(kTileChunk), X{}, field18_shift<U>(),
+                           top9_shift<U>(), tcount, csum, xhist, thist, bits);
+    else if (mode == 18)  // the field and the top 9 bits; no byte digit
         hipLaunchKernelGGL((k_hist<U, X, kHistThreads, 4, 2, true>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n,
                            first, passes, X{}, hist, bits, field18_shift<U>(), xhist,
                            static_cast<const int32_t*>(nullptr), top9_shift<U>(), thist);
@@ -480,7 +513,15 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
 
     // ---- hybrid: prefix passes (keys -> alt -> keys), bucket bounds, per-bucket LDS sort
     if (mode) {
-        if (!HAS_VAL && (mode == 17 || mode == 18) && (rc = pass(kc, ka, nullptr, nullptr, 9, ctl + C_A9, false)))
+        if (pre18) {  // the first prefix pass's tile offsets, iff the plan takes it
+            hipLaunchKernelGGL(k_tile_chunk_scan, dim3(1), dim3(kXBins), 0, s, csum, L.nchunks, xstart, ctl + C_A9);
+            HPXHIP_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_tile_offsets, dim3(static_cast<unsigned>(L.nchunks)), dim3(kXBins), 0, s, tcount,
+                               L.ntiles, static_cast<uint32_t>(kTileChunk), csum, ctl + C_A9);
+            HPXHIP_CHECK_LAUNCH();
+        }
+        if (!HAS_VAL && (mode == 17 || mode == 18) &&
+            (rc = pass(kc, ka, nullptr, nullptr, 9, ctl + C_A9, false, nullptr, pre18 ? tcount : nullptr)))
             return rc;
         // the second-byte pass runs in the 16-bit form only (pairs; keys the
         // 17-/18-bit form does not fit); the top-byte pass in the 16- and

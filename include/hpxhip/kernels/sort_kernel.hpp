@@ -177,6 +177,142 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
         }
 }
 
+// ------------------------------------------- per-tile counts (r04, 18-bit form)
+// The first prefix pass without a look-back.  A 9-bit pass runs 5.54 ms at
+// 2^30 keys with its look-back and 3.37 with none at all
+// (profiles/r04_ubench_sortpass3_lbb0.log; that ablation's wrong offsets
+// also fold its stores into a few lines, so it overstates the saving), and
+// the first pass's tiles are the input's own: their digit counts can come out
+// of the histogram read that precedes the pass.  Measured: the pass 5.3-5.5
+// -> 5.1 ms, the sort 2^30 u64 18.0 -> 17.6 ms, u32 13.2 -> 12.6.  k_hist_tiles reads the keys
+// once, in the onesweep's 8192-key tiles, CHUNK consecutive tiles per
+// workgroup, and writes
+//   tcount[t * 512 + d]  tile t's count of field digit d,
+//   csum[c * 512 + d]    chunk c's total of digit d,
+// plus the field's and the top 9 bits' histograms and the keys' OR / AND (what
+// k_hist<..., TF> gives).  k_tile_chunk_scan turns the chunk totals into
+// exclusive prefixes (from the digits' bin starts), k_tile_offsets the tile
+// counts into each tile's destination offsets, which the pass reads instead
+// of walking back (k_onesweep PRE).  Offsets are 32-bit: n < 2^32.
+template <typename U, typename X, int TILE = 8192, int THREADS = 512>
+__global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ keys, uint64_t n, uint64_t ntiles,
+                                                         uint32_t chunk, X xf, int xshift, int tshift,
+                                                         uint32_t* __restrict__ tcount, uint32_t* __restrict__ csum,
+                                                         unsigned long long* __restrict__ xhist,
+                                                         unsigned long long* __restrict__ thist,
+                                                         unsigned long long* __restrict__ bits) {
+    static_assert(THREADS == kXBins, "one thread per field digit");
+    constexpr int V = 16 / static_cast<int>(sizeof(U));
+    constexpr int VPT = TILE / V / THREADS;  // 16-B vectors per thread per tile
+    static_assert(VPT * V * THREADS == TILE, "tile of whole vectors");
+    using VT = vec<U, V>;
+    __shared__ uint32_t cnt[kXBins];
+    __shared__ uint32_t ht[kXBins * 2];
+    const int d = threadIdx.x;
+    cnt[d] = 0;
+    ht[2 * d] = 0;
+    ht[2 * d + 1] = 0;
+    __syncthreads();
+    const bool aligned = reinterpret_cast<uintptr_t>(keys) % 16 == 0;
+    const uint32_t copy = d & 1u;
+    U any = 0, all = static_cast<U>(~U(0));
+    uint32_t csum_d = 0;
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * chunk;
+    const uint64_t t1 = t0 + chunk < ntiles ? t0 + chunk : ntiles;
+    auto count = [&](U b) {
+        any |= b;
+        all &= b;
+        atomicAdd(&cnt[static_cast<uint32_t>(b >> xshift) & (kXBins - 1)], 1u);
+        atomicAdd(&ht[(static_cast<uint32_t>(b >> tshift) & (kXBins - 1)) * 2 + copy], 1u);
+    };
+    for (uint64_t t = t0; t < t1; ++t) {
+        const uint64_t base = t * TILE;
+        if (aligned && base + TILE <= n) {
+            const VT* vk = reinterpret_cast<const VT*>(keys + base);
+            VT x[VPT];
+#pragma unroll
+            for (int j = 0; j < VPT; ++j) x[j] = ld_stream(&vk[j * THREADS + d]);
+#pragma unroll
+            for (int j = 0; j < VPT; ++j)
+#pragma unroll
+                for (int e = 0; e < V; ++e) count(xf(x[j].v[e]));
+        } else {
+            const uint64_t m = n - base < TILE ? n - base : TILE;
+            for (uint64_t i = d; i < m; i += THREADS) count(xf(keys[base + i]));
+        }
+        __syncthreads();
+        const uint32_t c = cnt[d];
+        tcount[t * kXBins + d] = c;
+        csum_d += c;
+        cnt[d] = 0;
+        __syncthreads();
+    }
+    csum[static_cast<uint64_t>(blockIdx.x) * kXBins + d] = csum_d;
+    if (csum_d) atomicAdd(&xhist[d], static_cast<unsigned long long>(csum_d));
+    const uint32_t tc = ht[2 * d] + ht[2 * d + 1];
+    if (tc) atomicAdd(&thist[d], static_cast<unsigned long long>(tc));
+    any = wave_reduce(any, op_bit_or{});
+    all = wave_reduce(all, op_bit_and{});
+    if (lane_id() == 0) {
+        atomicOr(&bits[0], static_cast<unsigned long long>(any));
+        atomicAnd(&bits[1], static_cast<unsigned long long>(all) | (sizeof(U) == 8 ? 0ull : ~0ull << 32));
+    }
+}
+
+// Chunk totals -> exclusive prefixes from the field's bin starts (one
+// workgroup, thread d walks digit d's column); runs iff *gate >= 0.
+__global__ __launch_bounds__(kXBins) void k_tile_chunk_scan(uint32_t* __restrict__ csum, uint64_t nchunks,
+                                                            const unsigned long long* __restrict__ xstart,
+                                                            const int32_t* __restrict__ gate) {
+    if (*gate < 0) return;
+    const int d = threadIdx.x;
+    uint32_t run = static_cast<uint32_t>(xstart[d]);
+    uint64_t c = 0;
+    for (; c + 8 <= nchunks; c += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = csum[(c + j) * kXBins + d];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            csum[(c + j) * kXBins + d] = run;
+            run += v[j];
+        }
+    }
+    for (; c < nchunks; ++c) {
+        const uint32_t v = csum[c * kXBins + d];
+        csum[c * kXBins + d] = run;
+        run += v;
+    }
+}
+
+// Tile counts -> tile offsets in place (workgroup c: chunk c's tiles, thread
+// d: digit d); runs iff *gate >= 0.
+__global__ __launch_bounds__(kXBins) void k_tile_offsets(uint32_t* __restrict__ tcount, uint64_t ntiles,
+                                                         uint32_t chunk, const uint32_t* __restrict__ csum,
+                                                         const int32_t* __restrict__ gate) {
+    if (*gate < 0) return;
+    const int d = threadIdx.x;
+    uint32_t run = csum[static_cast<uint64_t>(blockIdx.x) * kXBins + d];
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * chunk;
+    const uint64_t t1 = t0 + chunk < ntiles ? t0 + chunk : ntiles;
+    uint64_t t = t0;
+    for (; t + 8 <= t1; t += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = tcount[(t + j) * kXBins + d];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            tcount[(t + j) * kXBins + d] = run;
+            run += v[j];
+        }
+    }
+    for (; t < t1; ++t) {
+        const uint32_t v = tcount[t * kXBins + d];
+        tcount[t * kXBins + d] = run;
+        run += v;
+    }
+}
+
 // Exclusive scan of each pass's R counts (one R-thread block per pass).
 template <int R = kRadix>
 __global__ __launch_bounds__(R) void k_bin_offsets(const unsigned long long* __restrict__ hist,
@@ -224,7 +360,8 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
                                                        const unsigned long long* __restrict__ bin_start,
                                                        G* __restrict__ lb, uint32_t* __restrict__ counter,
                                                        uint32_t* __restrict__ err, X xf,
-                                                       const int32_t* __restrict__ ctl = nullptr, uint64_t ntiles = 0) {
+                                                       const int32_t* __restrict__ ctl = nullptr, uint64_t ntiles = 0,
+                                                       const uint32_t* __restrict__ pre = nullptr) {
     static_assert(!PERSIST || STAGE, "the persistent form keeps the LDS-staged write-out");
     // device-planned sort (sort.hip): *ctl = this launch's digit shift, or
     // -1 when the plan does not take this pass (every block returns at once)
@@ -392,6 +529,8 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             __hip_atomic_store(&my[t], enc_incl<G>(excl + tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         s_adj[t] = static_cast<uint64_t>(bin_start[t]) + excl - (STAGE ? s_local[t] : 0u);
+        if constexpr (LBB < 0)  // PRE: the tile's destination offsets, precomputed (k_tile_offsets)
+            s_adj[t] = static_cast<uint64_t>(pre[tile * R + t]) - (STAGE ? s_local[t] : 0u);
     }
     __syncthreads();
     if constexpr (!STAGE) {

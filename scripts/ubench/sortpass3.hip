@@ -83,6 +83,10 @@ int main() {
                            n, SHIFT, BS, lbg, counter, err, X{});                                             \
     }, n)
     for (int rep = 0; rep < 2; ++rep) {
+        // r04: LBB 0 = no look-back at all (wrong offsets, in-bounds writes):
+        // what the look-back costs each pass
+        PASS(9, 0, 47, xstart);
+        PASS(8, 0, 56, start + 7 * 256);
         PASS(9, 4, 47, xstart);
         PASS(9, 2, 47, xstart);
         PASS(9, 1, 47, xstart);
