@@ -291,11 +291,20 @@ void merge_sort(compute::hip::target const& t, T* data, uint64_t n, Comp const& 
     uint64_t* splits = reinterpret_cast<uint64_t*>(ws + buf);
     T* src = data;
     T* dst = tmp;
+    // 16-B staging and stores when both buffers are 16-B aligned (the
+    // scratch is; the data is unless the range starts inside a vector) and
+    // n fills whole vectors (the staging reads whole vectors of each slice)
+    const bool vec = reinterpret_cast<uintptr_t>(data) % 16 == 0 && reinterpret_cast<uintptr_t>(tmp) % 16 == 0 &&
+                     n % M::vec_elems<T>() == 0;
     for (uint64_t w = M::kTile; w < n; w *= 2) {
         hipLaunchKernelGGL((M::k_pass_partition<T, L>), dim3(static_cast<unsigned>((ntiles + 255) / 256)), dim3(256),
                            0, stream_of(t), src, n, w, ntiles, less, splits);
-        hipLaunchKernelGGL((M::k_pass_merge<T, L>), dim3(static_cast<unsigned>(ntiles)), dim3(M::kThreads), 0,
-                           stream_of(t), src, n, w, splits, less, dst);
+        if (vec)
+            hipLaunchKernelGGL((M::k_pass_merge<T, L, true>), dim3(static_cast<unsigned>(ntiles)), dim3(M::kThreads),
+                               0, stream_of(t), src, n, w, splits, less, dst);
+        else
+            hipLaunchKernelGGL((M::k_pass_merge<T, L>), dim3(static_cast<unsigned>(ntiles)), dim3(M::kThreads), 0,
+                               stream_of(t), src, n, w, splits, less, dst);
         launched("sort (device closure): merge pass");
         std::swap(src, dst);
     }

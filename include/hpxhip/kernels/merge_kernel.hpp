@@ -243,7 +243,10 @@ __global__ __launch_bounds__(256) void k_pass_partition(const T* __restrict__ sr
     splits[t] = path_split(src + p0, na, src + p0 + na, nb, o - p0, less);
 }
 
-template <typename T, typename Less>
+// VEC (src and dst 16-B aligned): the run slices are staged with aligned
+// 16-B loads and a full tile is stored with 16-B nontemporal stores (r04;
+// element loads and stores before).
+template <typename T, typename Less, bool VEC = false>
 __global__ __launch_bounds__(kThreads) void k_pass_merge(const T* __restrict__ src, uint64_t n, uint64_t w,
                                                           const uint64_t* __restrict__ splits, Less less,
                                                           T* __restrict__ dst) {
@@ -264,12 +267,25 @@ __global__ __launch_bounds__(kThreads) void k_pass_merge(const T* __restrict__ s
     const int la = static_cast<int>(a1 - a0), lb = static_cast<int>(b1 - b0);
     const int len = la + lb;
     const T* a = src + p0;
-    const T* b = src + p0 + na;
-    for (int i = threadIdx.x; i < la; i += kThreads) s[i] = a[a0 + i];
-    for (int i = threadIdx.x; i < lb; i += kThreads) s[la + i] = b[b0 + i];
+    const T* b = src + p0 + na;  // 16-B aligned whenever lb > 0 (na = w, a multiple of kTile)
+    if constexpr (VEC) {
+        stage<T, true>(a, a0, a1, s);
+        stage<T, true>(b, b0, b1, s + la);
+    } else {
+        for (int i = threadIdx.x; i < la; i += kThreads) s[i] = a[a0 + i];
+        for (int i = threadIdx.x; i < lb; i += kThreads) s[la + i] = b[b0 + i];
+    }
     __syncthreads();
     merge_in_lds(s, la, lb, less);
-    for (int i = threadIdx.x; i < len; i += kThreads) dst[d0 + i] = s[i];
+    constexpr int V = vec_elems<T>();
+    if (VEC && V > 1 && len == kTile) {
+        using VT = vec<T, V>;
+        const VT* vsrc = reinterpret_cast<const VT*>(s);
+        VT* vo = reinterpret_cast<VT*>(dst + d0);
+        for (int v = threadIdx.x; v < kTile / V; v += kThreads) st_stream(&vo[v], vsrc[v]);
+    } else {
+        for (int i = threadIdx.x; i < len; i += kThreads) dst[d0 + i] = s[i];
+    }
 }
 
 }  // namespace merge_detail
