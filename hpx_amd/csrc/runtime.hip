@@ -372,8 +372,9 @@ int hpxhip_event_destroy(hpxhip_event event) {
     return static_cast<int>(hipEventDestroy(reinterpret_cast<hipEvent_t>(event)));
 }
 int hpxhip_event_record(hpxhip_event event, hpxhip_stream stream) {
-    return static_cast<int>(
-        hipEventRecord(reinterpret_cast<hipEvent_t>(event), reinterpret_cast<hipStream_t>(stream)));
+    const hipError_t e = hipEventRecord(reinterpret_cast<hipEvent_t>(event), reinterpret_cast<hipStream_t>(stream));
+    if (e != hipSuccess) (void)hipGetLastError();  // returned, not left for the next launch's check
+    return static_cast<int>(e);
 }
 // The event calls return their status and clear HIP's last error, so a
 // failure the caller handles (a completion falling back to its callback) is

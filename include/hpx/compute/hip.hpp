@@ -405,8 +405,14 @@ public:
                 return e;
             }
         }
+        // created with this pool's device current: an event is recorded on
+        // streams of the device it was created on (a multi-GPU process)
+        int prev = -1;
+        const bool swap = hpxhip_get_device(&prev) == HPXHIP_SUCCESS && prev != device_ &&
+                          hpxhip_set_device(device_) == HPXHIP_SUCCESS;
         hpxhip_event e = nullptr;
-        if (hpxhip_event_create(&e) != HPXHIP_SUCCESS) return nullptr;
+        if (hpxhip_event_create(&e) != HPXHIP_SUCCESS) e = nullptr;
+        if (swap) hpxhip_set_device(prev);
         return e;
     }
     void give_event(hpxhip_event e) {
