@@ -504,13 +504,20 @@ inline void on_stream_done(hpxhip_stream s, std::function<void()> fn) {
     }
 }
 
-// `after` waits (on the device) for the work queued on `before` so far.
+// `after` waits (on the device) for the work queued on `before` so far.  If
+// the runtime refuses the event on `before` (a stream of another device than
+// the current one), the host waits for `before` instead: slower, same order.
 inline void stream_after(hpxhip_stream after, hpxhip_stream before) {
     if (after == before) return;
     hpxhip_event e = nullptr;
     check(hpxhip_event_create(&e), "hpxhip_event_create");
     int rc = hpxhip_event_record(e, before);
-    if (rc == HPXHIP_SUCCESS) rc = hpxhip_stream_wait_event(after, e);
+    if (rc != HPXHIP_SUCCESS) {
+        hpxhip_event_destroy(e);
+        check(hpxhip_stream_synchronize(before), "stream ordering");
+        return;
+    }
+    rc = hpxhip_stream_wait_event(after, e);
     hpxhip_event_destroy(e);  // released once the wait no longer needs it
     check(rc, "stream ordering");
 }
