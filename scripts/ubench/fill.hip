@@ -56,6 +56,20 @@ int main() {
     CK(hipMalloc(&a, n * 8));
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+    {  // first writes into a fresh allocation vs the same launch again
+        double* f;
+        CK(hipMalloc(&f, n * 8));
+        for (int k = 0; k < 3; ++k) {
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL((k_fillv<256, 1, false>), dim3(nvec / 256), dim3(256), 0, 0, f, nvec, 2.5);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("fresh allocation, launch %d       %7.3f ms  %7.1f GB/s\n", k, ms, 8.0 * n / ms / 1e6);
+        }
+        CK(hipFree(f));
+    }
 #define V(T, U, NT)                                                                                          \
     bench("threads " #T " vec/thr " #U " nt " #NT, [&] {                                                    \
         hipLaunchKernelGGL((k_fillv<T, U, NT>), dim3((nvec + T * U - 1) / (T * U)), dim3(T), 0, 0, a, nvec, 1.5); \
