@@ -24,7 +24,7 @@ OFLAGS   := -O2 -fPIC -std=c++17 -ffp-contract=off -Wall -pthread
 .PHONY: all lib oracle clean cxxtests oracle-sanitize
 
 # C++ tests of include/hpx (plain g++ host code linked to the C ABI library)
-CXXT     := compute_api algorithms_known_answer stream_hip for_loop_merge stencil_partitioned call_overhead exception_list
+CXXT     := compute_api algorithms_known_answer stream_hip for_loop_merge stencil_partitioned call_overhead exception_list futures
 CXXTBIN  := $(CXXT:%=tests/cxx/bin/%)
 CXXHDR   := $(shell find include -name '*.hpp') include/hpxhip.h
 TFLAGS   := -O2 -std=c++17 -Wall -Wextra -Wno-unused-parameter -pthread -Iinclude
@@ -55,7 +55,7 @@ tests/cxx/bin/oracle_sanitize: tests/cxx/oracle_sanitize.cpp oracle/oracle.cpp o
 	$(CXX) $(SANFLAGS) tests/cxx/oracle_sanitize.cpp oracle/oracle.cpp -o $@
 
 # ... and the hipcc-compiled ones (device closures, HPX_HOST_DEVICE lambdas)
-HIPT     := device_closures partitioned_vector closure_algorithms closure_timing
+HIPT     := device_closures partitioned_vector closure_algorithms closure_timing dataflow_stencil
 HIPTBIN  := $(HIPT:%=tests/cxx/bin/%)
 HTFLAGS  := -O2 -std=c++17 --offload-arch=$(ARCH) --offload-compress -Wall -Wno-unused-parameter -Iinclude
 
@@ -68,6 +68,11 @@ tests/cxx/bin/%: tests/cxx/%.cpp $(CXXHDR) $(LIB)
 tests/cxx/bin/%: tests/cxx/%.hip $(CXXHDR) $(LIB)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HTFLAGS) $< -o $@ $(TLINK)
+
+# the dataflow stencil checks itself against the oracle (test infrastructure)
+tests/cxx/bin/dataflow_stencil: tests/cxx/dataflow_stencil.hip $(CXXHDR) $(LIB) $(ORACLE)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HTFLAGS) $< -o $@ $(TLINK) -Loracle/_build -loracle -Wl,-rpath,'$$ORIGIN/../../../oracle/_build'
 
 clean:
 	rm -rf $(BUILD) $(LIB) oracle/_build tests/cxx/bin

@@ -51,6 +51,8 @@ struct annotate {
 // the next algorithm entry on this thread.
 extern thread_local int g_inject_status;
 extern thread_local int g_inject_count;
+extern thread_local int g_event_inject_status;  // hpxhip_debug_inject_event_error
+extern thread_local int g_event_inject_count;
 inline int take_injected_error() {
     if (__builtin_expect(g_inject_count == 0, 1)) return 0;
     --g_inject_count;

@@ -230,9 +230,18 @@ extern "C++" {
 namespace hpxhip {
 thread_local int g_inject_status = 0;
 thread_local int g_inject_count = 0;
+thread_local int g_event_inject_status = 0;
+thread_local int g_event_inject_count = 0;
 }  // namespace hpxhip
 }
 
+int hpxhip_debug_inject_event_error(int status, int count) {
+    if (count < 0 || (count > 0 && (status == HPXHIP_SUCCESS || status == HPXHIP_ERROR_NOT_READY)))
+        return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hpxhip::g_event_inject_status = status;
+    hpxhip::g_event_inject_count = count;
+    return 0;
+}
 int hpxhip_debug_inject_error(int status, int count) {
     if (count < 0 || (count > 0 && status == HPXHIP_SUCCESS)) return HPXHIP_ERROR_INVALID_ARGUMENT;
     hpxhip::g_inject_status = status;
@@ -368,6 +377,29 @@ int hpxhip_event_create(hpxhip_event* event) {
     *event = reinterpret_cast<hpxhip_event>(e);
     return 0;
 }
+// An event created with `device` current and, unless `timing`, without
+// timestamps (an ordering or completion event: hipEventDisableTiming).  A
+// HIP event is recorded on streams of the device it was created on; this is
+// what lets one process order work across its GPUs without a host wait.
+int hpxhip_event_create_on(int device, int timing, hpxhip_event* event) {
+    if (!event) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    int prev = 0;
+    HPXHIP_CHECK(hipGetDevice(&prev));
+    if (prev != device) HPXHIP_CHECK(hipSetDevice(device));
+    hipEvent_t e = nullptr;
+    const hipError_t rc = hipEventCreateWithFlags(&e, timing ? hipEventDefault : hipEventDisableTiming);
+    if (prev != device) (void)hipSetDevice(prev);
+    if (rc != hipSuccess) {
+        (void)hipGetLastError();
+        return static_cast<int>(rc);
+    }
+    *event = reinterpret_cast<hpxhip_event>(e);
+    return 0;
+}
+int hpxhip_stream_device(hpxhip_stream stream, int* device) {
+    if (!device) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    return stream_device(reinterpret_cast<hipStream_t>(stream), device);
+}
 int hpxhip_event_destroy(hpxhip_event event) {
     return static_cast<int>(hipEventDestroy(reinterpret_cast<hipEvent_t>(event)));
 }
@@ -380,11 +412,19 @@ int hpxhip_event_record(hpxhip_event event, hpxhip_stream stream) {
 // failure the caller handles (a completion falling back to its callback) is
 // not reported again by the next launch's hipGetLastError().
 int hpxhip_event_synchronize(hpxhip_event event) {
+    if (hpxhip::g_event_inject_count > 0) {
+        --hpxhip::g_event_inject_count;
+        return hpxhip::g_event_inject_status;
+    }
     hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(event));
     if (e != hipSuccess) (void)hipGetLastError();
     return static_cast<int>(e);
 }
 int hpxhip_event_query(hpxhip_event event) {
+    if (hpxhip::g_event_inject_count > 0) {
+        --hpxhip::g_event_inject_count;
+        return hpxhip::g_event_inject_status;
+    }
     hipError_t e = hipEventQuery(reinterpret_cast<hipEvent_t>(event));
     if (e == hipErrorNotReady) {
         (void)hipGetLastError();

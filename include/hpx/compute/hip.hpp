@@ -9,8 +9,8 @@
 //   hpx::compute::vector<T, Alloc>       <- hpx/compute/vector.hpp:28-372
 //   device iterator + value_proxy        <- hpx/compute/detail/iterator.hpp:23-85,
 //                                           cuda/value_proxy.hpp:25-124
-//   hpx::future / make_ready_future      <- hpx/lcos/future.hpp (completion from a
-//                                           stream callback, cuda_target.cpp:97-142)
+//   completion of device work -> future  <- src/compute/cuda/cuda_target.cpp:97-142
+//                                           (futures: <hpx/lcos/future.hpp>)
 //
 // Compiles with any C++17 host compiler (g++ is enough) and links against
 // hpx_amd/libhpxhip.so; there is no host fallback -- a failing call throws.
@@ -19,6 +19,8 @@
 #include <hpxhip.h>
 #include <hpx/exception.hpp>
 #include <hpx/exception_list.hpp>
+#include <hpx/lcos/future.hpp>
+#include <hpx/lcos/when_all.hpp>
 
 #include <atomic>
 #include <condition_variable>
@@ -40,249 +42,9 @@
 
 namespace hpx {
 
-// ------------------------------------------------------------------ errors
-// hpx::exception, kernel_error, out_of_memory: <hpx/exception.hpp>;
-// hpx::exception_list: <hpx/exception_list.hpp>.
-
-namespace compute { namespace hip { namespace detail {
-inline void check(int status, char const* what) {
-    if (status == HPXHIP_SUCCESS) return;
-    std::string msg = std::string(what) + ": " + hpxhip_error_string(status);
-    if (status == HPXHIP_ERROR_OUT_OF_MEMORY) throw out_of_memory(msg);
-    throw kernel_error(status, msg);
-}
-inline kernel_error check_noexcept(int status) {
-    return kernel_error(status, std::string("hip stream callback: ") + hpxhip_error_string(status));
-}
-}}}  // namespace compute::hip::detail
-
-// ------------------------------------------------------------------ future
-namespace lcos { namespace detail {
-// A completion a waiting get() may run itself (target::async_result): it
-// waits on a HIP event recorded behind the work instead of for the host
-// callback, whose hand-off costs ~30 us (profiles/r03_cxx_call_overhead.log).
-// r04: the host callback is registered only when something must be told
-// without asking (a continuation, when_all); get() and is_ready() use the
-// event directly.
-struct early_completion {
-    virtual void wait_and_complete() = 0;
-    virtual bool try_complete() = 0;                          // non-blocking
-    virtual void arm(std::shared_ptr<void> keep_state) = 0;  // ensure a completion callback
-    virtual ~early_completion() = default;
-};
-
-template <typename T>
-struct shared_state {
-    std::mutex mtx;
-    std::condition_variable cv;
-    bool ready = false;
-    std::exception_ptr exc;
-    // Result bytes of a device computation, copied out of the pinned result
-    // slot by the completion callback itself: the state owns what get() reads,
-    // nothing is borrowed from the target that launched the work.
-    alignas(16) unsigned char raw[64] = {};
-    std::function<T()> value_fn;  // run once the device work is done
-    typename std::conditional<std::is_void<T>::value, int, T>::type value{};
-    std::vector<std::function<void()>> continuations;
-    std::once_flag evaluated;  // value_fn runs once, on the first get()
-    // The future of a parallel algorithm under a task policy: its failure is
-    // reported as the algorithm's error (bad_alloc or hpx::exception_list,
-    // hpx/parallel/exception_list.hpp:81-111), set by parallel::detail::guarded.
-    bool algorithm_result = false;
-    std::shared_ptr<early_completion> early;  // set by target::async_result
-
-    void set_ready(int status) {
-        std::vector<std::function<void()>> conts;
-        {
-            std::lock_guard<std::mutex> lk(mtx);
-            if (status != 0)
-                exc = std::make_exception_ptr(compute::hip::detail::check_noexcept(status));
-            ready = true;
-            conts.swap(continuations);
-        }
-        cv.notify_all();
-        for (auto& c : conts) c();
-    }
-    void wait() {
-        {
-            std::lock_guard<std::mutex> lk(mtx);
-            if (ready) return;
-        }
-        if (early) early->wait_and_complete();
-        std::unique_lock<std::mutex> lk(mtx);
-        cv.wait(lk, [&] { return ready; });
-    }
-};
-}}  // namespace lcos::detail
-
-template <typename T>
-class future {
-    using state = lcos::detail::shared_state<T>;
-    std::shared_ptr<state> st_;
-
-    void resolve() {
-        st_->wait();
-        std::call_once(st_->evaluated, [this] {
-            if (!st_->exc && st_->value_fn) {
-                try {
-                    if constexpr (std::is_void<T>::value) st_->value_fn();
-                    else st_->value = st_->value_fn();
-                } catch (...) {
-                    st_->exc = std::current_exception();
-                }
-            }
-            if (st_->exc && st_->algorithm_result) st_->exc = hpx::detail::to_algorithm_error(st_->exc);
-        });
-    }
-
-public:
-    using result_type = T;
-    future() = default;
-    explicit future(std::shared_ptr<state> s) : st_(std::move(s)) {}
-    bool valid() const { return static_cast<bool>(st_); }
-    bool is_ready() const {
-        {
-            std::lock_guard<std::mutex> lk(st_->mtx);
-            if (st_->ready) return true;
-        }
-        if (st_->early) st_->early->try_complete();
-        std::lock_guard<std::mutex> lk(st_->mtx);
-        return st_->ready;
-    }
-    void wait() { st_->wait(); }
-    T get() {
-        resolve();
-        if (st_->exc) std::rethrow_exception(st_->exc);
-        if constexpr (!std::is_void<T>::value) return st_->value;
-    }
-    bool has_exception() {
-        resolve();
-        return static_cast<bool>(st_->exc);
-    }
-    bool has_value() {
-        resolve();
-        return !st_->exc;
-    }
-    std::exception_ptr get_exception_ptr() {
-        resolve();
-        return st_->exc;
-    }
-    // hpx::future::then -- runs the continuation on the thread that calls get()
-    // on the returned future (deferred), after this future is ready.
-    template <typename F>
-    auto then(F&& f) -> future<decltype(f(std::declval<future<T>&>()))> {
-        using R = decltype(f(std::declval<future<T>&>()));
-        auto nst = std::make_shared<lcos::detail::shared_state<R>>();
-        auto self = std::make_shared<future<T>>(std::move(*this));
-        nst->value_fn = [self, f = std::forward<F>(f)]() mutable -> R { return f(*self); };
-        auto raw = nst;
-        auto parent = self->st_;
-        {
-            std::unique_lock<std::mutex> lk(parent->mtx);
-            if (!parent->ready) {
-                parent->continuations.push_back([raw] { raw->set_ready(0); });
-                lk.unlock();
-                if (parent->early) {
-                    parent->early->arm(parent);
-                    nst->early = parent->early;  // a get() on the continuation may complete the parent itself
-                }
-                return future<R>(nst);
-            }
-        }
-        nst->set_ready(0);
-        return future<R>(nst);
-    }
-    std::shared_ptr<state> const& shared() const { return st_; }
-};
-
-template <typename T>
-future<typename std::decay<T>::type> make_ready_future(T&& v) {
-    using V = typename std::decay<T>::type;
-    auto st = std::make_shared<lcos::detail::shared_state<V>>();
-    V val = std::forward<T>(v);
-    st->value_fn = [val]() { return val; };
-    st->set_ready(0);
-    return future<V>(st);
-}
-inline future<void> make_ready_future() {
-    auto st = std::make_shared<lcos::detail::shared_state<void>>();
-    st->set_ready(0);
-    return future<void>(st);
-}
-// hpx/lcos/future.hpp make_exceptional_future: a ready future holding e.
-template <typename T>
-future<T> make_exceptional_future(std::exception_ptr e) {
-    auto st = std::make_shared<lcos::detail::shared_state<T>>();
-    st->exc = std::move(e);
-    st->set_ready(0);
-    return future<T>(st);
-}
-template <typename T, typename E>
-future<T> make_exceptional_future(E const& e) {
-    return make_exceptional_future<T>(std::make_exception_ptr(e));
-}
-
-// when_all over a vector of futures (hpx/lcos/when_all.hpp): ready once every
-// input is ready; get() returns the input futures, whose values are then
-// read with get().  (r04) Like a single task future, the group completes
-// without host callbacks when it is waited on: a get() waits on each input
-// in turn (an event wait for a device input) and then readies the group;
-// is_ready() asks every input.  Only a continuation on the group (then) arms
-// it: each input then counts the group down from its own completion.
-namespace lcos { namespace detail {
-template <typename T>
-struct when_all_group final : early_completion {
-    using S = shared_state<std::vector<future<T>>>;
-    std::shared_ptr<std::vector<future<T>>> v;
-    S* st = nullptr;  // the group's state, which owns this object
-    std::once_flag armed;
-    void wait_and_complete() override {
-        for (auto& f : *v) f.shared()->wait();
-        st->set_ready(0);
-    }
-    bool try_complete() override {
-        for (auto& f : *v)
-            if (!f.is_ready()) return false;
-        st->set_ready(0);
-        return true;
-    }
-    void arm(std::shared_ptr<void> keep) override {
-        std::call_once(armed, [&] {
-            auto self = std::static_pointer_cast<S>(keep);
-            auto pending = std::make_shared<std::atomic<std::size_t>>(v->size() + 1);
-            auto count_down = [self, pending] {
-                if (pending->fetch_sub(1) == 1) self->set_ready(0);
-            };
-            for (auto& f : *v) {
-                auto const& in = f.shared();
-                std::unique_lock<std::mutex> lk(in->mtx);
-                if (in->ready) {
-                    lk.unlock();
-                    count_down();
-                } else {
-                    in->continuations.push_back(count_down);
-                    lk.unlock();
-                    if (in->early) in->early->arm(in);
-                }
-            }
-            count_down();
-        });
-    }
-};
-}}  // namespace lcos::detail
-
-template <typename T>
-future<std::vector<future<T>>> when_all(std::vector<future<T>>&& fs) {
-    using S = lcos::detail::shared_state<std::vector<future<T>>>;
-    auto st = std::make_shared<S>();
-    auto v = std::make_shared<std::vector<future<T>>>(std::move(fs));
-    st->value_fn = [v]() { return std::move(*v); };
-    auto g = std::make_shared<lcos::detail::when_all_group<T>>();
-    g->v = v;
-    g->st = st.get();
-    st->early = g;
-    return future<std::vector<future<T>>>(st);
-}
+// Errors (hpx::exception, kernel_error, out_of_memory, exception_list) come
+// from <hpx/exception.hpp> / <hpx/exception_list.hpp>; futures, when_all and
+// the completion engine from <hpx/lcos/future.hpp> / <hpx/lcos/when_all.hpp>.
 
 namespace compute { namespace hip {
 
@@ -329,14 +91,6 @@ public:
     void release(unsigned id) {
         std::lock_guard<std::mutex> lk(mtx_);
         free_.push_back(id);
-    }
-    // The device's callback stream: a completion armed after its work was
-    // queued waits there on its event (the stream that queued the work may
-    // have gone back to the pool, or been destroyed, by then).
-    hpxhip_stream callback_stream() {
-        std::lock_guard<std::mutex> lk(mtx_);
-        if (!cb_stream_) check(hpxhip_stream_create(device_, &cb_stream_), "hpxhip_stream_create");
-        return cb_stream_;
     }
     // A slot whose future was dropped before its work completed: freed (and
     // its event returned) once the event shows the work done.
@@ -405,14 +159,10 @@ public:
                 return e;
             }
         }
-        // created with this pool's device current: an event is recorded on
-        // streams of the device it was created on (a multi-GPU process)
-        int prev = -1;
-        const bool swap = hpxhip_get_device(&prev) == HPXHIP_SUCCESS && prev != device_ &&
-                          hpxhip_set_device(device_) == HPXHIP_SUCCESS;
+        // created on this pool's device (an event is recorded on streams of
+        // the device it was created on), without timestamps
         hpxhip_event e = nullptr;
-        if (hpxhip_event_create(&e) != HPXHIP_SUCCESS) e = nullptr;
-        if (swap) hpxhip_set_device(prev);
+        if (hpxhip_event_create_on(device_, 0, &e) != HPXHIP_SUCCESS) e = nullptr;
         return e;
     }
     void give_event(hpxhip_event e) {
@@ -481,10 +231,16 @@ private:
     std::vector<hpxhip_stream> streams_;
     std::vector<hpxhip_event> events_;
     std::vector<std::pair<unsigned, hpxhip_event>> deferred_;
-    hpxhip_stream cb_stream_ = nullptr;
     std::vector<void*> blocks_, host_blocks_;
     std::vector<unsigned> block_free_[64], host_free_[64];
 };
+
+// Host waits taken by stream ordering because the runtime refused a
+// device-side one (tests assert it stays 0).
+inline std::atomic<unsigned long>& stream_order_host_waits() {
+    static std::atomic<unsigned long> n{0};
+    return n;
+}
 
 // Run fn (no HIP calls: it runs on the HIP callback thread) once the work
 // queued on s so far is done.
@@ -504,22 +260,54 @@ inline void on_stream_done(hpxhip_stream s, std::function<void()> fn) {
     }
 }
 
-// `after` waits (on the device) for the work queued on `before` so far.  If
-// the runtime refuses the event on `before` (a stream of another device than
-// the current one), the host waits for `before` instead: slower, same order.
+// A mark behind the work queued on a stream so far: a pooled event of the
+// stream's own device recorded there (an event is recorded on streams of the
+// device it was created on; hipStreamWaitEvent accepts an event of another
+// device).  wait_on(after) makes `after` wait for it on the device, so a
+// cross-device hand-off -- a segmented carry, a stencil halo -- costs the
+// host two enqueues, not a wait (segmented_algorithms/reduce.hpp:191-207
+// chains the same dependencies through futures).  A wait captures the
+// event's state when it is enqueued, so the event may be re-recorded or go
+// back to the pool right after.  Only if the runtime refuses the record does
+// wait_on() fall back to a host wait for the stream.
+class stream_mark {
+    hpxhip_stream s_ = nullptr;
+    device_pool* pool_ = nullptr;
+    hpxhip_event ev_ = nullptr;
+
+public:
+    explicit stream_mark(hpxhip_stream s) : s_(s) {
+        int dev = 0;
+        check(hpxhip_stream_device(s, &dev), "stream ordering");
+        pool_ = &device_pool::get(dev);
+        ev_ = pool_->take_event();
+        if (ev_ && hpxhip_event_record(ev_, s) != HPXHIP_SUCCESS) {
+            pool_->give_event(ev_);
+            ev_ = nullptr;
+        }
+    }
+    stream_mark(stream_mark&& o) noexcept : s_(o.s_), pool_(o.pool_), ev_(o.ev_) { o.ev_ = nullptr; }
+    stream_mark(stream_mark const&) = delete;
+    stream_mark& operator=(stream_mark const&) = delete;
+    stream_mark& operator=(stream_mark&&) = delete;
+    ~stream_mark() {
+        if (ev_) pool_->give_event(ev_);
+    }
+    void wait_on(hpxhip_stream after) const {
+        if (after == s_) return;
+        if (ev_) {
+            check(hpxhip_stream_wait_event(after, ev_), "stream ordering");
+            return;
+        }
+        stream_order_host_waits().fetch_add(1);
+        check(hpxhip_stream_synchronize(s_), "stream ordering");
+    }
+};
+
+// `after` waits (on the device) for the work queued on `before` so far.
 inline void stream_after(hpxhip_stream after, hpxhip_stream before) {
     if (after == before) return;
-    hpxhip_event e = nullptr;
-    check(hpxhip_event_create(&e), "hpxhip_event_create");
-    int rc = hpxhip_event_record(e, before);
-    if (rc != HPXHIP_SUCCESS) {
-        hpxhip_event_destroy(e);
-        check(hpxhip_stream_synchronize(before), "stream ordering");
-        return;
-    }
-    rc = hpxhip_stream_wait_event(after, e);
-    hpxhip_event_destroy(e);  // released once the wait no longer needs it
-    check(rc, "stream ordering");
+    stream_mark(before).wait_on(after);
 }
 }  // namespace detail
 
@@ -578,8 +366,8 @@ class target {
 
     // Completion of an async_result future, run once: by a get() that
     // waited on the event recorded behind the work, by is_ready() finding
-    // the event complete, or by the stream callback -- registered only when
-    // a continuation needs it (arm).  Completion copies the result slot's
+    // the event complete, or by the completion engine polling the event --
+    // registered only when a continuation needs it (arm).  Completion copies the result slot's
     // bytes into the state and returns the slot to its pool (the work is
     // done by then); a future dropped before completion hands its slot and
     // event to the pool, which frees them once the event has fired.
@@ -611,56 +399,63 @@ class target {
             }
             if (first) st->set_ready(status);
         }
+        // A failing event wait (a faulted kernel: sticky HIP error) readies
+        // the future with that status, so get() reports it through the
+        // algorithm's error mapping (exception_list) and a second get()
+        // returns the same error.
         void wait_and_complete() override {
             {
                 std::lock_guard<std::mutex> lk(m);
                 if (done) return;
             }
-            if (ev && hpxhip_event_synchronize(ev) == HPXHIP_SUCCESS) complete(0);
-            else arm(nullptr);  // no event: the callback completes it
+            if (!ev) return;  // armed at creation: the callback completes it
+            complete(hpxhip_event_synchronize(ev));
         }
         bool try_complete() override {
             {
                 std::lock_guard<std::mutex> lk(m);
                 if (done) return true;
             }
-            if (ev && hpxhip_event_query(ev) == HPXHIP_SUCCESS) {
-                complete(0);
-                return true;
-            }
-            return false;
+            if (!ev) return false;
+            const int rc = hpxhip_event_query(ev);
+            if (rc == HPXHIP_ERROR_NOT_READY) return false;
+            complete(rc);
+            return true;
         }
+        // Complete without a waiter: the completion engine polls the event
+        // (its thread may run continuations that call HIP).  Without an event
+        // (its creation failed) a stream callback posts the completion to the
+        // engine, so no continuation runs on HIP's callback thread.  Both
+        // hold the state (keep) and this completion until it has run.
         void arm(std::shared_ptr<void> keep) override {
             {
                 std::lock_guard<std::mutex> lk(m);
                 if (done || armed) return;
                 armed = true;
             }
+            auto self = this->shared_from_this();
+            if (ev) {
+                lcos::detail::engine::get().watch(ev, [self, keep](int rc) { self->complete(rc); });
+                return;
+            }
             struct box {
-                std::shared_ptr<void> keep;  // the state the completion writes
+                std::shared_ptr<void> keep;
                 std::shared_ptr<completion> c;
             };
-            auto* b = new box{std::move(keep), this->shared_from_this()};
-            hpxhip_stream cs = stream;  // no event: armed at creation, on the stream of the work
-            if (ev) {
-                cs = detail::device_pool::get(device).callback_stream();
-                int rw = hpxhip_stream_wait_event(cs, ev);
-                if (rw != HPXHIP_SUCCESS) {
-                    delete b;
-                    detail::check(rw, "hpxhip_stream_wait_event");
-                }
-            }
+            auto* b = new box{std::move(keep), self};
             int rc = hpxhip_stream_add_callback(
-                cs,
+                stream,
                 [](void* p, int status) {
                     auto* bp = static_cast<box*>(p);
-                    bp->c->complete(status);
-                    delete bp;
+                    lcos::detail::engine::get().post([bp, status] {
+                        bp->c->complete(status);
+                        delete bp;
+                    });
                 },
                 b);
             if (rc != HPXHIP_SUCCESS) {
                 delete b;
-                detail::check(rc, "hpxhip_stream_add_callback");
+                complete(rc);
             }
         }
         ~completion() override {

@@ -105,7 +105,7 @@ public:
         for (auto const& c : chunks) total += c.second;
         result.reserve(total);
         for (auto& c : chunks)
-            for (std::size_t i = 0; i < c.second; ++i) result.push_back(c.first);
+            for (std::size_t i = 0; i < c.second; ++i) result.push_back(hpx::future<void>(c.first.shared()));
         return result;
     }
     template <typename F, typename Shape, typename... Ts>

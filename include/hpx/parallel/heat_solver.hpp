@@ -116,19 +116,31 @@ private:
         return j;
     }
 
+    // One pass of s steps.  Partition j's stream first waits, on the device,
+    // for the previous pass of its two neighbours: their kernels wrote the
+    // points j's halos copy now (RAW), and their halo copies read the points
+    // j's kernel overwrites now (WAR).  The marks are all recorded before any
+    // of this pass's work is queued, so a partition never waits for its
+    // neighbours' new pass; no host wait between passes (r04 synchronised
+    // every stream here).
     void pass(int s) {
         space& cur = u(cur_);
         space& nxt = u(cur_ ^ 1);
         const std::size_t np = cur.get_num_partitions();
-        synchronize();  // every partition's points of the previous pass are final
+        std::vector<detail::stream_mark> marks;
+        marks.reserve(np);
+        for (std::size_t j = 0; j != np; ++j) marks.emplace_back(stream(j));
         for (std::size_t j = 0; j != np; ++j) {
             auto& p = cur.get_partition(j);
             const uint64_t n = p.last - p.first;
             if (n == 0) continue;
-            auto const& l = cur.get_partition(neighbour(j, true));
-            auto const& r = cur.get_partition(neighbour(j, false));
+            const std::size_t jl = neighbour(j, true), jr = neighbour(j, false);
+            auto const& l = cur.get_partition(jl);
+            auto const& r = cur.get_partition(jr);
             double* halo = halo_[j].device_data();
             const hpxhip_stream st = stream(j);
+            marks[jl].wait_on(st);
+            marks[jr].wait_on(st);
             // left halo = the left neighbour's last s points, right halo = the right neighbour's first s
             detail::check(hpxhip_memcpy_peer_async(halo, p.target.device(), l.data->device_data() + (l.last - l.first) - s,
                                            l.target.device(), 8 * static_cast<size_t>(s), st),

@@ -167,6 +167,10 @@ int hpxhip_device_error(int device, uint32_t* code);
    the queued work completes. */
 int hpxhip_debug_inject_error(int status, int count);
 int hpxhip_debug_raise_device_error(hpxhip_stream stream, uint32_t code);
+/* The next `count` event waits or queries (hpxhip_event_synchronize /
+   hpxhip_event_query) on this host thread return `status` -- a completion
+   whose event wait fails, as after a kernel fault (count 0 cancels). */
+int hpxhip_debug_inject_event_error(int status, int count);
 
 /* ------------------------------------------------ devices (targets) */
 int hpxhip_get_device_count(int* count);
@@ -189,6 +193,15 @@ int hpxhip_stream_add_callback(hpxhip_stream stream, hpxhip_callback fn, void* u
 
 int hpxhip_event_create(hpxhip_event* event);
 int hpxhip_event_destroy(hpxhip_event event);
+/* An event created on `device` (timing 0: hipEventDisableTiming), so it can
+   be recorded on that device's streams from any host thread -- the ordering
+   event of a cross-device dependency in a multi-GPU process (the reference
+   chains such dependencies through futures, segmented_algorithms/
+   reduce.hpp:191-207; here hpxhip_stream_wait_event on the event). */
+int hpxhip_event_create_on(int device, int timing, hpxhip_event* event);
+/* The device a stream belongs to (NULL stream: the current device). */
+int hpxhip_stream_device(hpxhip_stream stream, int* device);
+
 int hpxhip_event_record(hpxhip_event event, hpxhip_stream stream);
 int hpxhip_event_synchronize(hpxhip_event event);
 int hpxhip_event_query(hpxhip_event event);

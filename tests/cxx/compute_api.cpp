@@ -166,6 +166,72 @@ void test_futures(executor_type& exec) {
     (void)exec;
 }
 
+// Completion paths of device futures:
+//   - futures dropped before their work finished hand slot and event to the
+//     pool, then more reductions than one 256-slot chunk holds;
+//   - when_all(...).then(...).get() over device futures (armed group);
+//   - is_ready() polled on a future armed by a continuation;
+//   - dataflow(unwrapping(f), device futures...) and a shared_future read by
+//     two continuations;
+//   - an event wait that fails (injected): get() reports exception_list with
+//     the HIP status, and a second get() reports it again instead of hanging.
+void test_completion_paths() {
+    hpx::compute::hip::target t;
+    hpx::compute::hip::allocator<double> alloc(t);
+    std::size_t const n = 1 << 22;
+    hpx::compute::vector<double, hpx::compute::hip::allocator<double>> a(n, 1.0, alloc), b(n, 2.0, alloc);
+    hpx::compute::hip::default_executor dexec(t);
+    auto pol = ex::par(ex::task).on(dexec);
+
+    for (int i = 0; i < 64; ++i) (void)hpx::parallel::reduce(pol, a.begin(), a.end(), 0.0);  // dropped at once
+    std::vector<hpx::future<double>> many;
+    for (int i = 0; i < 600; ++i) many.push_back(hpx::parallel::reduce(pol, (i & 1) ? a.begin() : b.begin(),
+                                                                       (i & 1) ? a.end() : b.end(), double(i)));
+    bool all_ok = true;
+    for (int i = 0; i < 600; ++i) all_ok &= many[i].get() == double(i) + ((i & 1) ? 1.0 : 2.0) * double(n);
+    HPX_TEST(all_ok);
+
+    std::vector<hpx::future<double>> fs;
+    for (int i = 0; i < 6; ++i) fs.push_back(hpx::parallel::reduce(pol, a.begin(), a.end(), double(i)));
+    auto sum = hpx::when_all(std::move(fs)).then([](hpx::future<std::vector<hpx::future<double>>> all) {
+        double s = 0;
+        for (auto& f : all.get()) s += f.get();
+        return s;
+    });
+    HPX_TEST_EQ(sum.get(), 6.0 * double(n) + 15.0);
+
+    hpx::future<double> armed = hpx::parallel::reduce(pol, b.begin(), b.end(), 0.0);
+    hpx::shared_future<double> shared = armed.share();
+    auto c1 = shared.then([](hpx::shared_future<double> f) { return f.get() + 1.0; });
+    auto c2 = shared.then([](hpx::shared_future<double> const& f) { return f.get() + 2.0; });
+    long polls = 0;
+    while (!c1.is_ready()) ++polls;  // armed: the completion engine readies it
+    HPX_TEST_EQ(c1.get(), 2.0 * double(n) + 1.0);
+    HPX_TEST_EQ(c2.get(), 2.0 * double(n) + 2.0);
+    HPX_TEST(shared.is_ready());
+    std::cout << "  is_ready() polls until the armed continuation ran: " << polls << std::endl;
+
+    auto df = hpx::dataflow(hpx::util::unwrapping([](double x, double y) { return x * y; }),
+                            hpx::parallel::reduce(pol, a.begin(), a.end(), 0.0),
+                            hpx::parallel::reduce(pol, b.begin(), b.end(), 0.0));
+    HPX_TEST_EQ(df.get(), double(n) * 2.0 * double(n));
+
+    hpx::future<double> failing = hpx::parallel::reduce(pol, a.begin(), a.end(), 0.0);
+    HPX_TEST_EQ(hpxhip_debug_inject_event_error(709 /* hipErrorContextIsDestroyed */, 1), 0);
+    int caught = 0;
+    for (int k = 0; k < 2; ++k) {
+        try {
+            (void)failing.get();
+        } catch (hpx::exception_list const& e) {
+            caught += e.status == 709 ? 1 : 0;
+        }
+    }
+    HPX_TEST_EQ(hpxhip_debug_inject_event_error(0, 0), 0);
+    HPX_TEST_EQ(caught, 2);
+    // the stream and the pools still work afterwards
+    HPX_TEST_EQ(hpx::parallel::reduce(pol, a.begin(), a.end(), 1.0).get(), double(n) + 1.0);
+}
+
 void test_errors() {
     hpx::compute::hip::target t;
     hpx::compute::hip::allocator<float> alloc(t);
@@ -218,6 +284,7 @@ int hpx_main(int argc, char* argv[]) {
     std::uniform_int_distribution<> dis(2, 101);
 
     test_proxy_outlives_iterator();
+    test_completion_paths();
     for (int N : {100, 10007, 1 << 20}) {
         std::vector<int> h_A(N), h_B(N);
         std::iota(h_A.begin(), h_A.end(), dis(gen));

@@ -166,6 +166,8 @@ int hpx_main(int, char**) {
         test_transform_copy(pol);
     }
     test_fp_segment_order(hip::target_layout(targets[0], 3));
+    // every cross-stream hand-off (carries, halos) was ordered on the device
+    HPX_TEST_EQ(hip::detail::stream_order_host_waits().load(), 0ul);
     return hpx::finalize();
 }
 

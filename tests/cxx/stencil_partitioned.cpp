@@ -14,6 +14,7 @@
 #include <hpx/parallel/heat_solver.hpp>
 #include <hpx/util/lightweight_test.hpp>
 
+#include <chrono>
 #include <cstdint>
 #include <iostream>
 #include <random>
@@ -62,6 +63,22 @@ void run(std::size_t nx, std::size_t nt, hip::target_distribution_policy const& 
                   << (random_init ? " random" : " ramp") << ": " << bad << " points differ" << std::endl;
 }
 
+// Wall time per fused pass with many small partitions on one device, where
+// the hand-offs between passes, not the kernels, set the pace (r05: marks
+// waited for on the device; r04 synchronised every stream between passes).
+void pass_timing(std::vector<hip::target> const& targets) {
+    for (std::size_t np : {7, 64}) {
+        hip::heat_solver hs(np * 4096, hip::target_layout(targets[0], np));
+        hs.do_work(16);
+        const std::size_t passes = 200;
+        const auto t0 = std::chrono::steady_clock::now();
+        hs.do_work(16 * passes);
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        std::cout << "  pass timing: " << np << " partitions x 4096 points, 16 steps per pass: " << us / passes
+                  << " us per pass" << std::endl;
+    }
+}
+
 int hpx_main(int, char**) {
     const auto targets = hip::get_local_targets();
     for (bool rnd : {false, true})
@@ -72,6 +89,9 @@ int hpx_main(int, char**) {
             run(90, nt, hip::target_layout(targets, 9), rnd);  // 10-point partitions: passes of <= 10 steps
         }
     run(1, 5, hip::target_layout, true);  // a ring of one point
+    pass_timing(targets);
+    // every cross-stream hand-off (carries, halos) was ordered on the device
+    HPX_TEST_EQ(hip::detail::stream_order_host_waits().load(), 0ul);
     return hpx::finalize();
 }
 

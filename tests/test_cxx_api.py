@@ -94,6 +94,8 @@ void f(hpx::compute::vector<int>& a) {
     ("stencil_partitioned", []),
     ("call_overhead", []),
     ("exception_list", []),
+    ("dataflow_stencil", []),
+    ("futures", []),
 ])
 def test_cxx_program(prog, args):
     exe = os.path.join(BIN, prog)
@@ -103,6 +105,19 @@ def test_cxx_program(prog, args):
     print(r.stdout[-4000:])
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert f"{prog}: all tests passed" in r.stdout
+
+
+def test_futures_compose_on_host():
+    """hpx::future / shared_future / dataflow / unwrapping / when_all /
+    wait_all / sliding_semaphore on host values (the restated lcos unit
+    tests, tests/cxx/futures.cpp): no device work, so it runs without a GPU;
+    the completion engine's thread runs the continuations."""
+    exe = os.path.join(BIN, "futures")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", ROOT, "tests/cxx/bin/futures"], check=True, capture_output=True, timeout=600)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "futures: all tests passed" in r.stdout
 
 
 def test_par_unseq_error_terminates():
