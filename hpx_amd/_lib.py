@@ -109,6 +109,7 @@ SIGNATURES = {
     "hpxhip_abi_version": [],
     "hpxhip_debug_inject_error": [_i, _i],
     "hpxhip_debug_raise_device_error": [ctypes.c_void_p, ctypes.c_uint32],
+    "hpxhip_debug_inject_event_error": [_i, _i],
     "hpxhip_device_error": [_i, ctypes.POINTER(ctypes.c_uint32)],
     "hpxhip_get_device_count": [ctypes.POINTER(_i)],
     "hpxhip_set_device": [_i],
@@ -123,6 +124,8 @@ SIGNATURES = {
     "hpxhip_stream_query": [_vp],
     "hpxhip_stream_add_callback": [_vp, CALLBACK, _vp],
     "hpxhip_event_create": [ctypes.POINTER(_vp)],
+    "hpxhip_event_create_on": [_i, _i, ctypes.POINTER(_vp)],
+    "hpxhip_stream_device": [_vp, ctypes.POINTER(_i)],
     "hpxhip_event_destroy": [_vp],
     "hpxhip_event_record": [_vp, _vp],
     "hpxhip_event_synchronize": [_vp],

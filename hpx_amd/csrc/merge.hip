@@ -66,10 +66,10 @@ int run_merge(const void* a, uint64_t na, const void* b, uint64_t nb, void* out,
                           reinterpret_cast<uintptr_t>(out)) % 16 == 0;
     if (aligned)
         hipLaunchKernelGGL((k_merge<U, C, true>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads), 0, s, ua, na, ub,
-                           nb, splits, C{}, static_cast<U*>(out));
+                           nb, splits, C{}, static_cast<U*>(out), device_error_word(s));
     else
         hipLaunchKernelGGL((k_merge<U, C, false>), dim3(static_cast<unsigned>(ntiles)), dim3(kThreads), 0, s, ua, na,
-                           ub, nb, splits, C{}, static_cast<U*>(out));
+                           ub, nb, splits, C{}, static_cast<U*>(out), device_error_word(s));
     HPXHIP_CHECK_LAUNCH();
     return 0;
 }

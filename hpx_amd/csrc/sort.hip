@@ -74,10 +74,13 @@ constexpr uint64_t kTileChunk = 256;
 
 struct sort_layout {
     uint64_t ntiles;
-    size_t alt_keys, alt_vals, hist, xhist, thist, bits, start, xstart, tstart, bounds, ctl, counter, lb, lb_bytes,
-        tcount, csum, nchunks, total;
+    size_t alt_keys, alt_vals, hist, xhist, thist, joint, bits, start, xstart, tstart, bounds, ctl, counter, lb,
+        lb_bytes, tcount, csum, nchunks, segs, big, shist, sstart, segs2, bs2, total;
     bool wide;  // 64-bit granules
 };
+
+bool takes_pre18(uint64_t n, size_t vsize, int tile);
+constexpr uint64_t kHybridMin = 1ull << 22;
 
 sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     sort_layout L;
@@ -94,6 +97,8 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     off += kXBins * 8;
     L.thist = off;  // the top 9 bits' histogram (18-bit form)
     off += kXBins * 8;
+    L.joint = off;  // ... per field region (8 x 512, k_hist_tiles; zeroed with the histograms)
+    off += 8 * kXBins * 8;
     L.bits = off;  // OR / AND of the ordered keys
     off += 256;
     L.start = off;
@@ -109,15 +114,35 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     L.counter = off;  // counter (16 B) immediately followed by lb: one zero fill per pass
     off += 256;
     L.lb = off;
-    L.lb_bytes = L.ntiles * kXBins * (L.wide ? 8 : 4);  // room for a 9-bit pass
+    // room for a 9-bit pass, and for the tiles of a segmented one (each
+    // segment rounds its tiles up)
+    L.lb_bytes = (L.ntiles + kMaxBig) * kXBins * (L.wide ? 8 : 4);
     off = align_up(off + L.lb_bytes, 256);
-    // 18-bit form, keys only: per-tile field counts -> offsets of the first
-    // prefix pass, and the chunk totals (k_hist_tiles)
-    L.nchunks = vsize ? 0 : (L.ntiles + kTileChunk - 1) / kTileChunk;
+    // 18-bit form, keys only, n < 2^32: per-tile field counts -> offsets of
+    // the first prefix pass, and the chunk totals (k_hist_tiles); reserved
+    // only when the sort takes that pass (2 KiB per 8192-key tile)
+    const bool pre = takes_pre18(n, vsize, tile);
+    L.nchunks = pre ? (L.ntiles + kTileChunk - 1) / kTileChunk : 0;
     L.tcount = off;
-    off = align_up(off + (vsize ? 0 : L.ntiles * kXBins * 4), 256);
+    off = align_up(off + (pre ? L.ntiles * kXBins * 4 : 0), 256);
     L.csum = off;
     off = align_up(off + L.nchunks * kXBins * 4, 256);
+    // hybrid-sized sorts: the segmented LSD's table, the oversized bucket
+    // ids, and per segment every digit's histogram and bin starts
+    const bool hybrid = n >= kHybridMin;
+    L.segs = off;
+    off = align_up(off + (hybrid ? sizeof(seg_table) : 0), 256);
+    L.big = off;
+    off = align_up(off + (hybrid ? 4 * (kMaxBig + 1) : 0), 256);
+    L.shist = off;
+    off = align_up(off + (hybrid ? 8ull * kMaxBig * 8 * kRadix : 0), 256);
+    L.sstart = off;
+    off = align_up(off + (hybrid ? 8ull * kMaxBig * 8 * kRadix : 0), 256);
+    // 18-bit form: the second prefix pass's 8 field regions and their bin starts
+    L.segs2 = off;
+    off = align_up(off + (pre ? sizeof(seg_table) : 0), 256);
+    L.bs2 = off;
+    off = align_up(off + (pre ? 8 * kXBins * 8 : 0), 256);
     L.total = off;
     return L;
 }
@@ -158,7 +183,6 @@ template <typename U>
 constexpr int field18_shift() { return static_cast<int>(8 * sizeof(U)) - 18; }
 template <typename U>
 constexpr int top9_shift() { return static_cast<int>(8 * sizeof(U)) - 9; }
-constexpr uint64_t kHybridMin = 1ull << 22;
 
 // Default form (r04): the 18-bit form -- 2^30 u64 17.81 vs 18.42 ms for the
 // 17-bit form, u32 12.84 vs 13.03, u32 2^28 3.39 vs 3.68
@@ -169,6 +193,12 @@ int hybrid_mode() {
     const char* e = std::getenv("HPXHIP_SORT_HYBRID");
     if (!e) return 18;
     return std::atoi(e);
+}
+
+// The 18-bit form's first prefix pass from precomputed tile offsets: keys
+// only, n < 2^32 (32-bit offsets), 8192-key tiles, and a hybrid-sized sort
+bool takes_pre18(uint64_t n, size_t vsize, int tile) {
+    return vsize == 0 && n >= kHybridMin && n < (uint64_t(1) << 32) && tile == 8192 && hybrid_mode() == 18;
 }
 
 // ---------------------------------------------------------------- the plan
@@ -188,7 +218,7 @@ enum : int {
     C_SEGB = 19,       // {on, nb, top_single}: 1024-thread segment sort (keys, buckets over 9216)
     C_OVERSIZED = 22,  // raised by a segment sort: a bucket over its LDS capacity
     C_HIST_A = 23,     // count digits [0, first) before the prefix passes
-    C_HIST_B = 24,     // ... after a hybrid that fell back to the LSD
+    C_HIST_B = 24,     // ... after a hybrid whose oversized buckets send the whole array to the LSD
     C_COPY = 25,       // the LSD ended in the alternate buffer: copy back
     C_PENDING = 26,    // stage 0 needs the second live byte's histogram to decide
     C_NLSD = 27,       // live digits
@@ -196,7 +226,9 @@ enum : int {
     C_FIRST = 36,      // the first histogram counted digits [first, passes)
     C_B9 = 37,         // shift of the top-9-bit prefix pass (18-bit form), -1
     C_SEGC = 38,       // {on, nb, top_single}: 512 x 9 segment sort (18-bit form)
-    C_WORDS = 44
+    C_SEGLSD = 44,     // hybrid-sized sorts: the LSD passes run over the segment table
+    C_SEGHIST = 45,    // ... whose histograms are counted first (the oversized-bucket finish)
+    C_WORDS = 46
 };
 static_assert(C_WORDS * 4 <= 256, "plan words fit their slot");
 
@@ -221,11 +253,77 @@ __device__ inline int top_bit_d(uint64_t x) { return x ? 64 - __builtin_clzll(x)
 //     on the two top live bytes, b2 <= 8, a 512-thread (keys) / pairs
 //     segment, or the 1024-thread keys segment for b2 = 8 buckets over 9216;
 //   otherwise the LSD over the live digits.
+// One segment covering the whole array (the segmented LSD as a plain LSD).
+__device__ inline void whole_array(seg_table* segs, uint64_t n, int tile) {
+    segs->nseg = 1;
+    segs->start[0] = 0;
+    segs->len[0] = n;
+    segs->tile0[0] = 0;
+    segs->tile0[1] = (n + tile - 1) / tile;
+}
+
 __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const unsigned long long* __restrict__ xhist,
                             const unsigned long long* __restrict__ thist,
                             const unsigned long long* __restrict__ bits, uint64_t n, int passes, int first, int mode,
-                            int has_val, int stage, int32_t* __restrict__ ctl) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+                            int has_val, int stage, int32_t* __restrict__ ctl, seg_table* __restrict__ segs = nullptr,
+                            uint32_t* __restrict__ big = nullptr, int tile = 0) {
+    if (blockIdx.x != 0) return;
+    // 18-bit form: the statistics of the two 9-bit histograms, by the 64
+    // threads of the launch (r05; one thread reading 9 x 512 bins took ~0.1
+    // ms per plan): the largest top-9 bin; per field width b2 the largest
+    // group of 2^(9-b2) field bins (all, and those without a hot bin); the
+    // hot bins (over twice the mean) of both and their excess keys
+    __shared__ double s_mtop, s_mt, s_et, s_ef, s_mg[10], s_mgn[10];
+    __shared__ int s_ht, s_hf;
+    if (mode == 18 && !has_val && stage == 0 && thist) {
+        const int t = threadIdx.x;
+        const double mean = static_cast<double>(n) / kXBins;
+        double mtop = 0, mt = mean, et = 0, ef = 0;
+        int ht = 0, hf = 0;
+        for (int i = t; i < kXBins; i += 64) {
+            const double a = static_cast<double>(thist[i]), b = static_cast<double>(xhist[i]);
+            mtop = a > mtop ? a : mtop;
+            if (a > 2 * mean) ++ht, et += a - mean;
+            else mt = a > mt ? a : mt;
+            if (b > 2 * mean) ++hf, ef += b - mean;
+        }
+        double mg[10], mgn[10];
+        for (int b2 = 1; b2 <= 9; ++b2) {
+            const int g = 1 << (9 - b2);
+            mg[b2] = 0;
+            mgn[b2] = 0;
+            for (int i = t * g; i < kXBins; i += 64 * g) {
+                double sum = 0;
+                bool hot = false;
+                for (int k = 0; k < g; ++k) {
+                    const double b = static_cast<double>(xhist[i + k]);
+                    sum += b;
+                    hot = hot || b > 2 * mean;
+                }
+                mg[b2] = sum > mg[b2] ? sum : mg[b2];
+                if (!hot) mgn[b2] = sum > mgn[b2] ? sum : mgn[b2];
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            auto mx = [](double a, double b) { return a > b ? a : b; };
+            mtop = mx(mtop, __shfl_xor(mtop, o));
+            mt = mx(mt, __shfl_xor(mt, o));
+            et += __shfl_xor(et, o);
+            ef += __shfl_xor(ef, o);
+            ht += __shfl_xor(ht, o);
+            hf += __shfl_xor(hf, o);
+            for (int b2 = 1; b2 <= 9; ++b2) {
+                mg[b2] = mx(mg[b2], __shfl_xor(mg[b2], o));
+                mgn[b2] = mx(mgn[b2], __shfl_xor(mgn[b2], o));
+            }
+        }
+        if (t == 0) {
+            s_mtop = mtop, s_mt = mt, s_et = et, s_ef = ef, s_ht = ht, s_hf = hf;
+            for (int b2 = 1; b2 <= 9; ++b2) s_mg[b2] = mg[b2], s_mgn[b2] = mgn[b2];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
     if (stage == 1) {
         if (!ctl[C_PENDING]) return;
         first = 0;  // every digit is counted now
@@ -234,6 +332,7 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
         for (int i = 0; i < 11; ++i) ctl[i] = -1;
         ctl[C_B9] = -1;
         ctl[C_FIRST] = first;
+        if (big) big[0] = 0;
     }
     ctl[C_PENDING] = 0;
     const uint64_t diff = bits[0] ^ bits[1];
@@ -246,6 +345,10 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
         for (int i = 0; i < nl; ++i) ctl[C_LSD + i] = 8 * live[nl - 1 - i];
         ctl[C_COPY] = nl & 1;
         if (stage == 0) ctl[C_HIST_A] = first > 0;
+        if (segs) {  // a hybrid-sized sort: its LSD runs as a one-segment segmented LSD
+            whole_array(segs, n, tile);
+            ctl[C_SEGLSD] = 1;
+        }
     };
     if (mode == 0 || nl < 3) return lsd();
     const double dn = static_cast<double>(n);
@@ -272,14 +375,32 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
     const bool top_two = live[0] == passes - 1 && live[1] == passes - 2;
     if (mode == 18 && !has_val && stage == 0 && top_two) {
         // top 9 bits [8P - 9, 8P), field [8P - 18, 8P - 9): b2 <= 9 bits of the field
-        const double m_top = bin_max(thist, kXBins, 1);
         const int fs = 8 * passes - 18;
         for (int b2 = 1; b2 <= 9; ++b2)
-            if (fits(m_top * bin_max(xhist, kXBins, 1 << (9 - b2)) / dn, kCap18)) {
+            if (fits(s_mtop * s_mg[b2] / dn, kCap18)) {
                 ctl[C_A9] = fs;
                 ctl[C_B9] = 8 * passes - 9;
                 return plan(8 * passes - 9, fs + 9 - b2, b2, C_SEGC, 9);
             }
+        // r05: skew concentrated in a few buckets -- a few hot top-9 bins
+        // whose excess keys sit in a few hot field bins (the same keys: the
+        // excess masses match) -- is left to the bounded finish of the
+        // oversized buckets (at most kMaxBig of them, k_sort_fallback) when
+        // every bucket outside the hot bins fits: buckets sized for the keys
+        // outside the hot bins (the fewest field bits whose groups without a
+        // hot bin fit) are planned instead of the whole-array LSD (VERDICT
+        // r04: one hot prefix had cost 2.5x the uniform sort).
+        if (s_ht > 0 && s_hf > 0 && s_ht * s_hf <= kMaxBig && s_et <= 1.25 * s_ef && s_ef <= 1.25 * s_et) {
+            const double mean = dn / kXBins;
+            for (int b2 = 1; b2 <= 9; ++b2) {
+                const double g = static_cast<double>(1 << (9 - b2)) * mean;
+                if (fits(s_mt * (s_mgn[b2] > g ? s_mgn[b2] : g) / dn, kCap18)) {
+                    ctl[C_A9] = fs;
+                    ctl[C_B9] = 8 * passes - 9;
+                    return plan(8 * passes - 9, fs + 9 - b2, b2, C_SEGC, 9);
+                }
+            }
+        }
     }
     if (mode == 17 && !has_val && first > 0 && top_two) {
         const double m_top = bin_max(hist + live[0] * kRadix, kRadix, 1);
@@ -314,16 +435,49 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
     lsd();
 }
 
-// After the segment sorts: a bucket over its LDS capacity (skewed keys) left
-// its keys unsorted -- the plan switches to the LSD over every live digit,
-// which sorts the prefix-ordered array from where it is (a permutation of
-// the input: same digit counts).
-__global__ void k_sort_fallback(int32_t* __restrict__ ctl) {
+// After the segment sorts: buckets over their LDS capacity (skewed keys)
+// were left unsorted.  Up to kMaxBig of them (the whole-array
+// LSD for one oversized bucket cost 2.5-2.9x) are finished by a segmented
+// LSD over their own ranges and the live digits under the bucket prefix
+// (the keys of a bucket agree on every bit at or above s2); more send the
+// whole array through the LSD over every live digit (a one-segment table).
+// Either way the passes count their segments' histograms first.
+__global__ void k_sort_fallback(int32_t* __restrict__ ctl, const uint64_t* __restrict__ bounds,
+                                const uint32_t* __restrict__ big, seg_table* __restrict__ segs, uint64_t n,
+                                int tile) {
     if (threadIdx.x != 0 || blockIdx.x != 0 || ctl[C_OVERSIZED] == 0) return;
     const int nl = ctl[C_NLSD];
-    for (int i = 0; i < nl; ++i) ctl[C_LSD + i] = 8 * ctl[C_DIGITS + i];
-    ctl[C_COPY] = nl & 1;
-    ctl[C_HIST_B] = ctl[C_FIRST] > 0 && !ctl[C_HIST_A];
+    const uint32_t nbig = big[0];
+    int np = 0;
+    if (nbig <= static_cast<uint32_t>(kMaxBig)) {
+        uint32_t ids[kMaxBig];
+        for (uint32_t i = 0; i < nbig; ++i) {  // the recorded buckets, in address order
+            uint32_t v = big[1 + i], k = i;
+            for (; k > 0 && ids[k - 1] > v; --k) ids[k] = ids[k - 1];
+            ids[k] = v;
+        }
+        segs->nseg = nbig;
+        uint64_t t = 0;
+        for (uint32_t j = 0; j < nbig; ++j) {
+            segs->start[j] = bounds[ids[j]];
+            segs->len[j] = bounds[ids[j] + 1] - bounds[ids[j]];
+            segs->tile0[j] = t;
+            t += (segs->len[j] + tile - 1) / tile;
+        }
+        segs->tile0[nbig] = t;
+        const int s2 = ctl[C_BOUNDS + 3];
+        for (int i = 0; i < nl; ++i)
+            if (8 * ctl[C_DIGITS + i] < s2) ctl[C_LSD + np++] = 8 * ctl[C_DIGITS + i];
+        ctl[C_SEGHIST] = np > 0;  // their histograms: k_seg_hist over just their keys
+    } else {
+        // the whole array: its histograms from the optimized count (k_hist),
+        // of the digits the first count skipped
+        whole_array(segs, n, tile);
+        for (int i = 0; i < nl; ++i) ctl[C_LSD + np++] = 8 * ctl[C_DIGITS + i];
+        ctl[C_HIST_B] = ctl[C_FIRST] > 0 && !ctl[C_HIST_A];
+    }
+    ctl[C_COPY] = np & 1;
+    ctl[C_SEGLSD] = np > 0;
 }
 
 // Zero fill of a pass's look-back state, run iff *gate >= 0 (the pass runs).
@@ -451,8 +605,11 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             // the pass ran 8.4 ms against 5.1 (profiles/r04_sort_pre_blockidx.txt)
             // -- the order in which tiles finish decides how the partial
             // lines at the ends of their digit runs meet in the caches
+            // r05: tiles in 8 contiguous regions, one per XCD (XREG): 4.75 ->
+            // 3.81 ms at 2^30 u64 (profiles/r05_ubench_sortpass5.log)
             if constexpr (!HAS_VAL)
-                hipLaunchKernelGGL((k_onesweep<U, VAL, false, uint32_t, X, TS::threads, TS::items, -1, 9, true, true>),
+                hipLaunchKernelGGL((k_onesweep<U, VAL, false, uint32_t, X, TS::threads, TS::items, -1, 9, true, false,
+                                               false, false, true>),
                                    grid, block, 0, s, kin, kout, vin, vout, n, 0, b9,
                                    reinterpret_cast<uint32_t*>(base + L.lb), counter, err, X{}, word, nt, pre);
         } else if (rb == 9) {
@@ -469,20 +626,21 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     };
 
     // ---- first histogram (+ OR / AND of the keys) and the plan
-    HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8 + 2 * kXBins * 8, s));  // hist, xhist, thist
+    HPXHIP_CHECK(hipMemsetAsync(hist, 0, 8 * kRadix * 8 + 10 * kXBins * 8, s));  // hist, xhist, thist, joint
     HPXHIP_CHECK(hipMemsetAsync(bits, 0, 8, s));
     HPXHIP_CHECK(hipMemsetAsync(bits + 1, 0xff, 8, s));
     // 18-bit form, keys, n < 2^32: the first count also leaves the field's
     // per-tile counts for the first prefix pass (k_hist_tiles)
     // (same-box A/B, profiles/r04_sort_ab_pre_offsets.log: 2^30 u64 17.99-18.05
     // -> 17.58-17.68 ms, u32 13.17-13.26 -> 12.55-12.62 against the look-back pass)
-    const bool pre18 = mode == 18 && !HAS_VAL && n < (uint64_t(1) << 32) && TS::tile == 8192;
+    const bool pre18 = takes_pre18(n, HAS_VAL ? sizeof(VAL) : 0, TS::tile);
     auto* tcount = reinterpret_cast<uint32_t*>(base + L.tcount);
     auto* csum = reinterpret_cast<uint32_t*>(base + L.csum);
     if (pre18)
         hipLaunchKernelGGL((k_hist_tiles<U, X, 8192, kXBins>), dim3(static_cast<unsigned>(L.nchunks)), dim3(kXBins), 0,
                            s, kc, n, L.ntiles, static_cast<uint32_t>(kTileChunk), X{}, field18_shift<U>(),
-                           top9_shift<U>(), tcount, csum, xhist, thist, bits);
+                           top9_shift<U>(), tcount, csum, xhist, thist, bits,
+                           reinterpret_cast<unsigned long long*>(base + L.joint));
     else if (mode == 18)  // the field and the top 9 bits; no byte digit
         hipLaunchKernelGGL((k_hist<U, X, kHistThreads, 4, 2, true>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n,
                            first, passes, X{}, hist, bits, field18_shift<U>(), xhist,
@@ -501,13 +659,24 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         hipLaunchKernelGGL(k_bin_offsets<kXBins>, dim3(1), dim3(kXBins), 0, s, thist, tstart);
         HPXHIP_CHECK_LAUNCH();
     }
+    if (pre18) {  // the second prefix pass's field regions
+        hipLaunchKernelGGL(k_region_plan, dim3(1), dim3(kXBins), 0, s, xstart, tstart,
+                           reinterpret_cast<const unsigned long long*>(base + L.joint), n, TS::tile,
+                           reinterpret_cast<seg_table*>(base + L.segs2),
+                           reinterpret_cast<unsigned long long*>(base + L.bs2));
+        HPXHIP_CHECK_LAUNCH();
+    }
+    // hybrid-sized sorts: the LSD runs over the segment table (the whole
+    // array, or the oversized buckets the segment sorts leave)
+    auto* segs = mode ? reinterpret_cast<seg_table*>(base + L.segs) : nullptr;
+    auto* big = mode ? reinterpret_cast<uint32_t*>(base + L.big) : nullptr;
     hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, thist, bits, n, passes, first, mode,
-                       HAS_VAL ? 1 : 0, 0, ctl);
+                       HAS_VAL ? 1 : 0, 0, ctl, segs, big, TS::tile);
     HPXHIP_CHECK_LAUNCH();
     if (first > 0) {
         if ((rc = count_rest(ctl + C_HIST_A))) return rc;
         hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, thist, bits, n, passes, first, mode,
-                           HAS_VAL ? 1 : 0, 1, ctl);
+                           HAS_VAL ? 1 : 0, 1, ctl, segs, big, TS::tile);
         HPXHIP_CHECK_LAUNCH();
     }
 
@@ -528,7 +697,35 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         // 17-bit forms, the top-9-bit pass in the 18-bit form
         if ((rc = pass(kc, ka, vc, va, 8, ctl + C_A8, mode >= 17))) return rc;
         if ((rc = pass(ka, kc, va, vc, 8, ctl + C_B, mode == 18))) return rc;
-        if (!HAS_VAL && mode == 18 && (rc = pass(ka, kc, nullptr, nullptr, 9, ctl + C_B9, false, tstart))) return rc;
+        if constexpr (!HAS_VAL) {
+            if (mode == 18 && pre18) {
+                // r05: the top-9 pass over the field-ordered keys in 8 field
+                // regions, one per XCD, each with its own look-back and bin
+                // starts (k_region_plan): consecutive tiles' digit runs meet in
+                // one L2, as in the first pass (XREG + SEG)
+                const uint64_t nt = L.ntiles + 8;
+                const uint64_t zbytes = align_up(256 + nt * kXBins * (L.wide ? 8 : 4), 16);
+                hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
+                                   reinterpret_cast<uint4*>(counter), zbytes / 16, ctl + C_B9);
+                HPXHIP_CHECK_LAUNCH();
+                auto launch = [&](auto gtag) {
+                    using G = decltype(gtag);
+                    hipLaunchKernelGGL((k_onesweep<U, VAL, false, G, X, TS::threads, TS::items, TS::lbb, 9, true, false,
+                                                   false, true, true>),
+                                       dim3(static_cast<unsigned>(nt)), dim3(TS::threads), 0, s, ka, kc,
+                                       static_cast<const VAL*>(nullptr), static_cast<VAL*>(nullptr), n, 0,
+                                       reinterpret_cast<const unsigned long long*>(base + L.bs2),
+                                       reinterpret_cast<G*>(base + L.lb), counter, err, X{}, ctl + C_B9, nt,
+                                       static_cast<const uint32_t*>(nullptr),
+                                       reinterpret_cast<const seg_table*>(base + L.segs2));
+                };
+                if (L.wide) launch((unsigned long long)0);
+                else launch(uint32_t(0));
+                HPXHIP_CHECK_LAUNCH();
+            } else if (mode == 18 && (rc = pass(ka, kc, nullptr, nullptr, 9, ctl + C_B9, false, tstart))) {
+                return rc;
+            }
+        }
         hipLaunchKernelGGL((k_bucket_bounds<U, X>), dim3((kMaxBuckets + 1 + 255) / 256), dim3(256), 0, s, kc, n, 0, 0,
                            0, 0u, X{}, bounds, ctl + C_BOUNDS);
         HPXHIP_CHECK_LAUNCH();
@@ -552,12 +749,12 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         if constexpr (HAS_VAL) {
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true, true>),
                                dim3(g0), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, vc, oversized,
-                               ctl + C_SEGA, 0u);
+                               ctl + C_SEGA, 0u, big);
             HPXHIP_CHECK_LAUNCH();
             if (g0 < kMax17)
                 hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true, true, true>),
                                    dim3(cus), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, vc, oversized,
-                                   ctl + C_SEGA, g0);
+                                   ctl + C_SEGA, g0, big);
         } else if (mode == 18) {
             // the 18-bit form's ~4096-key buckets: one workgroup per expected
             // bucket, then a striding grid; the 512 x 18 segment (a plan that
@@ -566,46 +763,90 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             const uint32_t g18 = static_cast<uint32_t>(want18 > kMaxBuckets ? kMaxBuckets : want18);
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true>),
                                dim3(g18), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
-                               ctl + C_SEGC, 0u);
+                               ctl + C_SEGC, 0u, big);
             HPXHIP_CHECK_LAUNCH();
             if (g18 < kMaxBuckets)
                 hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true, true>),
                                    dim3(3 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
-                                   oversized, ctl + C_SEGC, g18);
+                                   oversized, ctl + C_SEGC, g18, big);
             HPXHIP_CHECK_LAUNCH();
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true, true>),
                                dim3(2 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
-                               oversized, ctl + C_SEGA, 0u);
+                               oversized, ctl + C_SEGA, 0u, big);
             HPXHIP_CHECK_LAUNCH();
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItems, 16, uint32_t, false, true, true>),
                                dim3(cus), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, nullptr,
-                               oversized, ctl + C_SEGB, 0u);
+                               oversized, ctl + C_SEGB, 0u, big);
         } else {
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true>),
                                dim3(g0), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
-                               ctl + C_SEGA, 0u);
+                               ctl + C_SEGA, 0u, big);
             HPXHIP_CHECK_LAUNCH();
             if (g0 < kMax17)
                 hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true, true>),
                                    dim3(2 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
-                                   oversized, ctl + C_SEGA, g0);
+                                   oversized, ctl + C_SEGA, g0, big);
             HPXHIP_CHECK_LAUNCH();
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItems, 16, uint32_t, false, true, true>),
                                dim3(cus), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, nullptr,
-                               oversized, ctl + C_SEGB, 0u);
+                               oversized, ctl + C_SEGB, 0u, big);
         }
         HPXHIP_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_sort_fallback, dim3(1), dim3(64), 0, s, ctl);
+        hipLaunchKernelGGL(k_sort_fallback, dim3(1), dim3(64), 0, s, ctl, bounds, big, segs, n, TS::tile);
         HPXHIP_CHECK_LAUNCH();
         if (first > 0 && (rc = count_rest(ctl + C_HIST_B))) return rc;
     }
 
-    // ---- LSD over the live digits (keys <-> alt), when planned: the plan of
-    // a small sort (mode 0) or the fallback of a hybrid-sized one (persistent
-    // grids: usually skipped)
+    if (mode) {
+        // ---- a hybrid-sized sort's LSD (usually skipped): the planned LSD of
+        // keys the hybrid does not fit (one segment: the whole array, bin
+        // starts from the global histogram) or the oversized-bucket finish
+        // (the recorded buckets, their histograms counted here).  Persistent
+        // grids, every launch gated by the plan.
+        auto* shist = reinterpret_cast<unsigned long long*>(base + L.shist);
+        auto* sstart = reinterpret_cast<unsigned long long*>(base + L.sstart);
+        const unsigned cus = static_cast<unsigned>(current_device_info().cus);
+        HPXHIP_CHECK(hipMemsetAsync(shist, 0, 8ull * kMaxBig * 8 * kRadix, s));
+        hipLaunchKernelGGL((k_seg_hist<U, X, 256, TS::tile>), dim3(2 * cus), dim3(256), 0, s, kc, segs, X{}, shist,
+                           ctl + C_SEGHIST);
+        HPXHIP_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_seg_offsets, dim3(kMaxBig * 8), dim3(kRadix), 0, s, shist, segs, sstart, ctl + C_SEGLSD,
+                           ctl + C_SEGHIST, static_cast<const unsigned long long*>(hist));
+        HPXHIP_CHECK_LAUNCH();
+        const uint64_t nt = L.ntiles + kMaxBig;  // the segments' tiles (each segment rounds up)
+        const uint64_t zbytes = align_up(256 + nt * kRadix * (L.wide ? 8 : 4), 16);
+        for (int i = 0; i < passes; ++i) {
+            const bool even = (i & 1) == 0;
+            const int32_t* word = ctl + C_LSD + i;
+            hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
+                               reinterpret_cast<uint4*>(counter), zbytes / 16, word);
+            HPXHIP_CHECK_LAUNCH();
+            auto launch = [&](auto gtag) {
+                using G = decltype(gtag);
+                hipLaunchKernelGGL((k_onesweep<U, VAL, HAS_VAL, G, X, TS::threads, TS::items, TS::lbb, 8, true, true,
+                                               true, true>),
+                                   dim3(2 * cus), dim3(TS::threads), 0, s, even ? kc : ka, even ? ka : kc,
+                                   even ? vc : va, even ? va : vc, n, 0, sstart, reinterpret_cast<G*>(base + L.lb),
+                                   counter, err, X{}, word, uint64_t(0), static_cast<const uint32_t*>(nullptr),
+                                   static_cast<const seg_table*>(segs));
+            };
+            if (L.wide) launch((unsigned long long)0);
+            else launch(uint32_t(0));
+            HPXHIP_CHECK_LAUNCH();
+        }
+        hipLaunchKernelGGL((k_seg_copy<U>), dim3(grid_for(n)), dim3(256), 0, s, ka, kc, segs, ctl + C_COPY);
+        HPXHIP_CHECK_LAUNCH();
+        if constexpr (HAS_VAL) {
+            hipLaunchKernelGGL((k_seg_copy<VAL>), dim3(grid_for(n)), dim3(256), 0, s, va, vc, segs, ctl + C_COPY);
+            HPXHIP_CHECK_LAUNCH();
+        }
+        return 0;
+    }
+
+    // ---- LSD over the live digits (keys <-> alt): the plan of a small sort
     for (int i = 0; i < passes; ++i) {
         const bool even = (i & 1) == 0;
-        if ((rc = pass(even ? kc : ka, even ? ka : kc, even ? vc : va, even ? va : vc, 8, ctl + C_LSD + i, mode != 0)))
+        if ((rc = pass(even ? kc : ka, even ? ka : kc, even ? vc : va, even ? va : vc, 8, ctl + C_LSD + i, false)))
             return rc;
     }
     hipLaunchKernelGGL((k_copy_gated<U>), dim3(grid_for(n)), dim3(256), 0, s, ka, kc, n, ctl + C_COPY);

@@ -128,6 +128,9 @@ class LocalComm:
     def allgather_host(self, words):
         return np.ascontiguousarray(words, np.int64).reshape(1, -1)
 
+    def allreduce_host(self, words):
+        return np.ascontiguousarray(words, np.int64).copy()
+
     def slots(self, nbytes: int):
         """(send_ptr, recv_ptr) device buffers for one all-gather."""
         words = max(64, -(-int(nbytes) // 8))
@@ -296,6 +299,13 @@ class TorchComm:
         self.dist.all_gather_into_tensor(out, w)
         return out.cpu().numpy().reshape(self.size, -1)
 
+    def allreduce_host(self, words):
+        """Host-level sum over ranks of int64 words (one all-reduce)."""
+        torch = self.torch
+        w = torch.as_tensor(np.ascontiguousarray(words, np.int64), device=self.device).clone()
+        self.dist.all_reduce(w)
+        return w.cpu().numpy()
+
     def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream, recv_off=0):
         """All-to-all with uneven splits: send_counts[j] elements from
         send_buf[send_off:] go to rank j (in rank order); recv_counts[i]
@@ -393,6 +403,17 @@ class HipEngine:
         dv.free()
         dout.free()
         return out.astype(np.int64)
+
+    def read_ranges(self, vec, starts, counts):
+        """Host copies of vec[s:s+c] for each (s, c), one stream sync."""
+        npdt = np_dtype(vec.dtype)
+        out = [np.empty(int(c), npdt) for c in counts]
+        for o, st in zip(out, starts):
+            if o.size:
+                L.call("hpxhip_memcpy_async", o.ctypes.data_as(ctypes.c_void_p),
+                       ctypes.c_void_p(vec.data() + int(st) * vec.value_size), o.nbytes, L.D2H, self.stream)
+        L.call("hpxhip_stream_synchronize", self.stream)
+        return out
 
     def buffer(self, like, n):
         return vector(max(1, n), dtype=like.dtype, tgt=self.tgt)
@@ -494,6 +515,22 @@ class HipEngine:
         L.call("hpxhip_copy_if", src.dtype, pred.kind, L.scalar_buf(src.dtype, pred.arg),
                ctypes.c_void_p(src.data() + lo * src.value_size), ctypes.c_void_p(dst.data() + dlo * dst.value_size),
                hi - lo, ctypes.c_void_p(count_ptr), self.stream, None, 0)
+
+
+def _to_ordered(x, descending):
+    """The sort's key order (common.hpp ordered_bits): values -> unsigned
+    bits whose unsigned order is the sort order."""
+    x = np.asarray(x)
+    ut = np.uint64 if x.dtype.itemsize == 8 else np.uint32
+    raw = x.view(ut)
+    sign = ut(1) << ut(8 * x.dtype.itemsize - 1)
+    if x.dtype.kind == "f":
+        o = np.where(raw & sign, ~raw, raw | sign).astype(ut)
+    elif x.dtype.kind == "i":
+        o = raw ^ sign
+    else:
+        o = raw.copy()
+    return ~o if descending else o
 
 
 def _from_ordered(u, dt, descending):
@@ -838,11 +875,14 @@ class segmented:
         1. each rank radix-sorts its partition (hpxhip_sort);
         2. the p-1 partition boundaries (global ranks partition_bounds(n, p,
            j)[0]) are located exactly by a radix select over the ordered key
-           bits, 8 bits per round: every round each rank counts its keys
-           ordered before 256 candidates per boundary (hpxhip_sorted_bounds,
-           binary searches), one all-gather sums the counts;
+           bits (_sort_cuts: 16-bit digits, one all-reduce of counts per
+           round, then one all-gather of the few keys left in each
+           boundary's block): 3 host round trips for uniform 64- or 32-bit
+           keys, at most 5 (64-bit keys with long runs of equal keys);
         3. equal keys straddling a boundary are split in rank order, giving
-           each rank contiguous, key-ordered slices for every destination;
+           each rank contiguous, key-ordered slices for every destination
+           (every rank computes every rank's slices, so the receive counts
+           need no further exchange);
         4. one RCCL all-to-all with uneven splits moves the slices;
         5. the p received sorted runs are merged pairwise (hpxhip_merge,
            ceil(log2 p) rounds of 16 B/key) into the partition.
@@ -860,32 +900,7 @@ class segmented:
         p = comm.size
         if p == 1:
             return segmented_iterator(pv, pv.n)
-        bits = 8 * np_dtype(dt).itemsize
-        ut = np.uint64 if bits == 64 else np.uint32
-        targets = np.array([pv.layout.rank_bounds(j)[0] for j in range(1, p)], np.int64)
-        prefix = np.zeros(p - 1, ut)
-        digits = np.arange(256, dtype=ut)
-        for rnd in range(bits // 8):
-            shift = ut(bits - 8 * (rnd + 1))
-            cand = (prefix[:, None] | (digits[None, :] << shift)).ravel()
-            cnt = eng.bounds(pv.local, lo, hi, _from_ordered(cand, dt, desc), False, desc)
-            tot = comm.allgather_host(cnt).sum(axis=0).reshape(p - 1, 256)
-            d = (tot <= targets[:, None]).sum(axis=1) - 1          # count(< prefix|0) <= target holds
-            prefix = prefix | (d.astype(ut) << shift)
-        keys = _from_ordered(prefix, dt, desc)                        # key at each boundary's global rank
-        lt = eng.bounds(pv.local, lo, hi, keys, False, desc)
-        le = eng.bounds(pv.local, lo, hi, keys, True, desc)
-        g = comm.allgather_host(np.concatenate([lt, le - lt]))        # (p, 2(p-1))
-        LT, EQ = g[:, :p - 1], g[:, p - 1:]
-        remaining = targets - LT.sum(axis=0)                          # equal keys still owed to the left
-        before = np.cumsum(EQ, axis=0) - EQ                           # equal keys of lower ranks
-        take = np.clip(remaining[None, :] - before, 0, EQ)
-        cuts = np.concatenate([[0], (LT + take)[comm.rank], [n_loc]])
-        send = np.diff(cuts)
-        recv = comm.allgather_host(send)[:, comm.rank]
-        if int(recv.sum()) != n_loc:
-            raise RuntimeError(f"segmented sort: rank {comm.rank} receives {int(recv.sum())} keys for a "
-                               f"partition of {n_loc}")
+        send, recv = self._sort_cuts(eng, comm, pv, lo, hi, dt, desc)
         rbuf = eng.buffer(pv.local, n_loc)
         comm.alltoallv(pv.local, lo, send, rbuf, recv, np_dtype(dt).itemsize, eng.stream)
         # pairwise merge rounds, ping-pong between rbuf and the partition
@@ -909,6 +924,96 @@ class segmented:
             eng.copy(dt, src, src_base, n_loc, pv.local, lo)
         eng.release(rbuf)
         return segmented_iterator(pv, pv.n)
+
+    # digits per radix-select round, and the largest block (keys left in a
+    # boundary's candidate range, over all ranks) finished by gathering keys
+    SELECT_BITS = 16
+    SELECT_GATHER = 4096
+
+    def _sort_cuts(self, eng, comm, pv, lo, hi, dt, desc):
+        """Exact global cut of a sorted partitioned_vector (step 2-3 of sort):
+        the slice of my sorted partition each rank receives (send counts) and
+        the slice sizes every rank sends me (receive counts).
+
+        Radix select over the ordered key bits, SELECT_BITS per round: for
+        each boundary j (global rank t_j) every rank counts its keys ordered
+        before the 2^16 candidates prefix_j + d*2^shift (hpxhip_sorted_bounds,
+        binary searches on the sorted partition); one all-reduce sums them;
+        the digit d_j with count(< candidate) <= t_j < count(< next) extends
+        prefix_j.  Once every boundary's block [prefix_j, prefix_j + 2^shift)
+        holds at most SELECT_GATHER keys over all ranks (or is one key value),
+        one all-gather carries each rank's count below the block and its keys
+        in it; the host picks the key at rank t_j and every rank's count of
+        keys ordered before it (LT) and equal to it (EQ), and splits equal
+        keys across the boundary in rank order."""
+        p, me = comm.size, comm.rank
+        npdt = np_dtype(dt)
+        bits = 8 * npdt.itemsize
+        ut = np.uint64 if bits == 64 else np.uint32
+        nb = p - 1
+        n_rank = np.array([b - a for a, b in (pv.layout.rank_bounds(r) for r in range(p))], np.int64)
+        n_loc = hi - lo
+        targets = np.array([pv.layout.rank_bounds(j)[0] for j in range(1, p)], np.int64)
+        R = self.SELECT_BITS
+        D = 1 << R
+        prefix = np.zeros(nb, np.uint64)
+        g_lo = np.zeros(nb, np.int64)           # global count(< block start)
+        l_lo = np.zeros(nb, np.int64)           # my count(< block start)
+        l_hi = np.full(nb, n_loc, np.int64)     # my count(< block end)
+        n_tot = int(n_rank.sum())
+        past = targets >= n_tot                 # boundaries at the end (fewer keys than partitions)
+        block = np.where(past, 0, n_tot).astype(np.int64)
+        shift = bits
+        d = np.arange(1, D + 1, dtype=np.uint64)
+        while shift > 0 and int(block.max()) > self.SELECT_GATHER:
+            shift -= R
+            # count(<= prefix + d*2^shift - 1) = count(< prefix + d*2^shift), d = 1..D (uint64 wraps exactly)
+            probes = (prefix[:, None] + ((d[None, :] << np.uint64(shift)) - np.uint64(1))).ravel()
+            cnt = eng.bounds(pv.local, lo, hi, _from_ordered(probes.astype(ut), dt, desc), True, desc)
+            cnt = np.concatenate([l_lo[:, None], cnt.reshape(nb, D)], axis=1)          # (nb, D + 1)
+            tot = comm.allreduce_host(cnt[:, 1:].ravel()).reshape(nb, D)
+            tot = np.concatenate([g_lo[:, None], tot], axis=1)
+            dig = np.array([np.searchsorted(tot[j, :D], targets[j], side="right") - 1 for j in range(nb)],
+                           np.int64)
+            rows = np.arange(nb)
+            prefix = prefix + (dig.astype(np.uint64) << np.uint64(shift))
+            g_lo, block = tot[rows, dig], tot[rows, dig + 1] - tot[rows, dig]
+            l_lo, l_hi = cnt[rows, dig], cnt[rows, dig + 1]
+            block[past] = 0
+        # one all-gather: per boundary my count below the block, my keys in it
+        K = int(block.max()) if shift > 0 else 0
+        msg = np.zeros((nb, 2 + K), np.int64)
+        msg[:, 0] = l_lo
+        msg[:, 1] = np.where(past, 0, l_hi - l_lo)
+        if K:
+            for j, keys in enumerate(eng.read_ranges(pv.local, lo + l_lo, msg[:, 1])):
+                msg[j, 2:2 + keys.size] = _to_ordered(keys, desc).astype(np.uint64).view(np.int64)
+        g = comm.allgather_host(msg.ravel()).reshape(p, nb, 2 + K)
+        LT = np.zeros((p, nb), np.int64)
+        EQ = np.zeros((p, nb), np.int64)
+        for j in range(nb):
+            below, cnt_j = g[:, j, 0], g[:, j, 1]
+            if past[j]:         # every key goes to the ranks before this boundary
+                LT[:, j] = n_rank
+                continue
+            if K == 0:          # the block is one key value
+                LT[:, j], EQ[:, j] = below, cnt_j
+                continue
+            runs = [g[r, j, 2:2 + cnt_j[r]].view(np.uint64) for r in range(p)]
+            k = int(targets[j] - below.sum())
+            key = np.partition(np.concatenate(runs), k)[k]
+            for r in range(p):
+                LT[r, j] = below[r] + int(np.searchsorted(runs[r], key, side="left"))
+                EQ[r, j] = int(np.searchsorted(runs[r], key, side="right")) - (LT[r, j] - below[r])
+        remaining = targets - LT.sum(axis=0)                          # equal keys still owed to the left
+        before = np.cumsum(EQ, axis=0) - EQ                           # equal keys of lower ranks
+        take = np.clip(remaining[None, :] - before, 0, EQ)
+        cuts = np.concatenate([np.zeros((p, 1), np.int64), LT + take, n_rank[:, None]], axis=1)
+        sends = np.diff(cuts, axis=1)                                 # sends[r, q]: rank r -> rank q
+        if (sends < 0).any() or int(sends[:, me].sum()) != n_loc:
+            raise RuntimeError(f"segmented sort: rank {me} receives {int(sends[:, me].sum())} keys for a "
+                               f"partition of {n_loc}")
+        return sends[me], sends[:, me]
 
     # --- copy_if: local compaction + all-gather of counts -> global offsets
     def copy_if(self, pol, first, last, dest_pv, pred):

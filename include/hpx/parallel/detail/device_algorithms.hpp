@@ -296,15 +296,17 @@ void merge_sort(compute::hip::target const& t, T* data, uint64_t n, Comp const& 
     // n fills whole vectors (the staging reads whole vectors of each slice)
     const bool vec = reinterpret_cast<uintptr_t>(data) % 16 == 0 && reinterpret_cast<uintptr_t>(tmp) % 16 == 0 &&
                      n % M::vec_elems<T>() == 0;
+    uint32_t* err = nullptr;  // a clamped split raises it (a caller racing the sort)
+    compute::hip::detail::check(hpxhip_device_error_word(t.stream(), &err), "device error word");
     for (uint64_t w = M::kTile; w < n; w *= 2) {
         hipLaunchKernelGGL((M::k_pass_partition<T, L>), dim3(static_cast<unsigned>((ntiles + 255) / 256)), dim3(256),
                            0, stream_of(t), src, n, w, ntiles, less, splits);
         if (vec)
             hipLaunchKernelGGL((M::k_pass_merge<T, L, true>), dim3(static_cast<unsigned>(ntiles)), dim3(M::kThreads),
-                               0, stream_of(t), src, n, w, splits, less, dst);
+                               0, stream_of(t), src, n, w, splits, less, dst, err);
         else
             hipLaunchKernelGGL((M::k_pass_merge<T, L>), dim3(static_cast<unsigned>(ntiles)), dim3(M::kThreads), 0,
-                               stream_of(t), src, n, w, splits, less, dst);
+                               stream_of(t), src, n, w, splits, less, dst, err);
         launched("sort (device closure): merge pass");
         std::swap(src, dst);
     }

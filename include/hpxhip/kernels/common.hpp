@@ -391,6 +391,13 @@ __device__ __forceinline__ T wave_reduce(T x, Op op) {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// The XCD (0-7) this wave runs on: s_getreg_b32 of HW_REG_XCC_ID (hwreg 20,
+// bits [3:0]).  A placement hint for L2 affinity only, never for correctness
+// (cdna_hip_programming.md section 1, T1).
+__device__ __forceinline__ uint32_t xcc_id() {
+    return static_cast<uint32_t>(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20)) & 7u;
+}
+
 // ---------------------------------------------------------------------------
 // Inter-workgroup hand-off words (agent scope).  Producer: payload stored
 // with sc1 (`relaxed, agent` atomic store), then `s_waitcnt vmcnt(0)`, then
@@ -434,6 +441,14 @@ constexpr uint32_t kSpinLimit = 1u << 24;
 
 // Device error word (per library instance); set by a kernel that gave up a
 // spin, read back by hpxhip_device_error().
-enum : uint32_t { HPXHIP_DEVERR_NONE = 0, HPXHIP_DEVERR_LOOKBACK_TIMEOUT = 1 };
+// HPXHIP_DEVERR_RANGE: a scatter destination or merge split outside its
+// buffer (inputs changed while the algorithm ran, e.g. a caller racing a sort
+// from another stream); the store is dropped and the error raised, so the
+// caller gets an error instead of silently wrong output.
+enum : uint32_t { HPXHIP_DEVERR_NONE = 0, HPXHIP_DEVERR_LOOKBACK_TIMEOUT = 1, HPXHIP_DEVERR_RANGE = 2 };
+
+__device__ __forceinline__ void raise_device_error(uint32_t* err, uint32_t code) {
+    if (err) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 }  // namespace hpxhip

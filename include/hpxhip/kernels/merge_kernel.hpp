@@ -134,16 +134,20 @@ __device__ __forceinline__ void merge_in_lds(T* s, int la, int lb, const Less& l
 template <typename T, typename Less, bool VEC>
 __global__ __launch_bounds__(kThreads) void k_merge(const T* __restrict__ a, uint64_t na, const T* __restrict__ b,
                                                      uint64_t nb, const uint64_t* __restrict__ splits, Less less,
-                                                     T* __restrict__ out) {
+                                                     T* __restrict__ out, uint32_t* __restrict__ err = nullptr) {
     __shared__ T s[kTile];
     const uint64_t t = blockIdx.x;
     const uint64_t total = na + nb;
     const uint64_t d0 = t * kTile;
     const uint64_t d1 = d0 + kTile < total ? d0 + kTile : total;
-    // clamped as in k_pass_merge: consistent splits pass unchanged
-    const uint64_t a1 = min(splits[t + 1], min(na, d1));
-    const uint64_t a0 = min(splits[t], min(a1, d0));
+    // clamped as in k_pass_merge: consistent splits pass unchanged; a clamp
+    // that changes one raises the device error word
+    const uint64_t s0 = splits[t], s1 = splits[t + 1];
+    const uint64_t a1 = min(s1, min(na, d1));
+    const uint64_t a0 = min(s0, min(a1, d0));
     const uint64_t b0 = min(d0 - a0, nb), b1 = max(b0, min(d1 - a1, nb));
+    if (threadIdx.x == 0 && (a0 != s0 || a1 != s1 || b0 != d0 - a0 || b1 != d1 - a1))
+        raise_device_error(err, HPXHIP_DEVERR_RANGE);
     const int la = static_cast<int>(a1 - a0), lb = static_cast<int>(b1 - b0);
     const int len = la + lb;
     stage<T, VEC>(a, a0, a1, s);
@@ -251,7 +255,7 @@ __global__ __launch_bounds__(256) void k_pass_partition(const T* __restrict__ sr
 template <typename T, typename Less, bool VEC = false>
 __global__ __launch_bounds__(kThreads) void k_pass_merge(const T* __restrict__ src, uint64_t n, uint64_t w,
                                                           const uint64_t* __restrict__ splits, Less less,
-                                                          T* __restrict__ dst) {
+                                                          T* __restrict__ dst, uint32_t* __restrict__ err = nullptr) {
     __shared__ T s[kTile];
     const uint64_t t = blockIdx.x;
     const uint64_t d0 = t * kTile;
@@ -263,9 +267,13 @@ __global__ __launch_bounds__(kThreads) void k_pass_merge(const T* __restrict__ s
     // splits come from k_pass_partition over the same data; the clamps keep
     // every access inside the run pair even if the data changed in between
     // (a caller racing the sort: garbage order, but no stray access)
-    const uint64_t a1 = min(dl1 == na + nb ? na : splits[t + 1], min(na, dl1));  // tile t + 1 is in the same pair
-    const uint64_t a0 = min(splits[t], min(a1, dl0));
+    const uint64_t s1 = dl1 == na + nb ? na : splits[t + 1];  // tile t + 1 is in the same pair
+    const uint64_t s0 = splits[t];
+    const uint64_t a1 = min(s1, min(na, dl1));
+    const uint64_t a0 = min(s0, min(a1, dl0));
     const uint64_t b0 = min(dl0 - a0, nb), b1 = max(b0, min(dl1 - a1, nb));
+    if (threadIdx.x == 0 && (a0 != s0 || a1 != s1 || b0 != dl0 - a0 || b1 != dl1 - a1))
+        raise_device_error(err, HPXHIP_DEVERR_RANGE);
     const int la = static_cast<int>(a1 - a0), lb = static_cast<int>(b1 - b0);
     const int len = la + lb;
     const T* a = src + p0;

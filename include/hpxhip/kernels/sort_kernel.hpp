@@ -57,6 +57,21 @@ __device__ __forceinline__ uint32_t peers_below(uint64_t peers) {
                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(peers), 0u));
 }
 
+// ------------------------------------------------ segmented LSD (r05)
+// The oversized-bucket finish of the hybrid sort (sort.hip): the LSD passes
+// run over a table of segments -- the few buckets a segment sort could not
+// hold, or the whole array -- each sorted on its own.  Tile ids are global
+// (the look-back state is one array); tile t belongs to segment j with
+// tile0[j] <= t < tile0[j + 1], and its keys are start[j] + (t - tile0[j]) *
+// TILE onwards.  Written by the planner on the device.
+constexpr int kMaxBig = 64;
+struct seg_table {
+    uint64_t start[kMaxBig];
+    uint64_t len[kMaxBig];
+    uint64_t tile0[kMaxBig + 1];
+    uint32_t nseg;
+};
+
 // ---------------------------------------------------------------- histogram
 // One read of the keys -> all passes' 256-bin histograms.  Each bin has
 // COPIES lane-private LDS counters (lane % COPIES), interleaved so that bin
@@ -200,30 +215,58 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
                                                          uint32_t* __restrict__ tcount, uint32_t* __restrict__ csum,
                                                          unsigned long long* __restrict__ xhist,
                                                          unsigned long long* __restrict__ thist,
-                                                         unsigned long long* __restrict__ bits) {
+                                                         unsigned long long* __restrict__ bits,
+                                                         unsigned long long* __restrict__ joint) {
     static_assert(THREADS == kXBins, "one thread per field digit");
     constexpr int V = 16 / static_cast<int>(sizeof(U));
     constexpr int VPT = TILE / V / THREADS;  // 16-B vectors per thread per tile
     static_assert(VPT * V * THREADS == TILE, "tile of whole vectors");
     using VT = vec<U, V>;
     __shared__ uint32_t cnt[kXBins];
-    __shared__ uint32_t ht[kXBins * 2];
+    // r05: the top 9 bits counted per field region (field >> 6: 8 regions of
+    // 64 field digits) -- joint[region][top9], whose sum over the regions is
+    // the top-9 histogram; the second prefix pass runs one region per XCD
+    // and takes each region's bin starts from it (k_region_plan)
+    __shared__ uint32_t hj[8 * kXBins];
     const int d = threadIdx.x;
     cnt[d] = 0;
-    ht[2 * d] = 0;
-    ht[2 * d + 1] = 0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) hj[x * kXBins + d] = 0;
     __syncthreads();
     const bool aligned = reinterpret_cast<uintptr_t>(keys) % 16 == 0;
-    const uint32_t copy = d & 1u;
     U any = 0, all = static_cast<U>(~U(0));
     uint32_t csum_d = 0;
     const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * chunk;
     const uint64_t t1 = t0 + chunk < ntiles ? t0 + chunk : ntiles;
+    // The (field, top-9) cells of the first two lanes still to add are added
+    // once per wave, for all lanes that share them; the other lanes add one
+    // each (r05: sorted or heavily skewed input -- a hot prefix in the first
+    // tiles -- had serialized the lanes of a wave on one or two LDS words:
+    // the histogram took 2.9 ms at 2^28 u64hot against 0.42 for uniform keys)
     auto count = [&](U b) {
         any |= b;
         all &= b;
-        atomicAdd(&cnt[static_cast<uint32_t>(b >> xshift) & (kXBins - 1)], 1u);
-        atomicAdd(&ht[(static_cast<uint32_t>(b >> tshift) & (kXBins - 1)) * 2 + copy], 1u);
+        const uint32_t f = static_cast<uint32_t>(b >> xshift) & (kXBins - 1);
+        const uint32_t j = (f >> 6) * kXBins + (static_cast<uint32_t>(b >> tshift) & (kXBins - 1));
+        const uint32_t cell = (f << 12) | j;
+        uint64_t rem = __ballot(1);
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            if (rem == 0) break;
+            const int lead = __builtin_ctzll(rem);
+            const uint32_t c0 = __builtin_amdgcn_readlane(cell, lead);
+            const uint64_t grp = __ballot(cell == c0) & rem;
+            if (lane_id() == lead) {
+                const uint32_t c = static_cast<uint32_t>(__builtin_popcountll(grp));
+                atomicAdd(&cnt[c0 >> 12], c);
+                atomicAdd(&hj[c0 & 0xfffu], c);
+            }
+            rem &= ~grp;
+        }
+        if ((rem >> lane_id()) & 1u) {
+            atomicAdd(&cnt[f], 1u);
+            atomicAdd(&hj[j], 1u);
+        }
     };
     for (uint64_t t = t0; t < t1; ++t) {
         const uint64_t base = t * TILE;
@@ -249,7 +292,13 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
     }
     csum[static_cast<uint64_t>(blockIdx.x) * kXBins + d] = csum_d;
     if (csum_d) atomicAdd(&xhist[d], static_cast<unsigned long long>(csum_d));
-    const uint32_t tc = ht[2 * d] + ht[2 * d + 1];
+    uint32_t tc = 0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+        const uint32_t c = hj[x * kXBins + d];
+        tc += c;
+        if (c) atomicAdd(&joint[x * kXBins + d], static_cast<unsigned long long>(c));
+    }
     if (tc) atomicAdd(&thist[d], static_cast<unsigned long long>(tc));
     any = wave_reduce(any, op_bit_or{});
     all = wave_reduce(all, op_bit_and{});
@@ -313,6 +362,38 @@ __global__ __launch_bounds__(kXBins) void k_tile_offsets(uint32_t* __restrict__ 
     }
 }
 
+// The second prefix pass of the 18-bit form (r05): its input -- the first
+// pass's output, ordered by the field -- cut into 8 regions of 64 field
+// digits (contiguous: [xstart[64 x], xstart[64 x + 64])), one per XCD
+// (k_onesweep XREG + SEG), each with its own look-back; region x's bin start
+// for top-9 digit d is tstart[d] + the keys of digit d in regions < x
+// (joint, k_hist_tiles).  One workgroup, thread d owns digit d.
+__global__ __launch_bounds__(kXBins) void k_region_plan(const unsigned long long* __restrict__ xstart,
+                                                         const unsigned long long* __restrict__ tstart,
+                                                         const unsigned long long* __restrict__ joint, uint64_t n,
+                                                         int tile, seg_table* __restrict__ segs,
+                                                         unsigned long long* __restrict__ bs) {
+    const int d = threadIdx.x;
+    if (d == 0) {
+        segs->nseg = 8;
+        uint64_t t = 0;
+        for (int x = 0; x < 8; ++x) {
+            const uint64_t lo = xstart[64 * x], hi = x < 7 ? xstart[64 * (x + 1)] : n;
+            segs->start[x] = lo;
+            segs->len[x] = hi - lo;
+            segs->tile0[x] = t;
+            t += (hi - lo + tile - 1) / tile;
+        }
+        segs->tile0[8] = t;
+    }
+    unsigned long long run = tstart[d];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+        bs[x * kXBins + d] = run;
+        run += joint[x * kXBins + d];
+    }
+}
+
 // Exclusive scan of each pass's R counts (one R-thread block per pass).
 template <int R = kRadix>
 __global__ __launch_bounds__(R) void k_bin_offsets(const unsigned long long* __restrict__ hist,
@@ -328,6 +409,77 @@ __global__ __launch_bounds__(R) void k_bin_offsets(const unsigned long long* __r
     uint64_t pre = 0;
     for (int w = 0; w < wave; ++w) pre += s_w[w];
     start[p * R + d] = pre + incl - c;
+}
+
+// Every digit's 256-bin histogram of every segment (hist[j][8][256], the
+// segment's pass p at [j][p]); a persistent grid over the segments' TILE-key
+// tiles; runs iff *gate.
+template <typename U, typename X, int THREADS = 256, int TILE = 8192>
+__global__ __launch_bounds__(THREADS) void k_seg_hist(const U* __restrict__ keys, const seg_table* __restrict__ segs,
+                                                       X xf, unsigned long long* __restrict__ hist,
+                                                       const int32_t* __restrict__ gate) {
+    if (*gate == 0) return;
+    constexpr int P = static_cast<int>(sizeof(U));
+    __shared__ uint32_t s_h[P * kRadix];
+    const uint32_t nseg = segs->nseg;
+    const uint64_t ntiles = segs->tile0[nseg];
+    for (uint64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+        uint32_t j = 0;
+        while (j + 1 < nseg && segs->tile0[j + 1] <= tl) ++j;
+        const uint64_t lo = segs->start[j] + (tl - segs->tile0[j]) * TILE;
+        const uint64_t end = segs->start[j] + segs->len[j];
+        const uint64_t hi = lo + TILE < end ? lo + TILE : end;
+        for (int i = threadIdx.x; i < P * kRadix; i += THREADS) s_h[i] = 0;
+        __syncthreads();
+        for (uint64_t i = lo + threadIdx.x; i < hi; i += THREADS) {
+            const U u = xf(keys[i]);
+#pragma unroll
+            for (int q = 0; q < P; ++q) atomicAdd(&s_h[q * kRadix + ((u >> (8 * q)) & 0xffu)], 1u);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < P * kRadix; i += THREADS)
+            if (s_h[i]) atomicAdd(&hist[static_cast<uint64_t>(j) * 8 * kRadix + i], static_cast<unsigned long long>(s_h[i]));
+        __syncthreads();
+    }
+}
+
+// Segment j, pass p (block j * 8 + p): bin starts = start[j] + the exclusive
+// scan of its histogram; runs iff *gate.  Without *counted (a planned
+// whole-array LSD) segment 0's come from the global histogram (ghist).
+__global__ __launch_bounds__(kRadix) void k_seg_offsets(const unsigned long long* __restrict__ hist,
+                                                         const seg_table* __restrict__ segs,
+                                                         unsigned long long* __restrict__ bs,
+                                                         const int32_t* __restrict__ gate,
+                                                         const int32_t* __restrict__ counted,
+                                                         const unsigned long long* __restrict__ ghist) {
+    if (*gate == 0) return;
+    const uint32_t j = blockIdx.x / 8;
+    if (j >= segs->nseg) return;
+    __shared__ unsigned long long s_w[kRadix / kWave];
+    const uint64_t o = static_cast<uint64_t>(blockIdx.x) * kRadix;
+    const int t = threadIdx.x;
+    const unsigned long long c = *counted ? hist[o + t] : ghist[o + t];
+    const unsigned long long incl = wave_inclusive_scan(c, op_plus{});
+    if (lane_id() == kWave - 1) s_w[t / kWave] = incl;
+    __syncthreads();
+    unsigned long long pre = segs->start[j];
+    for (int w = 0; w < t / kWave; ++w) pre += s_w[w];
+    bs[o + t] = pre + incl - c;
+}
+
+// dst = src over the segments' ranges (the LSD ended in the alternate
+// buffer), runs iff *gate.
+template <typename E>
+__global__ __launch_bounds__(256) void k_seg_copy(const E* __restrict__ src, E* __restrict__ dst,
+                                                  const seg_table* __restrict__ segs,
+                                                  const int32_t* __restrict__ gate) {
+    if (*gate == 0) return;
+    for (uint32_t j = 0; j < segs->nseg; ++j) {
+        const uint64_t lo = segs->start[j], len = segs->len[j];
+        for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < len;
+             i += static_cast<uint64_t>(gridDim.x) * 256)
+            dst[lo + i] = src[lo + i];
+    }
 }
 
 // ----------------------------------------------------------------- onesweep
@@ -352,8 +504,11 @@ __global__ __launch_bounds__(R) void k_bin_offsets(const unsigned long long* __r
 // skipped 2^30-key pass had dispatched 131072 workgroups that only read the
 // gate and left (~0.1 ms each, ~0.9 ms per sort over the skipped second-byte
 // and LSD passes); a persistent grid leaves after one read per workgroup.
+// SEG (r05, with PERSIST): the tiles of a seg_table; bin_start holds
+// [segment][pass][256] bin starts, and each segment is sorted on its own.
 template <typename U, typename VAL, bool HAS_VAL, typename G, typename X, int THREADS = 512, int ITEMS = 16,
-          int LBB = 8, int RB = 8, bool STAGE = true, bool DYN_ID = HPXHIP_TILE_DYN_ID, bool PERSIST = false>
+          int LBB = 8, int RB = 8, bool STAGE = true, bool DYN_ID = HPXHIP_TILE_DYN_ID, bool PERSIST = false,
+          bool SEG = false, bool XREG = false>
 __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin, U* __restrict__ kout,
                                                        const VAL* __restrict__ vin, VAL* __restrict__ vout,
                                                        uint64_t n, int shift,
@@ -361,8 +516,14 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
                                                        G* __restrict__ lb, uint32_t* __restrict__ counter,
                                                        uint32_t* __restrict__ err, X xf,
                                                        const int32_t* __restrict__ ctl = nullptr, uint64_t ntiles = 0,
-                                                       const uint32_t* __restrict__ pre = nullptr) {
+                                                       const uint32_t* __restrict__ pre = nullptr,
+                                                       const seg_table* __restrict__ segs = nullptr) {
     static_assert(!PERSIST || STAGE, "the persistent form keeps the LDS-staged write-out");
+    static_assert(!SEG || ((PERSIST || XREG) && LBB > 0), "segmented passes: look-back passes, persistent or XREG");
+    static_assert(!XREG || !PERSIST, "XCD regions: one tile per block");
+    static_assert(!XREG || SEG || LBB < 0, "XCD regions of equal tile ranges: the offset-fed pass (no look-back)");
+    // segment table entries a workgroup loads (XREG: the 8 regions)
+    constexpr int NS = XREG ? 8 : kMaxBig;
     // device-planned sort (sort.hip): *ctl = this launch's digit shift, or
     // -1 when the plan does not take this pass (every block returns at once)
     if (ctl) {
@@ -378,6 +539,10 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     constexpr int WAVES = THREADS / kWave;
     constexpr int TILE = THREADS * ITEMS;
     __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_seg;
+    // SEG: the segment table, loaded once per (persistent) workgroup, so a
+    // tile's segment costs LDS reads, not a chain of global loads per tile
+    __shared__ uint64_t s_sg[SEG ? 3 * kMaxBig + 2 : 1];
     __shared__ CT s_whist[WAVES][R];
     __shared__ uint32_t s_local[R];
     __shared__ uint32_t s_wsum[R / kWave];
@@ -387,6 +552,19 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
 
     const int t_id = threadIdx.x;
     const int lane_ = lane_id();
+    // SEG: s_sg = {start[kMaxBig], len[kMaxBig], tile0[kMaxBig + 1], nseg}
+    // (the first NS segments)
+    if constexpr (SEG) {
+        for (int i = t_id; i <= NS; i += THREADS) {
+            if (i < NS) {
+                s_sg[i] = segs->start[i];
+                s_sg[kMaxBig + i] = segs->len[i];
+            }
+            s_sg[2 * kMaxBig + i] = segs->tile0[i];
+        }
+        if (t_id == 0) s_sg[3 * kMaxBig + 1] = segs->nseg;
+        __syncthreads();
+    }
     // one tile; the persistent form calls it in a loop, the plain form once
     // (a loop around the body in the plain form changes its register
     // allocation)
@@ -400,23 +578,79 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     const int wave = t / kWave;
     // tile order = dispatch order (lookback.hpp); DYN_ID / PERSIST: ids from
     // the atomic counter
-    if ((DYN_ID || PERSIST) && t == 0)
+    if (XREG && t == 0) {
+        // XREG: the tiles are cut into 8 contiguous regions, one per XCD
+        // (SEG: the table's segments; else equal tile ranges); a workgroup
+        // claims the next tile of its own XCD's region (counter 8 words per
+        // region), so consecutive tiles -- whose digit runs end and start in
+        // the same lines -- are written through one L2 (r05: the first prefix
+        // pass 4.75 -> 3.81 ms at 2^30 u64, profiles/r05_ubench_sortpass5.log);
+        // a region that is done sends its XCD's workgroups to the next ones
+        const uint32_t x = xcc_id();
+        uint32_t tl = 0xffffffffu, sg = 0;
+        for (uint32_t k = 0; k < 8 && tl == 0xffffffffu; ++k) {
+            const uint32_t xr = (x + k) & 7u;
+            uint64_t lo, cnt;
+            if constexpr (SEG) {
+                if (xr >= static_cast<uint32_t>(s_sg[3 * kMaxBig + 1])) continue;
+                lo = s_sg[2 * kMaxBig + xr];
+                cnt = s_sg[2 * kMaxBig + xr + 1] - lo;
+            } else {
+                const uint64_t per = (ntiles + 7) / 8;
+                lo = xr * per;
+                cnt = lo < ntiles ? (ntiles - lo < per ? ntiles - lo : per) : 0;
+            }
+            if (cnt == 0) continue;
+            const uint32_t c = __hip_atomic_fetch_add(counter + 8 * xr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c < cnt) {
+                tl = static_cast<uint32_t>(lo + c);
+                sg = xr;
+            }
+        }
+        s_tile = tl;
+        if constexpr (SEG) s_seg = sg;
+    } else if ((DYN_ID || PERSIST) && t == 0) {
         s_tile = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (SEG && !XREG) {  // the tile's segment
+            const uint32_t nseg = static_cast<uint32_t>(s_sg[3 * kMaxBig + 1]);
+            uint32_t j = 0;
+            while (j + 1 < nseg && s_sg[2 * kMaxBig + j + 1] <= s_tile) ++j;
+            s_seg = j;
+        }
+    }
     for (int i = t; i < WAVES * R; i += THREADS) (&s_whist[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t tile = (DYN_ID || PERSIST) ? s_tile : blockIdx.x;
-    if (PERSIST && tile >= ntiles) return false;
-    const uint64_t tile_base = tile * TILE;
+    const uint64_t tile = (DYN_ID || PERSIST || XREG) ? s_tile : blockIdx.x;
+    if (XREG && !SEG && tile >= ntiles) return false;
+    // SEG: the tile's segment [seg_lo, end), its first tile and bin starts
+    uint64_t end = n, seg_lo = 0, first_tile = 0, tile_base = tile * TILE;
+    const unsigned long long* bstart = bin_start;
+    if constexpr (SEG) {
+        const uint32_t nseg = static_cast<uint32_t>(s_sg[3 * kMaxBig + 1]);
+        if (tile >= s_sg[2 * kMaxBig + nseg]) return false;
+        const uint32_t j = s_seg;
+        first_tile = s_sg[2 * kMaxBig + j];
+        seg_lo = s_sg[j];
+        end = seg_lo + s_sg[kMaxBig + j];
+        tile_base = seg_lo + (tile - first_tile) * TILE;
+        bstart = bin_start + static_cast<uint64_t>(j) * (RB == 9 ? kXBins : 8 * kRadix);
+    } else if (PERSIST && tile >= ntiles) {
+        return false;
+    }
+    // where the outputs may land: the segment itself (a segmented LSD sorts
+    // each segment in place), or anywhere (XREG regions are input ranges
+    // whose keys go to the whole array)
+    const uint64_t out_lo = (SEG && !XREG) ? seg_lo : 0, out_hi = (SEG && !XREG) ? end : n;
     const uint64_t wbase = tile_base + static_cast<uint64_t>(wave) * (TILE / WAVES);
 
     // ---- load: round r, lane l -> tile position wave*(TILE/WAVES) + r*64 + l
     U k[ITEMS];
     VAL v[HAS_VAL ? ITEMS : 1];
-    const bool full = tile_base + TILE <= n;
+    const bool full = tile_base + TILE <= end;
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = wbase + r * kWave + lane;
-        if (full || i < n) {
+        if (full || i < end) {
             k[r] = kin[i];
             if constexpr (HAS_VAL) v[r] = vin[i];
         } else {
@@ -429,7 +663,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = wbase + r * kWave + lane;
-        const bool valid = full || i < n;
+        const bool valid = full || i < end;
         const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
         const uint64_t peers = match_digit<RB>(d, __ballot(valid));
         const uint32_t below = peers_below(peers);
@@ -452,7 +686,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             tile_count += c;
         }
         // publish this tile's aggregate for digit t as early as possible
-        if (tile != 0 && LBB > 0)
+        if (tile != first_tile && LBB > 0)
             __hip_atomic_store(&my[t], enc_agg<G>(tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         count_incl = wave_inclusive_scan(tile_count, op_plus{});
         if (lane == kWave - 1) s_wsum[wave] = count_incl;
@@ -478,7 +712,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = wbase + r * kWave + lane;
-        if (STAGE && (full || i < n)) {
+        if (STAGE && (full || i < end)) {
             const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
             const uint32_t pos = s_whist[wave][d] + rank[r];
             s_keys[pos] = k[r];
@@ -489,7 +723,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     // ---- per-digit look-back across tiles (thread t < R owns digit t)
     if (t < R) {
         uint64_t excl = 0;
-        if (tile == 0) {
+        if (tile == first_tile) {
             if (LBB > 0) __hip_atomic_store(&my[t], enc_incl<G>(tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if constexpr (LBB > 0) {
             int64_t pred = static_cast<int64_t>(tile) - 1;
@@ -499,7 +733,8 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
                 G g[LBB];
 #pragma unroll
                 for (int j = 0; j < LBB; ++j)
-                    g[j] = (pred - j >= 0) ? __hip_atomic_load(&lb[static_cast<uint64_t>(pred - j) * R + t],
+                    g[j] = (pred - j >= static_cast<int64_t>(first_tile))
+                               ? __hip_atomic_load(&lb[static_cast<uint64_t>(pred - j) * R + t],
                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                            : enc_incl<G>(0);
                 int used = 0;
@@ -528,7 +763,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             }
             __hip_atomic_store(&my[t], enc_incl<G>(excl + tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        s_adj[t] = static_cast<uint64_t>(bin_start[t]) + excl - (STAGE ? s_local[t] : 0u);
+        s_adj[t] = static_cast<uint64_t>(bstart[t]) + excl - (STAGE ? s_local[t] : 0u);
         if constexpr (LBB < 0)  // PRE: the tile's destination offsets, precomputed (k_tile_offsets)
             s_adj[t] = static_cast<uint64_t>(pre[tile * R + t]) - (STAGE ? s_local[t] : 0u);
     }
@@ -537,12 +772,14 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
 #pragma unroll
         for (int r = 0; r < ITEMS; ++r) {
             const uint64_t i = wbase + r * kWave + lane;
-            if (full || i < n) {
+            if (full || i < end) {
                 const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
                 const uint64_t dst = s_adj[d] + s_whist[wave][d] + rank[r];
-                if (dst < n) {  // see the write-out below
+                if (dst < out_hi && dst >= out_lo) {  // see the write-out below
                     kout[dst] = k[r];
                     if constexpr (HAS_VAL) vout[dst] = v[r];
+                } else {
+                    raise_device_error(err, HPXHIP_DEVERR_RANGE);
                 }
             }
         }
@@ -550,7 +787,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     }
 
     // ---- coalesced write of the LDS-sorted tile
-    const uint32_t nvalid = full ? TILE : static_cast<uint32_t>(n - tile_base);
+    const uint32_t nvalid = full ? TILE : static_cast<uint32_t>(end - tile_base);
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint32_t i = r * THREADS + t;
@@ -560,12 +797,14 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             const uint64_t dst = s_adj[d] + i;
             // Destinations come from the histogram taken before the pass: they
             // stay below n unless the keys were changed during the sort (a
-            // caller racing the sort on another stream).  Then the result is
-            // garbage, but no store leaves the output buffer (it would
-            // overwrite the plan words in the scratch that follows it).
-            if (dst < n) {
+            // caller racing the sort on another stream).  Then no store leaves
+            // the output buffer (it would overwrite the plan words in the
+            // scratch that follows it) and the device error word reports it.
+            if (dst < out_hi && dst >= out_lo) {
                 kout[dst] = key;
                 if constexpr (HAS_VAL) vout[dst] = s_vals[i];
+            } else {
+                raise_device_error(err, HPXHIP_DEVERR_RANGE);
             }
         }
     }
@@ -648,8 +887,9 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 // BOUNDS: `seg` is the bucket-bounds array itself (segment = one bucket,
 // [seg[b], seg[b + 1])), as the host uses when buckets average at least half
 // a segment: no bounds read-back and no host packing between the prefix
-// passes and this kernel.  A bucket too large for the LDS is left alone and
-// raises *oversized (the host then finishes it by per-bucket LSD).
+// passes and this kernel.  A bucket too large for the LDS is left alone,
+// raises *oversized and records its id in `big` (sort.hip finishes up to
+// kMaxBig of them by a segmented LSD over just their ranges).
 // PERSIST (device-planned sort, BOUNDS only): a fixed grid strides over the
 // planned buckets (bucket b by workgroup b mod gridDim), so a launch the plan
 // skips costs one gate read per workgroup instead of one dispatch per bucket.
@@ -658,7 +898,8 @@ template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX
 __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
     void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf,
                        VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr,
-                       const int32_t* __restrict__ ctl = nullptr, uint32_t first_bucket = 0) {
+                       const int32_t* __restrict__ ctl = nullptr, uint32_t first_bucket = 0,
+                       uint32_t* __restrict__ big = nullptr) {
     static_assert(!PERSIST || BOUNDS, "the persistent form strides over bucket bounds");
     // device-planned sort: ctl = {on, buckets, top_single}; the grid covers
     // the largest bucket count (or strides over it), blocks past the planned
@@ -696,7 +937,15 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
         b = seg[bk];
         mm = seg[bk + 1] - b;
         if (mm > static_cast<uint64_t>(THREADS) * ITEMS) {
-            if (t == 0) __hip_atomic_store(oversized, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == 0) {
+                __hip_atomic_store(oversized, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // r05: the bucket's id, for the planner's bounded finish
+                // (big[0] counts them; ids past kMaxBig are not kept)
+                if (big) {
+                    const uint32_t slot = __hip_atomic_fetch_add(big, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (slot < static_cast<uint32_t>(kMaxBig)) big[1 + slot] = bk;
+                }
+            }
             return;
         }
     } else {

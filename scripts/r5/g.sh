@@ -1,0 +1,17 @@
+# round 5, lease g: pass-2 look-back widths over XCD regions (sortpass6), pass-1 orders again (sortpass5),
+# skewed-sort fixes (wave-uniform histogram adds, b2 for concentrated skew): tests + probes + trace
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+L=gpurun_out/r5g
+timeout -k 10 300 ./scripts/ubench/sortpass6 > ${L}_sortpass6.log 2>&1 || exit $?
+timeout -k 10 300 ./scripts/ubench/sortpass5 > ${L}_sortpass5.log 2>&1 || exit $?
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_sort_hybrid.py \
+  > ${L}_tests.log 2>&1 || exit $?
+for c in u64 u32 u64hot; do
+  SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 30 >> ${L}_probe.log 2>&1 || exit $?
+done
+for c in u64hot u64corr u64; do
+  SORT_ONLY=$c timeout -k 10 120 python -u scripts/sort_probe.py 28 >> ${L}_probe.log 2>&1 || exit $?
+done
+SORT_ONLY=u64hot timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d ${L}_prof28 -o hot -- \
+  python3 scripts/sort_probe.py 28 > ${L}_prof.log 2>&1 || exit $?

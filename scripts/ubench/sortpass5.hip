@@ -1,0 +1,137 @@
+// Microbenchmark (round 5): the 18-bit sort's first prefix pass (the 9-bit
+// field [46, 55) of 2^30 random u64 keys) from precomputed tile offsets
+// (k_hist_tiles -> k_tile_chunk_scan -> k_tile_offsets, no look-back), in
+// three tile orders:
+//   counter : the shipped order, tiles claimed from one atomic counter;
+//   blockidx: tile = blockIdx (r04 measured it 8.4 vs 5.1 ms);
+//   xreg    : 8 contiguous regions, one per XCD (HW_REG_XCC_ID), each
+//             claimed in order from its own counter (k_onesweep XREG).
+// The offsets fix every key's destination, so all orders must produce the
+// same output: the XOR / sum checksums of the outputs are compared, and the
+// kernel's own time is the best of 7 (HIP events).
+// build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../include sortpass5.hip -o sortpass5
+#include <hpxhip/kernels/sort_kernel.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+using namespace hpxhip;
+using namespace hpxhip::sort_detail;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+__global__ void k_fill_rand(uint64_t* k, uint64_t n) {
+    const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    uint64_t z = (i ^ 0x5EEDull) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    k[i] = z ^ (z >> 31);
+}
+// position-weighted checksum: equal iff (with overwhelming probability) the arrays are equal
+__global__ void k_sum(const uint64_t* k, uint64_t n, unsigned long long* out) {
+    unsigned long long acc = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += 256ull * gridDim.x)
+        acc += k[i] * (2 * i + 1);
+    atomicAdd(out, acc);
+}
+
+static hipEvent_t e0, e1;
+template <typename F>
+float bench(F f) {
+    f();
+    CK(hipDeviceSynchronize());
+    std::vector<float> t;
+    for (int r = 0; r < 7; ++r) {
+        CK(hipEventRecord(e0));
+        f();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    return t[0];
+}
+
+int main() {
+    const uint64_t n = 1ull << 30;
+    const uint64_t ntiles = n / 8192, chunk = 256, nchunks = (ntiles + chunk - 1) / chunk;
+    uint64_t *kin, *kout;
+    unsigned long long *xhist, *xstart, *thist, *bits, *sum, *joint;
+    uint32_t *tcount, *csum, *err, *cnt;
+    int32_t* gate;
+    CK(hipMalloc(&kin, n * 8));
+    CK(hipMalloc(&kout, n * 8));
+    CK(hipMalloc(&xhist, 512 * 8));
+    CK(hipMalloc(&xstart, 512 * 8));
+    CK(hipMalloc(&thist, 512 * 8));
+    CK(hipMalloc(&joint, 8 * 512 * 8));
+    CK(hipMemset(joint, 0, 8 * 512 * 8));
+    CK(hipMalloc(&bits, 256));
+    CK(hipMalloc(&sum, 8));
+    CK(hipMalloc(&tcount, ntiles * 512 * 4));
+    CK(hipMalloc(&csum, nchunks * 512 * 4));
+    CK(hipMalloc(&err, 64));
+    CK(hipMalloc(&cnt, 256));
+    CK(hipMalloc(&gate, 4));
+    const int32_t shift = 46;
+    CK(hipMemcpy(gate, &shift, 4, hipMemcpyHostToDevice));
+    CK(hipMemset(err, 0, 64));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(k_fill_rand, dim3(n / 256), dim3(256), 0, 0, kin, n);
+    using X = ordered_bits<uint64_t, false>;
+    CK(hipMemset(xhist, 0, 512 * 8));
+    CK(hipMemset(thist, 0, 512 * 8));
+    CK(hipMemset(bits, 0, 8));
+    CK(hipMemset(bits + 1, 0xff, 8));
+    hipLaunchKernelGGL((k_hist_tiles<uint64_t, X, 8192, kXBins>), dim3(nchunks), dim3(kXBins), 0, 0, kin, n, ntiles,
+                       uint32_t(chunk), X{}, 46, 55, tcount, csum, xhist, thist, bits, joint);
+    hipLaunchKernelGGL(k_bin_offsets<512>, dim3(1), dim3(512), 0, 0, xhist, xstart);
+    hipLaunchKernelGGL(k_tile_chunk_scan, dim3(1), dim3(kXBins), 0, 0, csum, nchunks, xstart, gate);
+    hipLaunchKernelGGL(k_tile_offsets, dim3(nchunks), dim3(kXBins), 0, 0, tcount, ntiles, uint32_t(chunk), csum, gate);
+    CK(hipDeviceSynchronize());
+    auto checksum = [&] {
+        CK(hipMemset(sum, 0, 8));
+        hipLaunchKernelGGL(k_sum, dim3(4096), dim3(256), 0, 0, kout, n, sum);
+        unsigned long long h;
+        CK(hipMemcpy(&h, sum, 8, hipMemcpyDeviceToHost));
+        return h;
+    };
+    auto counter = [&](auto flag, auto xreg) {
+        constexpr bool DYN = decltype(flag)::value;
+        constexpr bool XR = decltype(xreg)::value;
+        return bench([&] {
+            CK(hipMemsetAsync(cnt, 0, 256));
+            hipLaunchKernelGGL((k_onesweep<uint64_t, uint32_t, false, uint32_t, X, 512, 16, -1, 9, true, DYN, false,
+                                           false, XR>),
+                               dim3(ntiles), dim3(512), 0, 0, kin, kout, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                               n, 46, xstart, (uint32_t*)nullptr, cnt, err, X{}, (const int32_t*)nullptr, ntiles,
+                               (const uint32_t*)tcount);
+        });
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    for (int rep = 0; rep < 3; ++rep) {
+        CK(hipMemset(kout, 0, n * 8));
+        const float a = counter(T_{}, F_{});
+        const unsigned long long ca = checksum();
+        CK(hipMemset(kout, 0, n * 8));
+        const float b = counter(F_{}, F_{});
+        const unsigned long long cb = checksum();
+        CK(hipMemset(kout, 0, n * 8));
+        const float c = counter(F_{}, T_{});
+        const unsigned long long cc = checksum();
+        printf("rep %d  counter %.3f ms  blockidx %.3f ms  xreg %.3f ms   (16 B/key: %.0f / %.0f / %.0f GB/s)  "
+               "same output: %s %s\n",
+               rep, a, b, c, 16.0 * n / a / 1e6, 16.0 * n / b / 1e6, 16.0 * n / c / 1e6, ca == cb ? "yes" : "NO",
+               ca == cc ? "yes" : "NO");
+        fflush(stdout);
+    }
+    uint32_t herr;
+    CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+    printf("deverr %u\n", herr);
+    return 0;
+}

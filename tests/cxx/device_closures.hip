@@ -123,6 +123,21 @@ struct bulk_slow {
     }
     HPX_HOST_DEVICE void operator()(int i) { out[i - 3] = expect(i, iters); }
 };
+// Waits (bounded: ~3 s, then runs anyway) until the host opens the gate, a
+// word in pinned host memory: the work is certainly pending until then.
+struct bulk_gated {
+    int* out;
+    int const* gate;
+    __device__ static bool open(int const* g) {
+        return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    }
+    HPX_HOST_DEVICE void operator()(int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        for (int spins = 0; spins < (1 << 20) && !open(gate); ++spins) __builtin_amdgcn_s_sleep(127);
+#endif
+        out[i - 3] = bulk_slow::expect(i, 16);
+    }
+};
 struct bulk_test_args {
     HPX_HOST_DEVICE void operator()(int i, int* out, int base, int add) { out[i - base] = i + add; }
 };
@@ -169,21 +184,23 @@ void test_executor(Executor& exec, hip::target const& t, std::mt19937& gen, char
     std::iota(big.begin(), big.end(), 3);
     hpx::compute::vector<int, hip::allocator<int>> bo(big.size(), -1, alloc);
     {
-        // ~10^12 device iterations (tens of ms): not done when the call
-        // returns, even after the concurrent executor has built its
-        // one-future-per-element result (a few ms; 10^11 iterations raced it);
-        // checked on a sample of the elements
-        constexpr int slow = 1000000;
-        auto fs = ex::bulk_async_execute(exec, bulk_slow{bo.data(), slow}, big);
-        bool pending = false;
-        for (auto& f : fs) pending = pending || !f.is_ready();
+        // the body waits for a gate the host opens only after checking that
+        // the futures are pending (r05: deterministic; r04 raced a slow
+        // kernel's duration against the host building 10^6 futures)
+        int* gate = nullptr;
+        HPX_TEST_EQ(hpxhip_malloc_host(reinterpret_cast<void**>(&gate), sizeof(int)), 0);
+        __atomic_store_n(gate, 0, __ATOMIC_SEQ_CST);
+        auto fs = ex::bulk_async_execute(exec, bulk_gated{bo.data(), gate}, big);
+        bool pending = true;
+        for (auto& f : fs) pending = pending && !f.is_ready();
         HPX_TEST(pending);
         big.assign(big.size(), 0);  // the caller's shape may go away at once
+        __atomic_store_n(gate, 1, __ATOMIC_SEQ_CST);
         hpx::when_all(std::move(fs)).get();
         std::vector<int> hb = to_host(bo);
-        for (std::size_t i = 0; i < hb.size(); i += 9973)
-            if (!HPX_TEST_EQ(hb[i], bulk_slow::expect(int(i) + 3, slow))) break;
-        HPX_TEST_EQ(hb.back(), bulk_slow::expect(int(hb.size()) + 2, slow));
+        for (std::size_t i = 0; i != hb.size(); ++i)
+            if (!HPX_TEST_EQ(hb[i], bulk_slow::expect(int(i) + 3, 16))) break;
+        hpxhip_free_host(gate);
     }
     std::iota(big.begin(), big.end(), 3);
     auto fs = ex::bulk_async_execute(exec, bulk_slow{bo.data()}, big);

@@ -56,6 +56,12 @@ class HostStagedComm:
     def allgather_host(self, words):
         return np.stack(self._allgather_bytes(np.ascontiguousarray(words, np.int64).view(np.uint8))).view(np.int64)
 
+    def allreduce_host(self, words):
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(words, np.int64).copy())
+        self.dist.all_reduce(t)
+        return t.numpy()
+
     def alltoallv(self, send_buf, send_off, send_counts, recv_buf, recv_counts, itemsize, stream, recv_off=0):
         import torch
         self.tgt.synchronize()

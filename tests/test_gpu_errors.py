@@ -67,3 +67,28 @@ def test_argument_errors_pass_unchanged(gpu_target, vec):
     with pytest.raises(ValueError):
         P.fill(ex.par, vec.end(), vec.begin(), 1)
     L.call("hpxhip_debug_inject_error", 0, 0)
+
+
+def test_inconsistent_merge_splits_raise(gpu_target):
+    """merge_kernel.hpp k_merge: merge-path splits that are out of order (an
+    input that is not sorted, or one changed while the merge ran, as a
+    caller racing a sort from another stream does) are clamped so no access
+    leaves the inputs, and the clamp raises the device error word
+    (HPXHIP_DEVERR_RANGE): the caller gets exception_list, not silently wrong
+    output (the clamped scatters of k_onesweep / k_merge used to
+    be silent).  Here the splits come out of order deterministically: with
+    2048-element tiles, a = [0]*2048 + [100]*2048 and the unsorted
+    b = [10]*2048 + [-5]*2048, the diagonal 2048 splits at 2048 and the
+    diagonal 4096 at 0 (path_split's binary search)."""
+    a = np.concatenate([np.zeros(2048, np.int64), np.full(2048, 100, np.int64)])
+    b = np.concatenate([np.full(2048, 10, np.int64), np.full(2048, -5, np.int64)])
+    va, vb = hpx.vector.from_host(a, gpu_target), hpx.vector.from_host(b, gpu_target)
+    out = hpx.vector(8192, dtype=np.int64, tgt=gpu_target)
+    with pytest.raises(L.exception_list) as ei:
+        P.merge(ex.par, va.begin(), va.end(), vb.begin(), vb.end(), out.begin())
+    (inner,) = list(ei.value)
+    assert ei.value.status == L.ERROR_DEVICE_TIMEOUT and "error word 2" in str(inner)
+    # reported once: a consistent merge afterwards is clean and correct
+    vb2 = hpx.vector.from_host(np.sort(b), gpu_target)
+    P.merge(ex.par, va.begin(), va.end(), vb2.begin(), vb2.end(), out.begin())
+    assert np.array_equal(out.to_host(), np.sort(np.concatenate([a, b]), kind="stable"))

@@ -103,8 +103,9 @@ def test_mixed_sign_double_scan_bound(pol, gpu_target):
 
 @pytest.mark.parametrize("desc,kdt", [(False, np.uint64), (True, np.uint64), (False, np.uint32)])
 def test_sort_2p30_permutation_and_order(pol, gpu_target, desc, kdt):
-    # u64: the 17-bit hybrid with direct per-bucket segments; u32: the same
-    # hybrid on 32-bit keys (two LDS passes finish each bucket)
+    # u64: the 18-bit hybrid (two 9-bit prefix passes, ~4096-key buckets in
+    # 512 x 9 LDS segments); u32: the same hybrid on 32-bit keys (two LDS
+    # passes finish each bucket)
     n = 1 << 30
     keys = hpx.vector(n, dtype=kdt, tgt=gpu_target)
     P.generate(pol, keys.begin(), keys.end(), "bits", 7)
@@ -189,10 +190,11 @@ def test_is_sorted_signed_zero_and_nan(pol, gpu_target, dt):
 
 def test_sort_2p30_oversized_bucket(pol, gpu_target):
     # 2^30 keys: the hybrid sorts one bucket per workgroup straight from the
-    # bucket bounds; 30000 extra keys in one 17-bit prefix make that bucket
-    # too large for the LDS segment -- the kernel flags it and the host
-    # finishes it by per-bucket LSD.  Checked on the device: ordered, and a
-    # permutation of the input (XOR and wrapping sum unchanged).
+    # bucket bounds; 30000 extra keys in one prefix make that bucket too
+    # large for the LDS segment -- the segment sort records it and the plan
+    # finishes it on the device (sort.hip: the oversized-bucket finish, or
+    # the whole-array LSD beyond its bucket limit).  Checked on the device:
+    # ordered, and a permutation of the input (XOR and wrapping sum unchanged).
     n = 1 << 30
     keys = hpx.vector(n, dtype=np.uint64, tgt=gpu_target)
     P.generate(pol, keys.begin(), keys.end(), "bits", 9)

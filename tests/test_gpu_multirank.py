@@ -1,4 +1,4 @@
-"""Two ranks on the GPU: the product engine (HipEngine: radix sort, sorted-
+"""Two and four ranks on the GPU: the product engine (HipEngine: radix sort, sorted-
 range searches, merge, heat steps, reduce/scan/fold kernels) driven by the
 multi-rank orchestration of hpx_amd.segmented, with both processes on
 cuda:0.  RCCL refuses two ranks on one device, so the collectives here go
@@ -82,9 +82,10 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("size,backend", [(2, "gloo"), (1, "nccl")])
+@pytest.mark.parametrize("size,backend", [(2, "gloo"), (4, "gloo"), (1, "nccl")])
 def test_ranks_on_gpu_segmented_sort_reduce_scan_stencil(gpu_target, size, backend):
-    """size 2: two processes on cuda:0, collectives host-staged over gloo;
+    """size 2 and 4: processes sharing cuda:0, collectives host-staged over
+    gloo (4 ranks: 3 sort cuts, 2 merge rounds, a 4-rank halo ring);
     size 1 over RCCL: the same orchestration through the product's
     TorchComm (RCCL all-gathers on device buffers, all_to_all_single into
     destination views, the halo ring's batch_isend_irecv to itself) -- the
@@ -97,7 +98,7 @@ def test_ranks_on_gpu_segmented_sort_reduce_scan_stencil(gpu_target, size, backe
     procs = [ctx.Process(target=_worker, args=(r, size, port, q, backend)) for r in range(size)]
     for p in procs:
         p.start()
-    results = dict(q.get(timeout=110) for _ in range(size))
+    results = dict(q.get(timeout=240) for _ in range(size))
     for p in procs:
         p.join(timeout=30)
     for r in range(size):

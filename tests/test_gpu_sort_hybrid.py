@@ -3,8 +3,9 @@ on the device (sort.hip k_sort_plan): two onesweep passes on the prefix --
 the top byte and the 9 bits under it (17-bit form) or the two top live bytes
 (16-bit form) --, bucket bounds by lower_bound over buckets of the top byte
 plus b2 bits, b2 chosen from the histograms, one LDS-resident sort per
-bucket (512- or 1024-thread segments); a bucket over its segment's capacity
-sends the whole sort to the LSD over the live digits.  Checked element for
+bucket (512- or 1024-thread segments); up to 64 buckets over their
+segment's capacity are finished by a segmented LSD over their own ranges,
+more send the whole array through the LSD over the live digits.  Checked element for
 element against the oracle on the distributions that steer it down each
 branch, in every form (HPXHIP_SORT_HYBRID=17 / 16 / 18; 18: two 9-bit
 prefix passes and ~4096-key buckets).  Sizes start at the
@@ -75,8 +76,8 @@ def test_constant_middle_digits(pol, gpu_target):
 
 def test_few_oversized_buckets(pol, gpu_target):
     # one prefix (0x12, 0x34) holds 30000 extra keys: its bucket exceeds the LDS
-    # segment (18432 keys) and is finished by per-bucket LSD; the marginal
-    # histograms alone do not reveal it
+    # segment and is finished by the segmented LSD over its own range (r05);
+    # the marginal histograms alone do not reveal it
     rng = np.random.default_rng(12)
     n = 1 << 23
     h = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
@@ -85,8 +86,29 @@ def test_few_oversized_buckets(pol, gpu_target):
     check(pol, gpu_target, h)
 
 
+@pytest.mark.parametrize("desc", [False, True])
+def test_several_oversized_buckets(pol, gpu_target, desc):
+    """r05: up to kMaxBig (64) oversized buckets are finished by a segmented
+    LSD over just their ranges (sort.hip k_sort_fallback): 11 hot prefixes of
+    very different sizes (one barely over a segment, one of n/8 keys), with
+    duplicates inside and keys at both ends of the key range."""
+    rng = np.random.default_rng(21)
+    n = 1 << 23
+    h = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    o = 0
+    for i, m in enumerate([19000, 25000, 40000, 70000, n // 8, 9000, 12000, 30000, 5000, 100000, 20000]):
+        prefix = np.uint64((0x0000 + 0x1777 * (i + 1)) & 0xFFFF) << np.uint64(48)
+        h[o:o + m] = prefix | rng.integers(0, 1 << 48, m, dtype=np.uint64)
+        h[o:o + m // 50] = prefix | np.uint64(7)  # a run of duplicates in the bucket
+        o += m
+    h[o] = np.uint64(0)
+    h[o + 1] = np.uint64(2**64 - 1)
+    check(pol, gpu_target, h, desc)
+
+
 def test_many_oversized_buckets(pol, gpu_target):
-    # digit 6 == digit 7 for every key: 256 buckets of 32K keys -> plain LSD finish
+    # digit 6 == digit 7 for every key: 256 buckets of 32K keys, more than the
+    # 64 the segmented finish keeps -> the whole-array LSD
     rng = np.random.default_rng(13)
     n = 1 << 23
     top = rng.integers(0, 256, n, dtype=np.uint64)

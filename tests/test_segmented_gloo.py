@@ -122,7 +122,8 @@ def _layout_worker(rank, size, port, q):
         ones = np.ones(n, np.int64)
         x = O.generate(np.int64, "range", n, 0x5EED, -1000, 1000)
         xf = O.generate(np.float64, "unit", n, 0x5EED)
-        for name, lay in (("default", CL), ("3", CL(3)), ("10", CL(10)), ("1000", CL(1000)), ("1", CL(1))):
+        for name, lay in (("default", CL), ("3", CL(3)), ("8", CL(8)), ("10", CL(10)), ("13", CL(13)),
+                          ("1000", CL(1000)), ("1", CL(1))):
             pv = HostPV(ones, comm, lay)
             res[("reduce_ones", name)] = alg.reduce(None, pv.begin(), pv.end(), 1, F.plus)
             pf = HostPV(xf, comm, lay)
@@ -198,7 +199,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("size", [2, 3])
+@pytest.mark.parametrize("size", [2, 3, 8])
 def test_segmented_algorithms_gloo(size):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -238,7 +239,7 @@ def test_segmented_algorithms_gloo(size):
     np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), sel)
 
 
-@pytest.mark.parametrize("size", [2, 3])
+@pytest.mark.parametrize("size", [2, 3, 8])
 def test_partitioned_vector_layouts_gloo(size):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -253,7 +254,7 @@ def test_partitioned_vector_layouts_gloo(size):
     n = 10007
     x = O.generate(np.int64, "range", n, 0x5EED, -1000, 1000)
     xf = O.generate(np.float64, "unit", n, 0x5EED)
-    for name, k in (("default", size), ("3", 3), ("10", 10), ("1000", 1000), ("1", 1)):
+    for name, k in (("default", size), ("3", 3), ("8", 8), ("10", 10), ("13", 13), ("1000", 1000), ("1", 1)):
         for r in range(size):
             assert results[r][("reduce_ones", name)] == n + 1
             # FP: the segment-order fold of the reference (init (+) S_0 (+) ... over k segments)

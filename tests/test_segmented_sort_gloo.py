@@ -1,4 +1,4 @@
-"""Segmented sort across ranks on CPU (gloo, world sizes 2-4): the exact
+"""Segmented sort across ranks on CPU (gloo, world sizes 2-4 and 8): the exact
 global cut (radix select over ordered key bits + rank-order split of equal
 keys), the uneven all-to-all and the pairwise merge rounds of
 hpx_amd.segmented.segmented.sort.  The per-partition kernels are replaced by
@@ -52,6 +52,9 @@ class SortEngine:
         v = _ordered(np.asarray(values, vec.dtype), desc)
         return np.searchsorted(keys, v, side="right" if upper else "left").astype(np.int64)
 
+    def read_ranges(self, vec, starts, counts):
+        return [vec[int(a):int(a) + int(c)].copy() for a, c in zip(starts, counts)]
+
     def buffer(self, like, n):
         return np.zeros(max(1, n), like.dtype)
 
@@ -92,21 +95,49 @@ def cases():
         "i32_small": np.array([5, -1, 3], np.int32),
         "f32": rng.standard_normal(2048).astype(np.float32),
         "empty": np.zeros(0, np.int64),
+        # r05: 8-rank cases -- fewer keys than ranks, a few keys per rank,
+        # uniform 64-bit keys (the 2-round-trip select), repeated wide keys
+        # straddling the cuts (gathered blocks with equal keys)
+        "i64_five": np.array([9, -3, 9, 0, -3], np.int64),
+        "u64_thirteen": rng.integers(0, 2 ** 63, 13, dtype=np.uint64),
+        "u64_uniform": O.generate(np.uint64, "bits", 200003, 11),
+        "i64_wide_dups": np.repeat(rng.integers(-2 ** 62, 2 ** 62, 9000, dtype=np.int64), 3),
     }
+
+
+class CountingComm:
+    """The product comm, counting the host-level exchanges of the select."""
+    def __init__(self, comm):
+        self.comm = comm
+        self.rounds = 0
+
+    def __getattr__(self, name):
+        return getattr(self.comm, name)
+
+    def allreduce_host(self, words):
+        self.rounds += 1
+        return self.comm.allreduce_host(words)
+
+    def allgather_host(self, words):
+        self.rounds += 1
+        return self.comm.allgather_host(words)
 
 
 def _worker(rank, size, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=size)
     try:
-        comm = S.TorchComm(None, memory="host")  # the product comm over host buffers
-        alg = S.segmented(SortEngine())
+        comm = CountingComm(S.TorchComm(None, memory="host"))  # the product comm over host buffers
         res = {}
-        for name, x in cases().items():
-            for desc in (False, True):
-                pv = HostPV(x, comm)
-                alg.sort(None, pv.begin(), pv.end(), F.greater if desc else F.less)
-                res[(name, desc)] = (pv.lo, pv.local.copy())
+        for gather in (S.segmented.SELECT_GATHER, 16):  # the shipped block size, and one forcing more rounds
+            alg = S.segmented(SortEngine())
+            alg.SELECT_GATHER = gather
+            for name, x in cases().items():
+                for desc in (False, True):
+                    pv = HostPV(x, comm)
+                    comm.rounds = 0
+                    alg.sort(None, pv.begin(), pv.end(), F.greater if desc else F.less)
+                    res[(gather, name, desc)] = (pv.lo, pv.local.copy(), comm.rounds)
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -120,7 +151,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("size", [2, 3, 4])
+@pytest.mark.parametrize("size", [2, 3, 4, 8])
 def test_segmented_sort_gloo(size):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -132,16 +163,22 @@ def test_segmented_sort_gloo(size):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for name, x in cases().items():
-        for desc in (False, True):
-            got = np.zeros_like(x)
-            sizes = []
-            for r in range(size):
-                lo, loc = results[r][(name, desc)]
-                got[lo:lo + loc.size] = loc
-                sizes.append(loc.size)
-            # partition sizes unchanged (partitioned_vector_impl.hpp:325) and
-            # the concatenation is the oracle sort bit for bit
-            assert sizes == [b - a for a, b in (S.partition_bounds(x.size, size, k) for k in range(size))]
-            exp = O.sort(x, desc)
-            np.testing.assert_array_equal(got.view(np.uint8), exp.view(np.uint8), err_msg=f"{name} desc={desc}")
+    for (gather, name, desc) in results[0]:
+        x = cases()[name]
+        got = np.zeros_like(x)
+        sizes = []
+        for r in range(size):
+            lo, loc, rounds = results[r][(gather, name, desc)]
+            got[lo:lo + loc.size] = loc
+            sizes.append(loc.size)
+        if name == "u64_uniform" and gather == S.segmented.SELECT_GATHER:
+            # one all-reduce round of 16-bit digits, then the gathered blocks
+            assert rounds == 2, rounds
+        # at most 4 digit rounds + the gather for 64-bit keys
+        assert rounds <= 5, (name, rounds)
+        # partition sizes unchanged (partitioned_vector_impl.hpp:325) and
+        # the concatenation is the oracle sort bit for bit
+        assert sizes == [b - a for a, b in (S.partition_bounds(x.size, size, k) for k in range(size))]
+        exp = O.sort(x, desc)
+        np.testing.assert_array_equal(got.view(np.uint8), exp.view(np.uint8),
+                                      err_msg=f"{name} desc={desc} gather={gather}")

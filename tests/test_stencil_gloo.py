@@ -1,4 +1,4 @@
-"""examples/1d_stencil over a partitioned periodic ring on CPU (gloo, 1-3
+"""examples/1d_stencil over a partitioned periodic ring on CPU (gloo, 1-4 and 8
 ranks): the halo ring, the double-buffered halo slots and the edge /
 exchange / interior ordering of hpx_amd.segmented.heat_solver, against the
 serial oracle (1d_stencil_1.cpp:41-72).  Per-partition kernels are replaced
@@ -76,7 +76,10 @@ class HeatEngine:
 # (nx, nt, initial state, halo width cap: None = HALO_MAX fused steps per pass,
 # 1 = one step per exchange as in 1d_stencil_8, 4 = four)
 CASES = [(1001, 25, "ramp", None), (1001, 25, "random", None), (9, 7, "random", None), (64, 40, "random", None),
-         (1001, 11, "random", 1), (1001, 13, "random", 4), (37, 9, "random", None), (1001, 30, "gen", None)]
+         (1001, 11, "random", 1), (1001, 13, "random", 4), (37, 9, "random", None), (1001, 30, "gen", None),
+         # r05, for the 8-rank ring: 25-point partitions (W = 16 halos), and 17-point partitions whose last
+         # one (11 points) is shorter than HALO_MAX (passes of <= 11 steps)
+         (200, 40, "random", None), (130, 33, "random", None)]
 GEN = ("unit", 0xC0FFEE)  # device-generated state: splitmix64(seed ^ global i) in [0, 1)
 
 
@@ -130,7 +133,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("size", [1, 2, 3, 4])
+@pytest.mark.parametrize("size", [1, 2, 3, 4, 8])
 def test_heat_solver_ring_gloo(size, tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
