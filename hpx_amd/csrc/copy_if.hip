@@ -9,7 +9,10 @@
 // (lookback.hpp), and hits are written to out[prefix + rank]: each wave
 // round's hits are compacted through LDS and stored by consecutive lanes.
 // Input loads are nontemporal.  Traffic: 8 B read + 8 B x selectivity
-// written per int64 element.
+// written per int64 element.  Aligned inputs (r05) run the pipelined form,
+// k_copy_if_pipe: one persistent workgroup per CU stages a tile's hits in
+// LDS and issues the next tile's loads before its look-back and write-out;
+// misaligned ones (element-wise loads) keep one tile per workgroup.
 #include <cstdlib>
 
 #include "internal.hpp"
@@ -86,10 +89,21 @@ int launch_copy_if_sv(const T* in, T* out, uint64_t n, P p, uint64_t* count_dev,
     // (copy_if_kernel.hpp): 2.18-2.20 -> 2.13-2.15 ms at 2^30 int64
     constexpr bool kWide = sizeof(T) == 8 && ALIGNED;
     constexpr bool kOneHop = sizeof(T) == 8;
-    hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId, kNtStore, kRpb, kFixed, kThreads, kWide, kOneHop>), dim3(static_cast<unsigned>(ntiles)),
-                       dim3(kThreads), 0, s, in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles,
-                       prefix0);
-    HPXHIP_CHECK_LAUNCH();
+    if constexpr (ALIGNED) {
+        // r05: the pipelined persistent form (copy_if_kernel.hpp), one
+        // workgroup per CU: 2^30 int64 at 50 % hits 2.13-2.14 -> 1.96-1.97 ms,
+        // 2^31 int32 2.26-2.28 -> 2.15 (profiles/r05_ubench_copyif9.log)
+        const uint64_t grid = std::min<uint64_t>(ntiles, static_cast<uint64_t>(current_device_info().cus));
+        hipLaunchKernelGGL((k_copy_if_pipe<T, P, R, SV>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, in,
+                           out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles, prefix0);
+        HPXHIP_CHECK_LAUNCH();
+    } else {
+        hipLaunchKernelGGL((k_copy_if<T, P, ALIGNED, R, kMinWaves, 0, SV, kDynId, kNtStore, kRpb, kFixed, kThreads,
+                                      kWide, kOneHop>),
+                           dim3(static_cast<unsigned>(ntiles)), dim3(kThreads), 0, s, in, out, n, p, count_dev,
+                           reinterpret_cast<uint32_t*>(ws), st, ntiles, prefix0);
+        HPXHIP_CHECK_LAUNCH();
+    }
     return 0;
 }
 

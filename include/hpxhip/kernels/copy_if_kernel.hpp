@@ -222,6 +222,156 @@ __global__ __launch_bounds__(THREADS, MINW) void k_copy_if(const T* in, T* out, 
     }
 }
 
+// Pipelined form (r05, aligned input): a persistent grid of one 1024-thread
+// workgroup per CU walks tiles claimed in order from `counter`.  A tile's
+// hits are compacted into LDS (the whole tile, 128 KiB), then the next
+// tile's loads are issued into the registers the tile just left, and only
+// then does the workgroup take the tile's look-back and store its hits from
+// LDS -- so a CU's write-out and look-back run under its next tile's reads
+// instead of between them (k_copy_if holds the tile in registers until its
+// write-out, and two of them per CU fall into step).  Tiles are claimed in
+// order, so every look-back waits only on tiles already claimed by running
+// workgroups (forward progress without co-residency).  Same tile shape,
+// look-back and output as k_copy_if<..., FIXED, ONEHOP>.
+template <typename T, typename Pred, int ROUNDS, typename SV, int MINW = 4>
+__global__ __launch_bounds__(kThreads, MINW) void k_copy_if_pipe(const T* in, T* out, uint64_t n, Pred pred,
+                                                                 uint64_t* count_dev, uint32_t* counter,
+                                                                 tile_state<SV> st, uint64_t ntiles,
+                                                                 const uint64_t* prefix0 = nullptr) {
+    constexpr int V = 16 / sizeof(T);
+    constexpr uint64_t TILE = tile_elems<T, ROUNDS>();
+    constexpr uint64_t WAVE_ELEMS = TILE / kWaves;
+    using VT = vec<T, V>;
+    using H = hit_word<ROUNDS * V>;
+    static_assert(ROUNDS * V <= 64, "hit bits per lane");
+
+    __shared__ T s_stage[TILE];
+    __shared__ uint32_t s_wave_total[kWaves];
+    __shared__ uint32_t s_next;
+    __shared__ uint64_t s_prefix;
+
+    const int wave = threadIdx.x / kWave;
+    const int lane = lane_id();
+    auto claim = [&] {
+        if (threadIdx.x == 0)
+            s_next = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    VT x[ROUNDS];
+    auto load = [&](uint64_t t) {
+        const uint64_t wbase = t * TILE + wave * WAVE_ELEMS;
+        if (wbase + WAVE_ELEMS <= n) {
+            const VT* src = reinterpret_cast<const VT*>(in + wbase);
+#pragma unroll
+            for (int r = 0; r < ROUNDS; ++r) x[r] = ld_stream(&src[r * kWave + lane]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < ROUNDS; ++r)
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    const uint64_t i = wbase + (static_cast<uint64_t>(r) * kWave + lane) * V + e;
+                    x[r].v[e] = i < n ? in[i] : T(0);
+                }
+        }
+    };
+
+    claim();
+    __syncthreads();
+    uint64_t tile = s_next;
+    if (tile >= ntiles) return;
+    load(tile);
+    while (true) {
+        const uint64_t wbase = tile * TILE + wave * WAVE_ELEMS;
+        H hit = 0;
+        if (wbase + WAVE_ELEMS <= n) {
+#pragma unroll
+            for (int r = 0; r < ROUNDS; ++r)
+#pragma unroll
+                for (int e = 0; e < V; ++e) hit |= static_cast<H>(pred(x[r].v[e])) << (r * V + e);
+        } else {
+#pragma unroll
+            for (int r = 0; r < ROUNDS; ++r)
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    const uint64_t i = wbase + (static_cast<uint64_t>(r) * kWave + lane) * V + e;
+                    hit |= static_cast<H>(i < n && pred(x[r].v[e])) << (r * V + e);
+                }
+        }
+        const uint32_t wave_count = wave_reduce(static_cast<uint32_t>(__builtin_popcountll(hit)), op_plus{});
+        if (lane == 0) s_wave_total[wave] = wave_count;
+        claim();
+        __syncthreads();  // (A) wave totals, the next tile id
+        uint32_t wave_prefix = 0, agg = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            if (w < wave) wave_prefix += s_wave_total[w];
+            agg += s_wave_total[w];
+        }
+        if (tile > 0 && threadIdx.x == 0) st.publish(tile, static_cast<SV>(agg), TILE_AGGREGATE);
+        // compaction: the wave's hits in segment order (round, lane, element)
+        uint32_t rb = wave_prefix;
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) {
+            uint32_t cnt = 0, below = 0;
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const uint64_t m = __ballot((hit >> (r * V + e)) & 1u);
+                below += rank_below(m);
+                cnt += static_cast<uint32_t>(__builtin_popcountll(m));
+            }
+            uint32_t lb = 0;
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+                if ((hit >> (r * V + e)) & 1u) s_stage[rb + below + lb++] = x[r].v[e];
+            rb += cnt;
+        }
+        const uint64_t next = s_next;
+        __syncthreads();  // (B) the tile's hits are in LDS; x is free
+        if (next < ntiles) load(next);
+        if (wave == 0) {
+            SV p = 0;
+            if (tile == 0) {
+                if (prefix0) p = static_cast<SV>(*prefix0);
+                if (lane == 0) {
+                    st.publish(0, static_cast<SV>(agg), TILE_AGGREGATE);
+                    st.publish(0, p, TILE_INCLUSIVE);
+                }
+            } else {
+                p = st.template exclusive_prefix_fixed<true>(tile, op_plus{});
+            }
+            if (lane == 0) {
+                s_prefix = p;
+                if (tile == ntiles - 1) *count_dev = static_cast<uint64_t>(p) + agg;
+            }
+        }
+        __syncthreads();  // (C) the tile's output offset
+        // write-out: a head up to the output's next 16-B boundary, whole
+        // 16-B vectors, a tail
+        T* o = out + s_prefix;
+        const uint32_t head =
+            agg ? min(agg, static_cast<uint32_t>(((16u - (reinterpret_cast<uintptr_t>(o) & 15u)) & 15u) / sizeof(T)))
+                : 0u;
+        const uint32_t nvec = (agg - head) / V;
+        const uint32_t tail = agg - head - nvec * V;
+        if (threadIdx.x < head) o[threadIdx.x] = s_stage[threadIdx.x];
+        else if (threadIdx.x >= 64 && threadIdx.x - 64 < tail) {
+            const uint32_t j = head + nvec * V + (threadIdx.x - 64);
+            o[j] = s_stage[j];
+        }
+#pragma unroll
+        for (int k = 0; k < static_cast<int>(TILE / V / kThreads); ++k) {
+            const uint32_t q = k * kThreads + threadIdx.x;
+            if (q < nvec) {
+                VT w;
+#pragma unroll
+                for (int e = 0; e < V; ++e) w.v[e] = s_stage[head + q * V + e];
+                st_stream(reinterpret_cast<VT*>(o + head) + q, w);
+            }
+        }
+        if (next >= ntiles) break;
+        tile = next;
+    }
+}
+
 // Head of a misaligned input (fewer than 16 B of elements): compacted by one
 // thread into out[0..c), c -> *count; the aligned kernel continues from c.
 template <typename T, typename Pred>

@@ -389,12 +389,16 @@ def test_copy_if_predicates(pol, gpu_target, pred, name, arg):
 
 @pytest.mark.parametrize("dt,n,sel", [(np.int64, (64 * 3 + 5) * 16384 + 777, 0.5), (np.float64, (64 * 2 + 40) * 16384, 0.5),
                                       (np.int64, (64 * 2 + 1) * 16384 + 1, 0.97), (np.int64, 64 * 16384 * 2 + 3, 0.02),
-                                      (np.int32, (64 * 3 + 5) * 32768 + 9, 0.5)])
+                                      (np.int32, (64 * 3 + 5) * 32768 + 9, 0.5),
+                                      (np.int64, 1000 * 16384 + 4321, 0.5), (np.int64, 777 * 16384, 1.0),
+                                      (np.int64, 600 * 16384 + 3, 0.0), (np.int32, 700 * 32768 + 5, 0.5),
+                                      (np.int32, 530 * 32768 + 2, 1.0)])
 def test_copy_if_lookback_groups(pol, gpu_target, dt, n, sel):
     """Several 64-tile look-back groups and a partial last one (16384-element
-    8-byte tiles: the one-hop look-back and 16-B stores; 32768-element int32
-    tiles: the two-hop form), near-empty and near-full selections, and an
-    output that starts 8 B past a 16-B boundary."""
+    8-byte tiles, 32768-element 4-byte tiles), empty, near-empty, near-full
+    and full selections, and an output that starts 8 B past a 16-B boundary.
+    From 600 tiles on, each persistent workgroup of the pipelined form (one
+    per CU) walks several tiles: a full tile's hits fill its LDS stage."""
     rng = np.random.default_rng(n)
     a = (rng.random(n) < sel).astype(np.int64) * 2 - 1  # +1 selected, -1 not
     a = (a * rng.integers(1, 1000, n)).astype(dt)
