@@ -69,7 +69,7 @@ struct tile_shape {
     static constexpr int tile = threads * items;
 };
 
-// tiles per k_hist_tiles workgroup (chunk of the per-tile offset scan)
+// tiles per chunk of the per-tile offset scan (k_chunk_sums, k_tile_offsets)
 constexpr uint64_t kTileChunk = 256;
 
 struct sort_layout {
@@ -636,11 +636,13 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     const bool pre18 = takes_pre18(n, HAS_VAL ? sizeof(VAL) : 0, TS::tile);
     auto* tcount = reinterpret_cast<uint32_t*>(base + L.tcount);
     auto* csum = reinterpret_cast<uint32_t*>(base + L.csum);
+    // (r05: tiles strided over 2 workgroups per CU; the chunk totals for the
+    // offsets come from k_chunk_sums)
     if (pre18)
-        hipLaunchKernelGGL((k_hist_tiles<U, X, 8192, kXBins>), dim3(static_cast<unsigned>(L.nchunks)), dim3(kXBins), 0,
-                           s, kc, n, L.ntiles, static_cast<uint32_t>(kTileChunk), X{}, field18_shift<U>(),
-                           top9_shift<U>(), tcount, csum, xhist, thist, bits,
-                           reinterpret_cast<unsigned long long*>(base + L.joint));
+        hipLaunchKernelGGL((k_hist_tiles<U, X, 8192, kXBins>),
+                           dim3(static_cast<unsigned>(std::min<uint64_t>(L.ntiles, 2ull * current_device_info().cus))),
+                           dim3(kXBins), 0, s, kc, n, L.ntiles, X{}, field18_shift<U>(), top9_shift<U>(), tcount, xhist,
+                           thist, bits, reinterpret_cast<unsigned long long*>(base + L.joint));
     else if (mode == 18)  // the field and the top 9 bits; no byte digit
         hipLaunchKernelGGL((k_hist<U, X, kHistThreads, 4, 2, true>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n,
                            first, passes, X{}, hist, bits, field18_shift<U>(), xhist,
@@ -683,6 +685,9 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     // ---- hybrid: prefix passes (keys -> alt -> keys), bucket bounds, per-bucket LDS sort
     if (mode) {
         if (pre18) {  // the first prefix pass's tile offsets, iff the plan takes it
+            hipLaunchKernelGGL(k_chunk_sums, dim3(static_cast<unsigned>(L.nchunks)), dim3(kXBins), 0, s, tcount,
+                               L.ntiles, static_cast<uint32_t>(kTileChunk), csum, ctl + C_A9);
+            HPXHIP_CHECK_LAUNCH();
             hipLaunchKernelGGL(k_tile_chunk_scan, dim3(1), dim3(kXBins), 0, s, csum, L.nchunks, xstart, ctl + C_A9);
             HPXHIP_CHECK_LAUNCH();
             hipLaunchKernelGGL(k_tile_offsets, dim3(static_cast<unsigned>(L.nchunks)), dim3(kXBins), 0, s, tcount,

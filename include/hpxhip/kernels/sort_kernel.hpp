@@ -200,19 +200,17 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
 // the first pass's tiles are the input's own: their digit counts can come out
 // of the histogram read that precedes the pass.  Measured: the pass 5.3-5.5
 // -> 5.1 ms, the sort 2^30 u64 18.0 -> 17.6 ms, u32 13.2 -> 12.6.  k_hist_tiles reads the keys
-// once, in the onesweep's 8192-key tiles, CHUNK consecutive tiles per
-// workgroup, and writes
+// once, in the onesweep's 8192-key tiles (strided over the grid), and writes
 //   tcount[t * 512 + d]  tile t's count of field digit d,
-//   csum[c * 512 + d]    chunk c's total of digit d,
 // plus the field's and the top 9 bits' histograms and the keys' OR / AND (what
-// k_hist<..., TF> gives).  k_tile_chunk_scan turns the chunk totals into
+// k_hist<..., TF> gives).  k_chunk_sums (r05) totals the tile counts per
+// chunk of kTileChunk tiles, k_tile_chunk_scan turns the chunk totals into
 // exclusive prefixes (from the digits' bin starts), k_tile_offsets the tile
 // counts into each tile's destination offsets, which the pass reads instead
 // of walking back (k_onesweep PRE).  Offsets are 32-bit: n < 2^32.
 template <typename U, typename X, int TILE = 8192, int THREADS = 512>
 __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ keys, uint64_t n, uint64_t ntiles,
-                                                         uint32_t chunk, X xf, int xshift, int tshift,
-                                                         uint32_t* __restrict__ tcount, uint32_t* __restrict__ csum,
+                                                         X xf, int xshift, int tshift, uint32_t* __restrict__ tcount,
                                                          unsigned long long* __restrict__ xhist,
                                                          unsigned long long* __restrict__ thist,
                                                          unsigned long long* __restrict__ bits,
@@ -236,13 +234,22 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
     const bool aligned = reinterpret_cast<uintptr_t>(keys) % 16 == 0;
     U any = 0, all = static_cast<U>(~U(0));
     uint32_t csum_d = 0;
-    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * chunk;
-    const uint64_t t1 = t0 + chunk < ntiles ? t0 + chunk : ntiles;
-    // The (field, top-9) cells of the first two lanes still to add are added
-    // once per wave, for all lanes that share them; the other lanes add one
-    // each (r05: sorted or heavily skewed input -- a hot prefix in the first
-    // tiles -- had serialized the lanes of a wave on one or two LDS words:
-    // the histogram took 2.9 ms at 2^28 u64hot against 0.42 for uniform keys)
+    // A (field, top-9) cell that the first lane still to add shares with at
+    // least 4 lanes of its wave is counted once, for all of them, up to three
+    // such cells per key; the other lanes add one each (r05: sorted or
+    // heavily skewed input -- a hot prefix in the first tiles -- had
+    // serialized the lanes of a wave on one or two LDS words: the histogram
+    // took 2.9 ms at 2^28 u64hot against 0.42 for uniform keys).  Those
+    // shared counts go to a two-entry per-wave cache (scalar registers) and
+    // reach LDS only when evicted or at the tile's end: the waves of a
+    // workgroup no longer take turns on the same hot words.  Uniform keys pay
+    // one readlane + compare + ballot per key (peeling the first two lanes'
+    // cells unconditionally had cost them 4x: 1.75 ms at 2^28).
+    uint32_t cc0 = ~0u, cc1 = ~0u, cn0 = 0, cn1 = 0;
+    auto add_cell = [&](uint32_t c, uint32_t v) {
+        atomicAdd(&cnt[c >> 12], v);
+        atomicAdd(&hj[c & 0xfffu], v);
+    };
     auto count = [&](U b) {
         any |= b;
         all &= b;
@@ -251,24 +258,34 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
         const uint32_t cell = (f << 12) | j;
         uint64_t rem = __ballot(1);
 #pragma unroll
-        for (int it = 0; it < 2; ++it) {
+        for (int it = 0; it < 3; ++it) {
             if (rem == 0) break;
             const int lead = __builtin_ctzll(rem);
             const uint32_t c0 = __builtin_amdgcn_readlane(cell, lead);
             const uint64_t grp = __ballot(cell == c0) & rem;
-            if (lane_id() == lead) {
-                const uint32_t c = static_cast<uint32_t>(__builtin_popcountll(grp));
-                atomicAdd(&cnt[c0 >> 12], c);
-                atomicAdd(&hj[c0 & 0xfffu], c);
+            const uint32_t c = static_cast<uint32_t>(__builtin_popcountll(grp));
+            if (c < 4) break;
+            if (c0 == cc0) {
+                cn0 += c;
+            } else if (c0 == cc1) {
+                cn1 += c;
+            } else {
+                if (cn1 && lane_id() == lead) add_cell(cc1, cn1);
+                cc1 = cc0;
+                cn1 = cn0;
+                cc0 = c0;
+                cn0 = c;
             }
             rem &= ~grp;
         }
-        if ((rem >> lane_id()) & 1u) {
-            atomicAdd(&cnt[f], 1u);
-            atomicAdd(&hj[j], 1u);
-        }
+        if ((rem >> lane_id()) & 1u) add_cell(cell, 1u);
     };
-    for (uint64_t t = t0; t < t1; ++t) {
+    // r05: tiles strided over the grid (workgroup w: tiles w, w + G, ...)
+    // instead of a chunk of consecutive tiles each: a hot run of keys (sorted
+    // or skewed input) no longer lands on a few workgroups that the whole
+    // launch then waits for, and a 2^28-key sort fills the chip (512
+    // workgroups against 128 chunks); the chunk totals come from k_chunk_sums
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t base = t * TILE;
         if (aligned && base + TILE <= n) {
             const VT* vk = reinterpret_cast<const VT*>(keys + base);
@@ -283,6 +300,14 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
             const uint64_t m = n - base < TILE ? n - base : TILE;
             for (uint64_t i = d; i < m; i += THREADS) count(xf(keys[base + i]));
         }
+        // lane 0 holds the wave's cache: in the ragged loop a lane that drops
+        // out never comes back, and lane 0 is the last of its wave to drop out
+        if (lane_id() == 0) {
+            if (cn0) add_cell(cc0, cn0);
+            if (cn1) add_cell(cc1, cn1);
+        }
+        cc0 = cc1 = ~0u;
+        cn0 = cn1 = 0;
         __syncthreads();
         const uint32_t c = cnt[d];
         tcount[t * kXBins + d] = c;
@@ -290,7 +315,6 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
         cnt[d] = 0;
         __syncthreads();
     }
-    csum[static_cast<uint64_t>(blockIdx.x) * kXBins + d] = csum_d;
     if (csum_d) atomicAdd(&xhist[d], static_cast<unsigned long long>(csum_d));
     uint32_t tc = 0;
 #pragma unroll
@@ -306,6 +330,28 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
         atomicOr(&bits[0], static_cast<unsigned long long>(any));
         atomicAnd(&bits[1], static_cast<unsigned long long>(all) | (sizeof(U) == 8 ? 0ull : ~0ull << 32));
     }
+}
+
+// Chunk totals of the tile counts (workgroup c: chunk c's tiles, thread d:
+// digit d); runs iff *gate >= 0.
+__global__ __launch_bounds__(kXBins) void k_chunk_sums(const uint32_t* __restrict__ tcount, uint64_t ntiles,
+                                                       uint32_t chunk, uint32_t* __restrict__ csum,
+                                                       const int32_t* __restrict__ gate) {
+    if (*gate < 0) return;
+    const int d = threadIdx.x;
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * chunk;
+    const uint64_t t1 = t0 + chunk < ntiles ? t0 + chunk : ntiles;
+    uint32_t sum = 0;
+    uint64_t t = t0;
+    for (; t + 8 <= t1; t += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = tcount[(t + j) * kXBins + d];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum += v[j];
+    }
+    for (; t < t1; ++t) sum += tcount[t * kXBins + d];
+    csum[static_cast<uint64_t>(blockIdx.x) * kXBins + d] = sum;
 }
 
 // Chunk totals -> exclusive prefixes from the field's bin starts (one
@@ -894,7 +940,7 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 // planned buckets (bucket b by workgroup b mod gridDim), so a launch the plan
 // skips costs one gate read per workgroup instead of one dispatch per bucket.
 template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16, typename VAL = uint32_t,
-          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false, int MINW = 4>
+          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false, int MINW = 4, bool PRE16 = false>
 __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
     void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf,
                        VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr,
@@ -920,6 +966,10 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     __shared__ uint16_t s_whist[WAVES][kRadix];
     __shared__ uint32_t s_wsum[kRadix / kWave];
     __shared__ U s_ends[2];
+    // PRE16 (r05): the second LDS pass also leaves each key's 16 sorted bits
+    // here, so the run detection reads 8 prefixes per 16-B LDS load instead
+    // of three 8-B keys per position
+    __shared__ alignas(16) uint16_t s_pre[PRE16 ? THREADS * ITEMS + 16 : 1];
 
     const int t_id = threadIdx.x;
     const int lane_ = lane_id();
@@ -1000,7 +1050,7 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     if (top <= 0) return;  // all keys equal
 
     // one stable pass on the digit at `shift`: registers -> s_keys (ranked)
-    auto pass = [&](int shift) {
+    auto pass = [&](int shift, bool keep_pre) {
         __syncthreads();  // earlier readers of s_keys / s_whist are done
         for (int i = t; i < WAVES * kRadix / 2; i += THREADS) reinterpret_cast<uint32_t*>(&s_whist[0][0])[i] = 0;
         __syncthreads();
@@ -1055,6 +1105,8 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
                 const uint32_t pos = s_whist[wave][d] + ((rank2[r / 2] >> (16 * (r & 1))) & 0xffffu);
                 s_keys[pos] = k[r];
                 if constexpr (HAS_VAL) s_vals[pos] = v[r];
+                if constexpr (PRE16)
+                    if (keep_pre) s_pre[pos] = static_cast<uint16_t>(xf(k[r]) >> (top - 16));
             }
         }
         __syncthreads();
@@ -1075,7 +1127,7 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     int npass = 2;
     for (int q = 0; q < npass;) {
         const int lo = lsd ? top - 8 * (npass - q) : top - 8 * (2 - q);
-        pass(lo > 0 ? lo : 0);
+        pass(lo > 0 ? lo : 0, !lsd && q == 1 && top > 16);
         if (++q < npass) {
             reload();
             continue;
@@ -1091,23 +1143,54 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
             const int fs = top - 16;
             auto pre = [&](const U& x) { return xf(x) >> fs; };
             uint32_t starts = 0;
-#pragma unroll 3
-            for (int j = 0; j < ITEMS; ++j) {
-                const uint32_t i = static_cast<uint32_t>(t) + static_cast<uint32_t>(j) * THREADS;
-                if (i + 1 < m) {
-                    const U a = pre(s_keys[i]);
-                    if (a == pre(s_keys[i + 1]) && (i == 0 || pre(s_keys[i - 1]) != a)) starts |= 1u << j;
+            constexpr int kGroups = (THREADS * ITEMS / 8 + THREADS - 1) / THREADS;  // PRE16: 8 positions per group
+            static_assert(!PRE16 || 8 * kGroups <= 32, "run starts: one bit per position");
+            if constexpr (PRE16) {
+                using P8 = vec<uint16_t, 8>;
+#pragma unroll
+                for (int j = 0; j < kGroups; ++j) {
+                    const uint32_t g = static_cast<uint32_t>(t) + static_cast<uint32_t>(j) * THREADS;
+                    const uint32_t base = 8 * g;
+                    if (base + 1 >= m) continue;
+                    const P8 w = reinterpret_cast<const P8*>(s_pre)[g];
+                    const uint16_t before = base > 0 ? s_pre[base - 1] : uint16_t(0);
+                    const uint16_t after = s_pre[base + 8];  // read only if base + 8 < m
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint32_t idx = base + i;
+                        const uint16_t a = w.v[i];
+                        const uint16_t nx = i < 7 ? w.v[i < 7 ? i + 1 : 7] : after;
+                        const uint16_t pv = i > 0 ? w.v[i > 0 ? i - 1 : 0] : before;
+                        if (idx + 1 < m && a == nx && (idx == 0 || pv != a)) starts |= 1u << (8 * j + i);
+                    }
                 }
+                // no barrier: the insertion below moves keys (s_keys), and
+                // the detection reads prefixes only (s_pre, equal along a run)
+            } else {
+#pragma unroll 3
+                for (int j = 0; j < ITEMS; ++j) {
+                    const uint32_t i = static_cast<uint32_t>(t) + static_cast<uint32_t>(j) * THREADS;
+                    if (i + 1 < m) {
+                        const U a = pre(s_keys[i]);
+                        if (a == pre(s_keys[i + 1]) && (i == 0 || pre(s_keys[i - 1]) != a)) starts |= 1u << j;
+                    }
+                }
+                __syncthreads();  // detection reads done before any run moves
             }
-            __syncthreads();  // detection reads done before any run moves
             int long_run = 0;
             while (starts) {
                 const int j = __builtin_ctz(starts);
                 starts &= starts - 1;
-                const uint32_t s = static_cast<uint32_t>(t) + static_cast<uint32_t>(j) * THREADS;
-                const U p0 = pre(s_keys[s]);
+                const uint32_t s = PRE16 ? 8 * (static_cast<uint32_t>(t) + static_cast<uint32_t>(j / 8) * THREADS) + j % 8
+                                         : static_cast<uint32_t>(t) + static_cast<uint32_t>(j) * THREADS;
                 uint32_t e = s + 2;  // the detection saw s + 1 in the run
-                while (e < m && e - s <= kRunMax && pre(s_keys[e]) == p0) ++e;
+                if constexpr (PRE16) {
+                    const uint16_t p0 = s_pre[s];
+                    while (e < m && e - s <= kRunMax && s_pre[e] == p0) ++e;
+                } else {
+                    const U p0 = pre(s_keys[s]);
+                    while (e < m && e - s <= kRunMax && pre(s_keys[e]) == p0) ++e;
+                }
                 if (e - s > kRunMax) {
                     long_run = 1;
                     continue;

@@ -87,9 +87,10 @@ int main() {
     CK(hipMemset(thist, 0, 512 * 8));
     CK(hipMemset(bits, 0, 8));
     CK(hipMemset(bits + 1, 0xff, 8));
-    hipLaunchKernelGGL((k_hist_tiles<uint64_t, X, 8192, kXBins>), dim3(nchunks), dim3(kXBins), 0, 0, kin, n, ntiles,
-                       uint32_t(chunk), X{}, 46, 55, tcount, csum, xhist, thist, bits, joint);
+    hipLaunchKernelGGL((k_hist_tiles<uint64_t, X, 8192, kXBins>), dim3(512), dim3(kXBins), 0, 0, kin, n, ntiles,
+                       X{}, 46, 55, tcount, xhist, thist, bits, joint);
     hipLaunchKernelGGL(k_bin_offsets<512>, dim3(1), dim3(512), 0, 0, xhist, xstart);
+    hipLaunchKernelGGL(k_chunk_sums, dim3(nchunks), dim3(kXBins), 0, 0, tcount, ntiles, uint32_t(chunk), csum, gate);
     hipLaunchKernelGGL(k_tile_chunk_scan, dim3(1), dim3(kXBins), 0, 0, csum, nchunks, xstart, gate);
     hipLaunchKernelGGL(k_tile_offsets, dim3(nchunks), dim3(kXBins), 0, 0, tcount, ntiles, uint32_t(chunk), csum, gate);
     CK(hipDeviceSynchronize());
