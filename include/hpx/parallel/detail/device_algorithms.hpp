@@ -33,6 +33,8 @@
 #include <hpx/compute/hip/detail/launch.hpp>
 #include <hpx/compute/hip/functional.hpp>
 
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <type_traits>
 #include <utility>
@@ -231,6 +233,23 @@ void copy_if_launch(compute::hip::target const& t, T const* in, T* out, uint64_t
     char* ws = static_cast<char*>(scratch(t, state, "copy_if scratch"));
     compute::hip::detail::check(hpxhip_memset_async(ws, 0, state, t.stream()), "copy_if scratch");
     K::tile_state<SV> st{reinterpret_cast<uint64_t*>(ws + 256), error_word(t)};
+    if constexpr (ALIGNED) {
+        // r05: the shipped pipelined form (copy_if.hip), one persistent
+        // workgroup per CU
+        static std::atomic<int> cus[64];
+        const int dev = t.device();
+        int c = dev >= 0 && dev < 64 ? cus[dev].load(std::memory_order_relaxed) : 0;
+        if (c <= 0) {
+            c = static_cast<int>(t.native_handle().processing_units());
+            if (dev >= 0 && dev < 64) cus[dev].store(c, std::memory_order_relaxed);
+        }
+        const uint64_t grid = std::min<uint64_t>(ntiles, static_cast<uint64_t>(c));
+        hipLaunchKernelGGL((C::k_copy_if_pipe<T, P, R, SV>), dim3(static_cast<unsigned>(grid)), dim3(C::kThreads), 0,
+                           stream_of(t), in, out, n, p, count_dev, reinterpret_cast<uint32_t*>(ws), st, ntiles,
+                           static_cast<const uint64_t*>(nullptr));
+        launched("copy_if (device closure)");
+        return;
+    }
     // blockIdx tile order with the fixed-association look-back (the shipped
     // choice for copy_if, copy_if.hip); 4 waves per SIMD: a user predicate
     // may need more than 64 VGPRs.  r04: the shipped kernel's 8-byte

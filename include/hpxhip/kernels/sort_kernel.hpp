@@ -220,7 +220,7 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
     constexpr int VPT = TILE / V / THREADS;  // 16-B vectors per thread per tile
     static_assert(VPT * V * THREADS == TILE, "tile of whole vectors");
     using VT = vec<U, V>;
-    __shared__ uint32_t cnt[kXBins];
+    __shared__ uint32_t cnt[2 * kXBins];
     // r05: the top 9 bits counted per field region (field >> 6: 8 regions of
     // 64 field digits) -- joint[region][top9], whose sum over the regions is
     // the top-9 histogram; the second prefix pass runs one region per XCD
@@ -228,6 +228,7 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
     __shared__ uint32_t hj[8 * kXBins];
     const int d = threadIdx.x;
     cnt[d] = 0;
+    cnt[kXBins + d] = 0;
 #pragma unroll
     for (int x = 0; x < 8; ++x) hj[x * kXBins + d] = 0;
     __syncthreads();
@@ -246,11 +247,11 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
     // one readlane + compare + ballot per key (peeling the first two lanes'
     // cells unconditionally had cost them 4x: 1.75 ms at 2^28).
     uint32_t cc0 = ~0u, cc1 = ~0u, cn0 = 0, cn1 = 0;
-    auto add_cell = [&](uint32_t c, uint32_t v) {
-        atomicAdd(&cnt[c >> 12], v);
+    auto add_cell = [&](uint32_t c, uint32_t v, uint32_t* ct) {
+        atomicAdd(&ct[c >> 12], v);
         atomicAdd(&hj[c & 0xfffu], v);
     };
-    auto count = [&](U b) {
+    auto count = [&](U b, uint32_t* ct) {
         any |= b;
         all &= b;
         const uint32_t f = static_cast<uint32_t>(b >> xshift) & (kXBins - 1);
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
             } else if (c0 == cc1) {
                 cn1 += c;
             } else {
-                if (cn1 && lane_id() == lead) add_cell(cc1, cn1);
+                if (cn1 && lane_id() == lead) add_cell(cc1, cn1, ct);
                 cc1 = cc0;
                 cn1 = cn0;
                 cc0 = c0;
@@ -278,42 +279,61 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
             }
             rem &= ~grp;
         }
-        if ((rem >> lane_id()) & 1u) add_cell(cell, 1u);
+        if ((rem >> lane_id()) & 1u) add_cell(cell, 1u, ct);
     };
     // r05: tiles strided over the grid (workgroup w: tiles w, w + G, ...)
     // instead of a chunk of consecutive tiles each: a hot run of keys (sorted
     // or skewed input) no longer lands on a few workgroups that the whole
     // launch then waits for, and a 2^28-key sort fills the chip (512
     // workgroups against 128 chunks); the chunk totals come from k_chunk_sums
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint64_t base = t * TILE;
-        if (aligned && base + TILE <= n) {
-            const VT* vk = reinterpret_cast<const VT*>(keys + base);
-            VT x[VPT];
+    // r05: the next tile's keys are loaded while this tile's are counted
+    // (x / xn; the grid has 2 workgroups per CU, so the registers are there),
+    // and the per-tile counts alternate between two LDS arrays, so one
+    // barrier per tile separates a tile's counting from its flush
+    auto full_tile = [&](uint64_t t) { return aligned && (t + 1) * TILE <= n; };
+    auto load = [&](VT (&dst)[VPT], uint64_t t) {
+        const VT* vk = reinterpret_cast<const VT*>(keys + t * TILE);
 #pragma unroll
-            for (int j = 0; j < VPT; ++j) x[j] = ld_stream(&vk[j * THREADS + d]);
+        for (int j = 0; j < VPT; ++j) dst[j] = ld_stream(&vk[j * THREADS + d]);
+    };
+    VT x[VPT];
+    uint64_t t = blockIdx.x;
+    if (t < ntiles && full_tile(t)) load(x, t);
+    int buf = 0;
+    for (; t < ntiles; t += gridDim.x) {
+        const uint64_t base = t * TILE;
+        const uint64_t tn = t + gridDim.x;
+        const bool pf = tn < ntiles && full_tile(tn);
+        VT xn[VPT];
+        if (pf) load(xn, tn);
+        uint32_t* ct = cnt + buf * kXBins;
+        if (full_tile(t)) {
 #pragma unroll
             for (int j = 0; j < VPT; ++j)
 #pragma unroll
-                for (int e = 0; e < V; ++e) count(xf(x[j].v[e]));
+                for (int e = 0; e < V; ++e) count(xf(x[j].v[e]), ct);
         } else {
             const uint64_t m = n - base < TILE ? n - base : TILE;
-            for (uint64_t i = d; i < m; i += THREADS) count(xf(keys[base + i]));
+            for (uint64_t i = d; i < m; i += THREADS) count(xf(keys[base + i]), ct);
         }
         // lane 0 holds the wave's cache: in the ragged loop a lane that drops
         // out never comes back, and lane 0 is the last of its wave to drop out
         if (lane_id() == 0) {
-            if (cn0) add_cell(cc0, cn0);
-            if (cn1) add_cell(cc1, cn1);
+            if (cn0) add_cell(cc0, cn0, ct);
+            if (cn1) add_cell(cc1, cn1, ct);
         }
         cc0 = cc1 = ~0u;
         cn0 = cn1 = 0;
-        __syncthreads();
-        const uint32_t c = cnt[d];
+        __syncthreads();  // the tile's counts are complete; the other array was flushed a tile ago
+        const uint32_t c = ct[d];
         tcount[t * kXBins + d] = c;
         csum_d += c;
-        cnt[d] = 0;
-        __syncthreads();
+        ct[d] = 0;  // counted into again two tiles on, after the next barrier
+        buf ^= 1;
+        if (pf) {
+#pragma unroll
+            for (int j = 0; j < VPT; ++j) x[j] = xn[j];
+        }
     }
     if (csum_d) atomicAdd(&xhist[d], static_cast<unsigned long long>(csum_d));
     uint32_t tc = 0;

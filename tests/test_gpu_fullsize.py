@@ -13,7 +13,9 @@ is_sorted (is_sorted.hpp).
   (exact prefix in 80-bit long double on the host), a bound that stays
   meaningful under cancellation;
 * sort of 2^30 uint64: a permutation of the input (XOR and wrapping sum of the
-  keys unchanged) with no adjacent pair out of order (device-side is_sorted)."""
+  keys unchanged) with no adjacent pair out of order (device-side is_sorted);
+  and (r05) element for element against a closed form: keys whose top bits
+  are a permutation of [0, n) (test_sort_2p30_element_exact)."""
 import ctypes
 
 import numpy as np
@@ -208,6 +210,74 @@ def test_sort_2p30_oversized_bucket(pol, gpu_target):
     assert P.is_sorted(pol, keys.begin(), keys.end())
     assert P.reduce(pol, keys.begin(), keys.end(), 0, F.bit_xor) == xor0
     assert P.reduce(pol, keys.begin(), keys.end(), 0, F.plus) == sum0
+    keys.free()
+
+
+_PERM_A, _PERM_B = 0x2545F491, 0x1234567  # i -> (A i + B) mod n: a bijection of [0, n) (A odd)
+_HASH_C = 0x9E3779B97F4A7C15 - (1 << 64)  # multiplicative hash (as int64)
+_CHUNK = 1 << 26
+
+
+def _perm_keys(lo, cnt, n, shift, dev):
+    """Bit patterns (int64) of the keys of indices [lo, lo + cnt): the top
+    bits hold a permutation of [0, n), the `shift` low bits a hash of the
+    index.  Computed with torch on the test's GPU (test plumbing: numpy took
+    ~3 s per 2^26 keys); int64 products wrap like uint64 ones."""
+    import torch
+    i = torch.arange(lo, lo + cnt, dtype=torch.int64, device=dev)
+    p = (i * _PERM_A + _PERM_B) & (n - 1)
+    h = ((i * _HASH_C) >> (64 - shift)) & ((1 << shift) - 1)
+    return (p << shift) | h
+
+
+def _perm_sorted(lo, cnt, n, shift, dev):
+    """Ascending positions [lo, lo + cnt) of the sorted keys, in closed form:
+    position j holds the key whose permuted top bits are j."""
+    import torch
+    j = torch.arange(lo, lo + cnt, dtype=torch.int64, device=dev)
+    i = ((j - _PERM_B) * pow(_PERM_A, -1, n)) & (n - 1)
+    h = ((i * _HASH_C) >> (64 - shift)) & ((1 << shift) - 1)
+    return (j << shift) | h
+
+
+@pytest.mark.parametrize("kdt,logn,desc", [(np.uint64, 30, False), (np.uint32, 30, False), (np.uint64, 28, True)])
+def test_sort_2p30_element_exact(pol, gpu_target, kdt, logn, desc):
+    """Element for element at the benchmark's size (weak item r04: the 2^30
+    sort had been checked by checksums and sortedness only): the keys' top
+    log2(n) bits are a permutation of [0, n) and the low bits a hash of the
+    index, so the sorted array has a closed form (_perm_sorted).  Keys are
+    made and checked in 2^26-key windows on the device with torch (D2D
+    copies in and out of the library's vector); the sort is the library's."""
+    import torch
+    dev = torch.device("cuda", gpu_target.device)
+    n = 1 << logn
+    isz = np.dtype(kdt).itemsize
+    shift = 8 * isz - logn
+    tdt = torch.int64 if isz == 8 else torch.int32
+
+    def narrow(x):  # int64 bit patterns -> the key width (exact: wrap 32-bit patterns to int32)
+        return x if isz == 8 else (x - ((x >> 31) & 1) * (1 << 32)).to(torch.int32)
+
+    keys = hpx.vector(n, dtype=kdt, tgt=gpu_target)
+    torch.cuda.synchronize(dev)
+    for lo in range(0, n, _CHUNK):
+        h = narrow(_perm_keys(lo, _CHUNK, n, shift, dev))
+        torch.cuda.synchronize(dev)
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(keys.data() + lo * isz), ctypes.c_void_p(h.data_ptr()),
+               h.numel() * isz, L.D2D, gpu_target.stream)
+        gpu_target.synchronize()
+    P.sort(pol, keys.begin(), keys.end(), F.greater if desc else F.less)
+    got = torch.empty(_CHUNK, dtype=tdt, device=dev)
+    for lo in range(0, n, _CHUNK):
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(got.data_ptr()), ctypes.c_void_p(keys.data() + lo * isz),
+               _CHUNK * isz, L.D2D, gpu_target.stream)
+        gpu_target.synchronize()
+        if desc:  # position lo + t holds ascending rank n - 1 - lo - t
+            exp = narrow(_perm_sorted(n - lo - _CHUNK, _CHUNK, n, shift, dev)).flip(0)
+        else:
+            exp = narrow(_perm_sorted(lo, _CHUNK, n, shift, dev))
+        bad = int((got != exp).sum())
+        assert bad == 0, (lo, bad)
     keys.free()
 
 
