@@ -26,7 +26,7 @@ B_ADD, B_TRIAD, B_SUB, B_MUL, B_AXPY, B_MIN, B_MAX = range(7)
 P_LT, P_LE, P_GT, P_GE, P_EQ, P_NE, P_NOT_LT, P_BITS = range(8)
 H2H, H2D, D2H, D2D, DEFAULT = range(5)
 GEN_IOTA, GEN_BITS, GEN_RANGE, GEN_UNIT = range(4)
-ALGO_REDUCE, ALGO_SCAN, ALGO_COPY_IF, ALGO_SORT, ALGO_SORT_BY_KEY, ALGO_MERGE = range(6)
+ALGO_REDUCE, ALGO_SCAN, ALGO_COPY_IF, ALGO_SORT, ALGO_SORT_BY_KEY, ALGO_MERGE, ALGO_MERGE_RUNS = range(7)
 STENCIL_MAX_FUSED = 16  # HPXHIP_STENCIL_MAX_FUSED
 
 SUCCESS = 0
@@ -162,6 +162,7 @@ SIGNATURES = {
     "hpxhip_sort": [_i, _vp, _u64, _i, _vp, _vp, _sz],
     "hpxhip_sort_by_key": [_i, _i, _vp, _vp, _u64, _i, _vp, _vp, _sz],
     "hpxhip_merge": [_i, _vp, _u64, _vp, _u64, _vp, _i, _vp, _vp, _sz],
+    "hpxhip_merge_runs": [_i, _vp, _vp, _i, _vp, _i, _vp, _vp, _sz],
     "hpxhip_unsorted_pairs": [_i, _vp, _u64, _i, _vp, _vp],
     "hpxhip_sorted_bounds": [_i, _vp, _u64, _vp, _u64, _i, _i, _vp, _vp],
     "hpxhip_stencil_heat_step": [_vp, _vp, _u64, _vp, _vp, _d, _d, _d, _vp],

@@ -318,5 +318,6 @@ size_t scan_scratch_bytes(int dtype, uint64_t n);
 size_t copy_if_scratch_bytes(int dtype, uint64_t n);
 size_t sort_scratch_bytes(int key_dtype, int value_dtype, uint64_t n);
 size_t merge_scratch_bytes(uint64_t n);
+size_t merge_runs_scratch_bytes(uint64_t n);
 
 }  // namespace hpxhip

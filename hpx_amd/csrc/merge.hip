@@ -74,10 +74,393 @@ int run_merge(const void* a, uint64_t na, const void* b, uint64_t nb, void* out,
     return 0;
 }
 
+// ---------------------------------------------------------- multiway merge
+// hpxhip_merge_runs (r05): the p <= 8 sorted runs the segmented sort's
+// all-to-all delivers, merged in ONE pass over the keys (16 B/key) instead of
+// ceil(log2 p) pairwise rounds (3 x 16 B/key at p = 8).
+//   1. k_mw_samples: every S-th key of every run (p sorted sample runs, kept),
+//      merged pairwise (run_merge) into one sorted sample of M keys;
+//   2. splitters v_k = sample[k q], k = 1 .. K-1 (q = 3p); k_mw_bounds: for
+//      every splitter and run the lower and upper bound -- first in the run's
+//      own samples (a few MiB, cache resident), then inside the S keys
+//      between two of them;
+//   3. k_mw_merge, one 256-thread workgroup per task k: the keys equal to
+//      v_k are copied straight to their place (any order is sorted), the
+//      keys strictly between v_k and v_{k+1} -- at most (q + p) S = CAP of
+//      them: run j holds fewer than (c_j + 1) S keys between two of its
+//      samples, and at most q samples lie strictly between two splitters --
+//      are staged in LDS and merged there by ceil(log2 p) merge-path rounds
+//      (outputs staged in registers: one LDS buffer, 16 KiB, so several
+//      workgroups share a CU), then written out.  Task k starts at output
+//      position sum_j lower_bound_j(v_k); a repeated splitter leaves its
+//      equal keys to the last task holding it.
+// Keys only (equal keys are interchangeable), in the sort's key order.
+// Measured at 2^30 u64 (profiles/r05_merge_runs_probe.log): p = 4 5.8 ms
+// against 6.5 for two pairwise rounds, p = 8 8.5-9.0 against 9.6, p = 2 4.2
+// against 3.3 -- the LDS rounds, not the bytes, bound it; the segmented sort
+// takes it for 4 <= p <= 8.
+inline size_t merge_scratch_bytes_for(uint64_t n) { return ((n + kTile - 1) / kTile + 1) * 8; }
+
+constexpr int kMwThreads = 256;
+constexpr int kMwItems = 8;
+constexpr int kMwCap = kMwThreads * kMwItems;  // keys strictly between two splitters, at most
+constexpr int kMwMaxRuns = 8;
+constexpr uint32_t kMwQ = 3;  // splitters every kMwQ * p samples
+
+struct mw_runs {
+    uint64_t off[kMwMaxRuns + 1];   // run j = in[off[j], off[j + 1])
+    uint64_t soff[kMwMaxRuns + 1];  // run j's samples = sample[soff[j], soff[j + 1])
+    uint32_t p;
+    uint32_t stride;  // S
+    uint32_t q;       // samples per splitter
+};
+
+template <typename U>
+__global__ __launch_bounds__(256) void k_mw_samples(const U* __restrict__ in, mw_runs r, U* __restrict__ sample) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= r.soff[r.p]) return;
+    uint32_t j = 0;
+    while (j + 1 < r.p && r.soff[j + 1] <= i) ++j;
+    sample[i] = in[r.off[j] + (i - r.soff[j]) * r.stride];
+}
+
+// first index in [lo, hi) of a[] whose key is not before v (UPPER: after v)
+template <bool UPPER, typename U, typename X>
+__device__ __forceinline__ uint64_t mw_search(const U* a, uint64_t lo, uint64_t hi, U v, X xf) {
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const U x = xf(a[mid]);
+        if (UPPER ? (x <= v) : (x < v)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// lower (UPPER: upper) bound of v in run j, through the run's samples
+template <bool UPPER, typename U, typename X>
+__device__ __forceinline__ uint64_t mw_bound(const U* run, uint64_t len, const U* samp, uint64_t ns, uint32_t S, U v,
+                                            X xf) {
+    // c samples (run[0], run[S], ...) are before v: the bound is in
+    // ((c - 1) S, c S]
+    const uint64_t c = mw_search<UPPER>(samp, 0, ns, v, xf);
+    if (c == 0) return 0;
+    const uint64_t lo = (c - 1) * S + 1;
+    const uint64_t hi = c * S < len ? c * S : len;
+    return mw_search<UPPER>(run, lo, hi, v, xf);
+}
+
+// LB / UB [(K + 1) x p]: row k = the lower / upper bounds of splitter v_k in
+// every run, relative to the run's start (row 0: 0, row K: the run lengths)
+template <typename U, typename X>
+__global__ __launch_bounds__(256) void k_mw_bounds(const U* __restrict__ in, mw_runs r, const U* __restrict__ runsamp,
+                                                   const U* __restrict__ sorted, uint64_t K, X xf,
+                                                   uint64_t* __restrict__ LB, uint64_t* __restrict__ UB) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= (K + 1) * r.p) return;
+    const uint64_t k = i / r.p;
+    const uint32_t j = static_cast<uint32_t>(i % r.p);
+    const uint64_t len = r.off[j + 1] - r.off[j];
+    if (k == 0 || k == K) {
+        LB[i] = UB[i] = k == 0 ? 0 : len;
+        return;
+    }
+    const U* run = in + r.off[j];
+    const U* samp = runsamp + r.soff[j];
+    const uint64_t ns = r.soff[j + 1] - r.soff[j];
+    const U v = xf(sorted[k * r.q]);
+    const uint64_t lb = mw_bound<false>(run, len, samp, ns, r.stride, v, xf);
+    LB[i] = lb;
+    // distinct keys: the key at the lower bound is already past v
+    UB[i] = (lb == len || xf(run[lb]) != v) ? lb : mw_bound<true>(run, len, samp, ns, r.stride, v, xf);
+}
+
+// LDS position of staged key i: one pad element every 8, so the lanes of a
+// merge round -- 8 outputs apart, 64 B for u64 -- do not pile onto the same
+// banks (16 lanes per bank unpadded)
+__device__ __forceinline__ constexpr int mw_pad(int i) { return i + (i >> 3); }
+
+// One round inside the LDS: runs (2i, 2i + 1) of s (bounds b[0..nruns])
+// merged in place; thread t computes outputs [8t, 8t + 8) into registers,
+// then (after the barrier every thread reaches) writes them back.  The pair
+// state is set up by a merge-path search at the thread's first output and
+// restarted (at the pair's start, no search) when the outputs cross into
+// the next pair.
+template <typename U, typename X>
+__device__ __forceinline__ void mw_round(U* s, const int* b, int nruns, int total, X xf) {
+    const int o0 = static_cast<int>(threadIdx.x) * kMwItems;
+    U r[kMwItems];
+    int a0 = 0, a1 = 0, b1 = 0, ia = 0, ib = 0, la = 0, lb = 0, pi = 0;
+    U va{}, vb{};
+    auto enter = [&](int i, int dk) {  // pair i, its first dk outputs done
+        pi = i;
+        a0 = b[2 * i];
+        const bool pair = 2 * i + 1 < nruns;
+        a1 = pair ? b[2 * i + 1] : b[nruns];
+        b1 = pair ? b[2 * i + 2] : a1;
+        la = a1 - a0;
+        lb = b1 - a1;
+        int lo = dk > lb ? dk - lb : 0, hi = dk < la ? dk : la;
+        while (lo < hi) {  // a-elements among the pair's first dk outputs (a first on ties)
+            const int mid = (lo + hi) >> 1;
+            if (!(xf(s[mw_pad(a1 + dk - mid - 1)]) < xf(s[mw_pad(a0 + mid)]))) lo = mid + 1;
+            else hi = mid;
+        }
+        ia = lo;
+        ib = dk - lo;
+        va = s[mw_pad(a0 + (ia < la ? ia : 0))];
+        vb = s[mw_pad(a1 + (ib < lb ? ib : 0))];
+    };
+    if (o0 < total) {
+        int i = 0;
+        while (2 * (i + 1) < nruns && b[2 * (i + 1)] <= o0) ++i;
+        enter(i, o0 - b[2 * i]);
+    }
+#pragma unroll
+    for (int q = 0; q < kMwItems; ++q) {
+        const int o = o0 + q;
+        if (o < total) {
+            while (o == b1 && 2 * (pi + 1) < nruns) enter(pi + 1, 0);  // (skipping empty pairs)
+            const bool takeb = ia >= la || (ib < lb && xf(vb) < xf(va));
+            if (takeb) {
+                r[q] = vb;
+                ++ib;
+                vb = s[mw_pad(a1 + (ib < lb ? ib : 0))];
+            } else {
+                r[q] = va;
+                ++ia;
+                va = s[mw_pad(a0 + (ia < la ? ia : 0))];
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kMwItems; ++q)
+        if (o0 + q < total) s[mw_pad(o0 + q)] = r[q];
+    __syncthreads();
+}
+
+// (69 VGPRs, 7 waves per SIMD.  Forcing 8 with __launch_bounds__(256, 8)
+// spilled 22 SGPRs and the float64 instantiation then wrote wrong keys --
+// scripts/mw_debug.py, profiles/r05_merge_runs_debug.log -- so it keeps the
+// default bound.)
+template <typename U, typename X, bool VEC>
+__global__ __launch_bounds__(kMwThreads) void k_mw_merge(const U* __restrict__ in, mw_runs r,
+                                                         const uint64_t* __restrict__ LB,
+                                                         const uint64_t* __restrict__ UB, X xf, U* __restrict__ out,
+                                                         uint32_t* __restrict__ err) {
+    __shared__ alignas(16) U s[mw_pad(kMwCap) + 1];  // (+1: a finished run's head reads one past)
+    __shared__ int sbnd[kMwMaxRuns + 1];
+    const uint64_t k = blockIdx.x;
+    const uint32_t p = r.p;
+    // run j: keys == v_k at [eq_j, lo_j), keys strictly between at [lo_j, hi_j)
+    uint64_t eq[kMwMaxRuns], lo[kMwMaxRuns], hi[kMwMaxRuns];
+    uint64_t pos = 0;  // sum_j lower_bound_j(v_k): where the task's output starts
+    bool dup = false;
+#pragma unroll
+    for (uint32_t j = 0; j < kMwMaxRuns; ++j)
+        if (j < p) {
+            eq[j] = LB[k * p + j];
+            lo[j] = UB[k * p + j];
+            hi[j] = LB[(k + 1) * p + j];
+            dup = dup || hi[j] < lo[j];
+            pos += eq[j];
+        }
+    // v_{k+1} == v_k (a repeated splitter: some run holds keys equal to v_k
+    // before lower_bound(v_{k+1})): the last task with this splitter copies
+    // its equal keys, this one has nothing to do
+    if (dup) return;
+    // the keys equal to v_k, run after run
+#pragma unroll
+    for (uint32_t j = 0; j < kMwMaxRuns; ++j)
+        if (j < p) {
+            const uint64_t ne = lo[j] - eq[j];
+            const U* src = in + r.off[j] + eq[j];
+            for (uint64_t e = threadIdx.x; e < ne; e += kMwThreads) out[pos + e] = src[e];
+            pos += ne;
+        }
+    uint64_t total = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kMwMaxRuns; ++j)
+        if (j < p) total += hi[j] - lo[j];
+    if (total > static_cast<uint64_t>(kMwCap)) {  // cannot happen with consistent keys (see above)
+        if (threadIdx.x == 0) raise_device_error(err, HPXHIP_DEVERR_RANGE);
+        return;
+    }
+    // stage the runs' middle parts back to back
+    int c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kMwMaxRuns; ++j)
+        if (j < p) {
+            const int nj = static_cast<int>(hi[j] - lo[j]);
+            if constexpr (VEC) {  // 16-B loads of the aligned vectors covering the part
+                constexpr int V = 16 / sizeof(U);
+                using VT = vec<U, V>;
+                const uint64_t g0 = r.off[j] + lo[j], g1 = r.off[j] + hi[j];
+                const VT* vs = reinterpret_cast<const VT*>(in);
+                for (uint64_t v = g0 / V + threadIdx.x; v < (g1 + V - 1) / V; v += kMwThreads) {
+                    const VT x = ld_stream(&vs[v]);
+#pragma unroll
+                    for (int e = 0; e < V; ++e) {
+                        const uint64_t i = v * V + e;
+                        if (i >= g0 && i < g1) s[mw_pad(c + static_cast<int>(i - g0))] = x.v[e];
+                    }
+                }
+            } else {
+                const U* src = in + r.off[j] + lo[j];
+                for (int e = threadIdx.x; e < nj; e += kMwThreads) s[mw_pad(c + e)] = ld_stream(&src[e]);
+            }
+            if (threadIdx.x == 0) sbnd[j] = c;
+            c += nj;
+        }
+    if (threadIdx.x == 0) sbnd[p] = c;
+    __syncthreads();
+    const int n = c;
+    int nruns = static_cast<int>(p);
+    while (nruns > 1) {
+        mw_round(s, sbnd, nruns, n, xf);
+        const int nn = (nruns + 1) / 2;
+        if (threadIdx.x == 0) {
+            for (int i = 1; i < nn; ++i) sbnd[i] = sbnd[2 * i];
+            sbnd[nn] = n;
+        }
+        __syncthreads();
+        nruns = nn;
+    }
+    // write-out: a head up to the output's next 16-B boundary, 16-B vectors,
+    // a tail (out 16-B aligned when VEC)
+    U* o = out + pos;
+    constexpr int V = 16 / sizeof(U);
+    using VT = vec<U, V>;
+    const int head = VEC ? min(n, static_cast<int>(((16u - (reinterpret_cast<uintptr_t>(o) & 15u)) & 15u) / sizeof(U)))
+                         : n;
+    const int nvec = (n - head) / V;
+    for (int e = threadIdx.x; e < head; e += kMwThreads) o[e] = s[mw_pad(e)];
+    for (int q = threadIdx.x; q < nvec; q += kMwThreads) {
+        VT w;
+#pragma unroll
+        for (int e = 0; e < V; ++e) w.v[e] = s[mw_pad(head + q * V + e)];
+        st_stream(reinterpret_cast<VT*>(o + head) + q, w);
+    }
+    for (int e = head + nvec * V + threadIdx.x; e < n; e += kMwThreads) o[e] = s[mw_pad(e)];
+}
+
+// sample stride S for p runs: the bound (q + p) S <= kMwCap with q = kMwQ p
+inline uint32_t mw_stride(uint32_t p) { return static_cast<uint32_t>(kMwCap / ((kMwQ + 1) * p)); }
+
+struct mw_layout {
+    uint64_t M, K;
+    size_t runsamp, sa, sb, splits, lb, ub, total;
+};
+
+inline mw_layout mw_plan(const uint64_t* len, uint32_t p) {
+    mw_layout L{};
+    const uint32_t S = mw_stride(p);
+    const uint64_t q = kMwQ * p;
+    for (uint32_t j = 0; j < p; ++j) L.M += (len[j] + S - 1) / S;
+    L.K = (L.M + q - 1) / q;
+    if (L.K == 0) L.K = 1;
+    size_t off = 0;
+    L.runsamp = off;  // the samples in run order (kept for the bound searches)
+    off = align_up(off + L.M * 8, 256);
+    L.sa = off;  // the merge's ping-pong buffers
+    off = align_up(off + L.M * 8, 256);
+    L.sb = off;
+    off = align_up(off + L.M * 8, 256);
+    L.splits = off;
+    off = align_up(off + merge_scratch_bytes_for(L.M), 256);
+    L.lb = off;
+    off = align_up(off + (L.K + 1) * p * 8, 256);
+    L.ub = off;
+    off = align_up(off + (L.K + 1) * p * 8, 256);
+    L.total = off;
+    return L;
+}
+
+template <typename T, bool DESC>
+int run_merge_runs(const void* in, const uint64_t* off, uint32_t p, void* out, hipStream_t s, void* scratch,
+                   size_t scratch_bytes) {
+    using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
+    using X = ordered_bits<T, DESC>;
+    const U* ui = static_cast<const U*>(in) + off[0];
+    mw_runs r{};
+    r.p = p;
+    r.stride = mw_stride(p);
+    r.q = kMwQ * p;
+    uint64_t len[kMwMaxRuns];
+    for (uint32_t j = 0; j <= p; ++j) r.off[j] = off[j] - off[0];
+    for (uint32_t j = 0; j < p; ++j) len[j] = r.off[j + 1] - r.off[j];
+    for (uint32_t j = 0; j < p; ++j) r.soff[j + 1] = r.soff[j] + (len[j] + r.stride - 1) / r.stride;
+    const mw_layout L = mw_plan(len, p);
+    void* ws = nullptr;
+    int rc = resolve_scratch(s, scratch, scratch_bytes, L.total, &ws);
+    if (rc) return rc;
+    char* base = static_cast<char*>(ws);
+    U* runsamp = reinterpret_cast<U*>(base + L.runsamp);
+    U* sbuf[2] = {reinterpret_cast<U*>(base + L.sa), reinterpret_cast<U*>(base + L.sb)};
+    if (L.M) {
+        hipLaunchKernelGGL((k_mw_samples<U>), dim3(static_cast<unsigned>((L.M + 255) / 256)), dim3(256), 0, s, ui, r,
+                           runsamp);
+        HPXHIP_CHECK_LAUNCH();
+    }
+    // the sample's p sorted runs, merged pairwise (runsamp -> sa -> sb -> sa ...)
+    uint64_t sr[kMwMaxRuns + 1];
+    uint32_t ns = p;
+    for (uint32_t j = 0; j <= p; ++j) sr[j] = r.soff[j];
+    const U* src = runsamp;
+    int which = 0;
+    while (ns > 1) {
+        U* dst = sbuf[which];
+        uint32_t nn = 0;
+        for (uint32_t j = 0; j < ns; j += 2) {
+            const uint64_t a0 = sr[j], a1 = sr[j + 1];
+            if (j + 1 < ns) {
+                const uint64_t b1 = sr[j + 2];
+                if (b1 > a0 && (rc = run_merge<T, DESC>(src + a0, a1 - a0, src + a1, b1 - a1, dst + a0, s,
+                                                        base + L.splits, merge_scratch_bytes_for(L.M))))
+                    return rc;
+            } else if (a1 > a0) {
+                HPXHIP_CHECK(hipMemcpyAsync(dst + a0, src + a0, (a1 - a0) * sizeof(U), hipMemcpyDeviceToDevice, s));
+            }
+            sr[nn++] = a0;
+        }
+        sr[nn] = sr[ns];
+        ns = nn;
+        src = dst;
+        which ^= 1;
+    }
+    auto* LB = reinterpret_cast<uint64_t*>(base + L.lb);
+    auto* UB = reinterpret_cast<uint64_t*>(base + L.ub);
+    const uint64_t nb = (L.K + 1) * p;
+    hipLaunchKernelGGL((k_mw_bounds<U, X>), dim3(static_cast<unsigned>((nb + 255) / 256)), dim3(256), 0, s, ui, r,
+                       runsamp, src, L.K, X{}, LB, UB);
+    HPXHIP_CHECK_LAUNCH();
+    if ((reinterpret_cast<uintptr_t>(ui) | reinterpret_cast<uintptr_t>(out)) % 16 == 0)
+        hipLaunchKernelGGL((k_mw_merge<U, X, true>), dim3(static_cast<unsigned>(L.K)), dim3(kMwThreads), 0, s, ui, r,
+                           LB, UB, X{}, static_cast<U*>(out), device_error_word(s));
+    else
+        hipLaunchKernelGGL((k_mw_merge<U, X, false>), dim3(static_cast<unsigned>(L.K)), dim3(kMwThreads), 0, s, ui, r,
+                           LB, UB, X{}, static_cast<U*>(out), device_error_word(s));
+    HPXHIP_CHECK_LAUNCH();
+    return 0;
+}
+
 }  // namespace
 
 namespace hpxhip {
 size_t merge_scratch_bytes(uint64_t n) { return ((n + kTile - 1) / kTile + 1) * 8; }
+// worst case over the run counts for n keys in total (the sample is largest
+// at 8 runs, plus one partial sample block per run)
+size_t merge_runs_scratch_bytes(uint64_t n) {
+    size_t worst = 0;
+    for (uint32_t p = 2; p <= kMwMaxRuns; ++p) {
+        uint64_t len[kMwMaxRuns] = {};
+        len[0] = n;
+        for (uint32_t j = 1; j < p; ++j) len[j] = 1;  // every run adds a partial sample block
+        const mw_layout L = mw_plan(len, p);
+        worst = std::max(worst, L.total + static_cast<size_t>(p) * 8 * 4 + 4096);
+    }
+    return worst;
+}
 }  // namespace hpxhip
 
 // is_sorted.hpp:40-120 counts a pair (i, i+1) as out of order iff
@@ -138,6 +521,31 @@ int hpxhip_merge(int dtype, const void* in1, uint64_t n1, const void* in2, uint6
         using T = typename decltype(t)::type;
         if (descending) return run_merge<T, true>(in1, n1, in2, n2, out, s, scratch, scratch_bytes);
         return run_merge<T, false>(in1, n1, in2, n2, out, s, scratch, scratch_bytes);
+    });
+}
+
+int hpxhip_merge_runs(int dtype, const void* in, const uint64_t* run_offsets, int nruns, void* out, int descending,
+                      hpxhip_stream stream, void* scratch, size_t scratch_bytes) {
+    HPXHIP_ANNOTATE("hpxhip_merge_runs");
+    if (!run_offsets || nruns < 1 || nruns > kMwMaxRuns) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    for (int j = 0; j < nruns; ++j)
+        if (run_offsets[j + 1] < run_offsets[j]) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    const uint64_t n = run_offsets[nruns] - run_offsets[0];
+    if (n == 0) return 0;
+    if (!in || !out) return HPXHIP_ERROR_INVALID_ARGUMENT;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    device_guard g(s);
+    if (g.status) return g.status;
+    return with_dtype(dtype, [&](auto t) -> int {
+        using T = typename decltype(t)::type;
+        if (nruns == 1) {
+            HPXHIP_CHECK(hipMemcpyAsync(out, static_cast<const T*>(in) + run_offsets[0], n * sizeof(T),
+                                        hipMemcpyDeviceToDevice, s));
+            return 0;
+        }
+        const uint32_t p = static_cast<uint32_t>(nruns);
+        if (descending) return run_merge_runs<T, true>(in, run_offsets, p, out, s, scratch, scratch_bytes);
+        return run_merge_runs<T, false>(in, run_offsets, p, out, s, scratch, scratch_bytes);
     });
 }
 

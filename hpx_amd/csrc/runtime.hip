@@ -520,6 +520,7 @@ int hpxhip_scratch_bytes(int algo, int dtype, int aux_dtype, uint64_t n, size_t*
         case HPXHIP_ALGO_COPY_IF: *bytes = copy_if_scratch_bytes(dtype, n); return 0;
         case HPXHIP_ALGO_SORT: *bytes = sort_scratch_bytes(dtype, -1, n); return 0;
         case HPXHIP_ALGO_MERGE: *bytes = merge_scratch_bytes(n); return 0;
+        case HPXHIP_ALGO_MERGE_RUNS: *bytes = merge_runs_scratch_bytes(n); return 0;
         case HPXHIP_ALGO_SORT_BY_KEY:
             if (dtype_size(aux_dtype) == 0) return HPXHIP_ERROR_INVALID_ARGUMENT;
             *bytes = sort_scratch_bytes(dtype, aux_dtype, n);

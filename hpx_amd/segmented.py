@@ -423,6 +423,15 @@ class HipEngine:
         L.call("hpxhip_merge", dt, ctypes.c_void_p(a.data() + a_off * it), na, ctypes.c_void_p(b.data() + b_off * it),
                nb, ctypes.c_void_p(out.data() + out_off * it), 1 if descending else 0, self.stream, None, 0)
 
+    def merge_runs(self, dt, src, s_off, offsets, out, out_off, descending):
+        """hpxhip_merge_runs: the sorted runs src[s_off + offsets[j],
+        s_off + offsets[j + 1]) (up to 8) merged into out[out_off, ...) in one
+        pass."""
+        it = np_dtype(dt).itemsize
+        offs = (ctypes.c_uint64 * len(offsets))(*[int(o) for o in offsets])
+        L.call("hpxhip_merge_runs", dt, ctypes.c_void_p(src.data() + s_off * it), offs, len(offsets) - 1,
+               ctypes.c_void_p(out.data() + out_off * it), 1 if descending else 0, self.stream, None, 0)
+
     def copy(self, dt, src, s_off, n, dst, d_off):
         if n:
             it = np_dtype(dt).itemsize
@@ -884,8 +893,9 @@ class segmented:
            (every rank computes every rank's slices, so the receive counts
            need no further exchange);
         4. one RCCL all-to-all with uneven splits moves the slices;
-        5. the p received sorted runs are merged pairwise (hpxhip_merge,
-           ceil(log2 p) rounds of 16 B/key) into the partition.
+        5. the p received sorted runs are merged into the partition: in one
+           pass for 4 <= p <= 8 (hpxhip_merge_runs, 16 B/key), else pairwise
+           (hpxhip_merge, ceil(log2 p) rounds of 16 B/key).
         Returns last (the partitioned_vector's end)."""
         comp = F.require(comp, F.Compare, "segmented sort")
         pv, a, b = _range(first, last)
@@ -903,7 +913,13 @@ class segmented:
         send, recv = self._sort_cuts(eng, comm, pv, lo, hi, dt, desc)
         rbuf = eng.buffer(pv.local, n_loc)
         comm.alltoallv(pv.local, lo, send, rbuf, recv, np_dtype(dt).itemsize, eng.stream)
+        # r05: 4 to 8 runs in one pass (hpxhip_merge_runs); otherwise
         # pairwise merge rounds, ping-pong between rbuf and the partition
+        if self.MERGE_RUNS_MIN <= p <= self.MERGE_RUNS_MAX and hasattr(eng, "merge_runs"):
+            offsets = [0] + [int(c) for c in np.cumsum(recv)]
+            eng.merge_runs(dt, rbuf, 0, offsets, pv.local, lo, desc)
+            eng.release(rbuf)
+            return segmented_iterator(pv, pv.n)
         runs = [(int(o), int(c)) for o, c in zip(np.cumsum(recv) - recv, recv)]
         src, dst = rbuf, pv.local
         src_base, dst_base = 0, lo
@@ -924,6 +940,13 @@ class segmented:
             eng.copy(dt, src, src_base, n_loc, pv.local, lo)
         eng.release(rbuf)
         return segmented_iterator(pv, pv.n)
+
+    # runs merged by one hpxhip_merge_runs call: its limit, and the fewest it
+    # beats pairwise rounds at (2^30 u64, profiles/r05_merge_runs_probe.log:
+    # p = 2 4.2 vs 3.3 ms, p = 4 5.8 vs 6.5, p = 8 8.5-9.0 vs 9.6; its LDS
+    # merge rounds, log2 p per task, bound it, not its 16 B/key)
+    MERGE_RUNS_MIN = 4
+    MERGE_RUNS_MAX = 8
 
     # digits per radix-select round, and the largest block (keys left in a
     # boundary's candidate range, over all ranks) finished by gathering keys

@@ -129,7 +129,8 @@ enum hpxhip_algo {
     HPXHIP_ALGO_COPY_IF = 2,
     HPXHIP_ALGO_SORT = 3,
     HPXHIP_ALGO_SORT_BY_KEY = 4,
-    HPXHIP_ALGO_MERGE = 5  /* n = n1 + n2 */
+    HPXHIP_ALGO_MERGE = 5,  /* n = n1 + n2 */
+    HPXHIP_ALGO_MERGE_RUNS = 6  /* n = the runs' total (hpxhip_merge_runs, up to 8 runs) */
 };
 
 typedef struct hpxhip_stream_opaque* hpxhip_stream; /* == hipStream_t */
@@ -356,6 +357,15 @@ int hpxhip_sort_by_key(int key_dtype, int value_dtype, void* keys, void* values,
    hpxhip_sort.  out must not overlap the inputs. */
 int hpxhip_merge(int dtype, const void* in1, uint64_t n1, const void* in2, uint64_t n2, void* out,
                  int descending, hpxhip_stream stream, void* scratch, size_t scratch_bytes);
+/* The segmented sort's merge step (no reference counterpart: HPX 1.4 has no
+   segmented sort; its local algorithm is sort.hpp:364): the nruns (1..8)
+   sorted runs in[run_offsets[j], run_offsets[j+1]) (run_offsets: a HOST
+   array of nruns+1 non-decreasing element offsets) merged into
+   out[0, run_offsets[nruns] - run_offsets[0]) in one pass, in the key order
+   of hpxhip_sort (keys only: equal keys are not told apart).  out must not
+   overlap in.  Scratch: HPXHIP_ALGO_MERGE_RUNS with n = the total. */
+int hpxhip_merge_runs(int dtype, const void* in, const uint64_t* run_offsets, int nruns, void* out,
+                      int descending, hpxhip_stream stream, void* scratch, size_t scratch_bytes);
 /* Batched binary search in a sorted range (the partition cut of the
    segmented sort; std::lower_bound / std::upper_bound semantics under the
    sort's key order): out_dev[i] = number of sorted[] elements ordered before

@@ -12,6 +12,7 @@ from hpx_amd import _lib as L
 from hpx_amd import execution as ex, functional as F
 from hpx_amd import parallel as P
 from hpx_amd import segmented as S
+from hpx_amd.compute import dtype_code
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -93,6 +94,99 @@ def test_sorted_bounds(gpu_target, dt):
     # sub-range
     lo2 = eng.bounds(v, 1000, 50000, probes, False, False)
     np.testing.assert_array_equal(lo2, np.searchsorted(xs[1000:50000], ps, "left"))
+
+
+def _merge_runs(gpu_target, runs, dt, desc, lead=0):
+    """hpxhip_merge_runs over the runs laid back to back after `lead` keys."""
+    src = np.concatenate([np.zeros(lead, dt)] + [np.asarray(r, dt) for r in runs])
+    offsets = [lead] + list(lead + np.cumsum([len(r) for r in runs]))
+    eng = S.HipEngine(gpu_target)
+    d = hpx.vector.from_host(src if src.size else np.zeros(1, dt), gpu_target)
+    out = hpx.vector(max(1, offsets[-1] - lead + 1), dtype=dt, tgt=gpu_target)
+    eng.merge_runs(dtype_code(dt), d, 0, offsets, out, 1, desc)
+    gpu_target.synchronize()
+    return out.to_host()[1:1 + offsets[-1] - lead]
+
+
+@pytest.mark.parametrize("p", [2, 3, 5, 8])
+@pytest.mark.parametrize("dt", [np.uint64, np.int32, np.float64])
+def test_merge_runs_bit_exact(gpu_target, p, dt):
+    """The segmented sort's one-pass merge of p <= 8 sorted runs
+    (hpxhip_merge_runs): ragged and empty runs, keys with heavy repeats
+    (the copied equal-key blocks), against the oracle sort of the union."""
+    rng = np.random.default_rng(p)
+    for shape in ("random", "repeats", "empty_runs"):
+        lens = rng.integers(0, 300000, p)
+        if shape == "empty_runs":
+            lens[::2] = 0
+        runs = []
+        for j, n in enumerate(lens):
+            if shape == "repeats":
+                x = rnd(dt, int(n), 10 + j, 0, 40) if np.dtype(dt).kind != "f" else np.round(rnd(dt, int(n), 10 + j), 1)
+            else:
+                x = rnd(dt, int(n), 10 + j)
+            runs.append(O.sort(np.asarray(x, dt)))
+        for desc in (False, True):
+            rs = [O.sort(r, desc) for r in runs]
+            got = _merge_runs(gpu_target, rs, dt, desc, lead=3)
+            np.testing.assert_array_equal(bits(got), bits(O.sort(np.concatenate(rs), desc)),
+                                          err_msg=f"{shape} desc={desc}")
+
+
+@pytest.mark.parametrize("case", ["all_equal", "two_values", "one_long_run", "tiny"])
+def test_merge_runs_edge_cases(gpu_target, case):
+    """All keys equal (one task copies them), two values, one run holding
+    nearly everything, and runs shorter than a sample stride."""
+    dt = np.int64
+    rng = np.random.default_rng(7)
+    if case == "all_equal":
+        # (repeated splitters: only the last task with the value copies them)
+        runs = [np.full(n, 5, dt) for n in (70000, 3, 50000, 1, 120000, 0, 9, 40000)]
+    elif case == "two_values":
+        runs = [O.sort(rng.integers(0, 2, n).astype(dt)) for n in (80000, 60000, 1, 99999, 5)]
+    elif case == "one_long_run":
+        runs = [O.sort(rnd(dt, 1 << 21, 8))] + [O.sort(rnd(dt, 3, 9 + j)) for j in range(6)]
+    else:
+        runs = [O.sort(rnd(dt, n, 20 + n)) for n in (1, 2, 0, 7, 1, 0, 3, 1)]
+    for desc in (False, True):
+        rs = [O.sort(r, desc) for r in runs]
+        got = _merge_runs(gpu_target, rs, dt, desc)
+        np.testing.assert_array_equal(got, O.sort(np.concatenate(rs), desc), err_msg=f"{case} desc={desc}")
+
+
+def test_merge_runs_2p30_eight_runs(gpu_target):
+    """The 8-GPU sort's merge at full size: 2^30 u64 keys in 8 runs (the
+    all-to-all's slices), generated and checked on the device (torch: the
+    runs are the sorted columns of a permutation-closed form; the merged
+    array must be 0, 1, ..., n-1, element for element)."""
+    import torch
+    dev = torch.device("cuda", gpu_target.device)
+    n, p = 1 << 30, 8
+    # run j = sorted keys (i << 3 | j) for i < n/p: merged = 0 .. n-1 in order
+    m = n // p
+    src = hpx.vector(n, dtype=np.uint64, tgt=gpu_target)
+    out = hpx.vector(n, dtype=np.uint64, tgt=gpu_target)
+    import ctypes
+    for j in range(p):
+        t = (torch.arange(m, dtype=torch.int64, device=dev) << 3) | j
+        torch.cuda.synchronize(dev)
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(src.data() + j * m * 8), ctypes.c_void_p(t.data_ptr()), m * 8,
+               L.D2D, gpu_target.stream)
+        gpu_target.synchronize()
+        del t
+    eng = S.HipEngine(gpu_target)
+    eng.merge_runs(L.U64, src, 0, [j * m for j in range(p + 1)], out, 0, False)
+    gpu_target.synchronize()
+    chunk = 1 << 26
+    got = torch.empty(chunk, dtype=torch.int64, device=dev)
+    for lo in range(0, n, chunk):
+        L.call("hpxhip_memcpy_async", ctypes.c_void_p(got.data_ptr()), ctypes.c_void_p(out.data() + lo * 8), chunk * 8,
+               L.D2D, gpu_target.stream)
+        gpu_target.synchronize()
+        exp = torch.arange(lo, lo + chunk, dtype=torch.int64, device=dev)
+        assert int((got != exp).sum()) == 0, lo
+    src.free()
+    out.free()
 
 
 def test_segmented_sort_single_rank(gpu_target):

@@ -68,6 +68,17 @@ class SortEngine:
         pass
 
 
+class RunsEngine(SortEngine):
+    """With the one-pass merge of up to 8 runs (hpxhip_merge_runs's role):
+    the oracle's merge folded over the runs."""
+
+    def merge_runs(self, dt, src, s_off, offsets, out, out_off, desc):
+        acc = src[s_off + offsets[0]:s_off + offsets[0]]
+        for a, b in zip(offsets[:-1], offsets[1:]):
+            acc = O.merge(acc, src[s_off + a:s_off + b], desc)
+        out[out_off:out_off + acc.size] = acc
+
+
 class HostPV(S.partitioned_vector):
     def __init__(self, glob, comm, layout=None):
         self.comm = comm
@@ -129,15 +140,19 @@ def _worker(rank, size, port, q):
     try:
         comm = CountingComm(S.TorchComm(None, memory="host"))  # the product comm over host buffers
         res = {}
-        for gather in (S.segmented.SELECT_GATHER, 16):  # the shipped block size, and one forcing more rounds
-            alg = S.segmented(SortEngine())
+        # the shipped block size and one forcing more rounds, with the
+        # one-pass run merge (p <= 8); the shipped block size with the
+        # pairwise merge rounds (p > 8)
+        for eng, gather in ((RunsEngine, S.segmented.SELECT_GATHER), (RunsEngine, 16),
+                            (SortEngine, S.segmented.SELECT_GATHER)):
+            alg = S.segmented(eng())
             alg.SELECT_GATHER = gather
             for name, x in cases().items():
                 for desc in (False, True):
                     pv = HostPV(x, comm)
                     comm.rounds = 0
                     alg.sort(None, pv.begin(), pv.end(), F.greater if desc else F.less)
-                    res[(gather, name, desc)] = (pv.lo, pv.local.copy(), comm.rounds)
+                    res[(eng.__name__, gather, name, desc)] = (pv.lo, pv.local.copy(), comm.rounds)
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -163,12 +178,12 @@ def test_segmented_sort_gloo(size):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for (gather, name, desc) in results[0]:
+    for (eng, gather, name, desc) in results[0]:
         x = cases()[name]
         got = np.zeros_like(x)
         sizes = []
         for r in range(size):
-            lo, loc, rounds = results[r][(gather, name, desc)]
+            lo, loc, rounds = results[r][(eng, gather, name, desc)]
             got[lo:lo + loc.size] = loc
             sizes.append(loc.size)
         if name == "u64_uniform" and gather == S.segmented.SELECT_GATHER:
@@ -181,4 +196,4 @@ def test_segmented_sort_gloo(size):
         assert sizes == [b - a for a, b in (S.partition_bounds(x.size, size, k) for k in range(size))]
         exp = O.sort(x, desc)
         np.testing.assert_array_equal(got.view(np.uint8), exp.view(np.uint8),
-                                      err_msg=f"{name} desc={desc} gather={gather}")
+                                      err_msg=f"{name} desc={desc} gather={gather} {eng}")
