@@ -13,6 +13,155 @@
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 using namespace hpxhip;
 
+namespace hpxhip {
+namespace scan_detail {
+// Pipelined form (r05, measured here and rejected: 3.23-3.38 ms against
+// 2.56 for the shipped k_scan at 2^30, profiles/r05_ubench_scan8_pipe.log): the copy_if
+// structure (copy_if_kernel.hpp k_copy_if_pipe) for the scan.  A persistent
+// grid of one 1024-thread workgroup per CU claims 128-KiB tiles in order; a
+// tile's wave-local scan goes to LDS (the whole tile), the next tile's loads
+// are issued into the registers it left, and only then does wave 0 take the
+// tile's look-back and the workgroup store the tile from LDS with its
+// prefixes added -- the stores run under the next tile's reads.  Same values
+// as k_scan with DEFER (round r's prefix = the wave prefix folded with the
+// totals of rounds < r, left to right; fixed-association look-back), so
+// floating-point results are the shipped kernel's bit for bit.
+template <typename T, typename Conv, typename Op, bool INCL, int ROUNDS, typename X = T>
+__global__ __launch_bounds__(kThreads, 1) void k_scan_pipe(const T* in, T* out, uint64_t n, Conv conv, Op op,
+                                                           X init, const X* prefix_dev, uint32_t* counter,
+                                                           scan_state<X> st, uint64_t ntiles) {
+    constexpr int V = 16 / sizeof(T);
+    constexpr int WAVES = kThreads / kWave;
+    constexpr uint64_t TILE = tile_elems<T, ROUNDS, kThreads>();
+    constexpr uint64_t WAVE_ELEMS = TILE / WAVES;
+    constexpr int ROUND_ELEMS = kWave * V;
+    using VT = vec<T, V>;
+    static_assert(std::is_same_v<X, T>, "built-in operators: the scanned type is the element type");
+
+    __shared__ alignas(16) X s_stage[TILE];
+    __shared__ X s_wave_total[WAVES];
+    __shared__ X s_tr[WAVES][ROUNDS];  // round totals
+    __shared__ X s_rp[WAVES][ROUNDS];  // round prefixes
+    __shared__ uint32_t s_next;
+    const X id = Op::template identity<X>();
+    const int wave = threadIdx.x / kWave;
+    const int lane = lane_id();
+
+    auto claim = [&] {
+        if (threadIdx.x == 0)
+            s_next = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    VT raw[ROUNDS];
+    auto load = [&](uint64_t t) {
+        const uint64_t wbase = t * TILE + wave * WAVE_ELEMS;
+        if (wbase + WAVE_ELEMS <= n) {
+            const VT* src = reinterpret_cast<const VT*>(in + wbase);
+#pragma unroll
+            for (int r = 0; r < ROUNDS; ++r) raw[r] = ld_stream(&src[r * kWave + lane]);
+        }
+    };
+
+    claim();
+    __syncthreads();
+    uint64_t tile = s_next;
+    if (tile >= ntiles) return;
+    load(tile);
+    while (true) {
+        const uint64_t tile_base = tile * TILE;
+        const uint64_t wbase = tile_base + wave * WAVE_ELEMS;
+        X x[ROUNDS][V];
+        if (wbase + WAVE_ELEMS <= n) {
+#pragma unroll
+            for (int r = 0; r < ROUNDS; ++r)
+#pragma unroll
+                for (int e = 0; e < V; ++e) x[r][e] = conv(raw[r].v[e]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < ROUNDS; ++r)
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    const uint64_t i = wbase + (static_cast<uint64_t>(r) * kWave + lane) * V + e;
+                    x[r][e] = i < n ? conv(in[i]) : id;
+                }
+        }
+        // wave-local scan of each round (k_scan's DEFER form)
+        X tr[ROUNDS];
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) {
+            X local[V];
+            X run = id;
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const X nxt = op(run, x[r][e]);
+                local[e] = INCL ? nxt : run;
+                run = nxt;
+            }
+            const X incl = wave_inclusive_scan(run, op);
+            const X excl = wave_shift_right<X, Op>(incl);
+#pragma unroll
+            for (int e = 0; e < V; ++e) x[r][e] = op(excl, local[e]);
+            tr[r] = readlane(incl, kWave - 1);
+        }
+        X carry = id;
+#pragma unroll
+        for (int r = 0; r < ROUNDS; ++r) carry = op(carry, tr[r]);
+        __syncthreads();  // (A) the previous tile's stores have read the stage
+        {
+            X* st_w = s_stage + wave * WAVE_ELEMS;
+#pragma unroll
+            for (int r = 0; r < ROUNDS; ++r) {
+                VT y;
+#pragma unroll
+                for (int e = 0; e < V; ++e) y.v[e] = x[r][e];
+                *reinterpret_cast<VT*>(st_w + (r * kWave + lane) * V) = y;
+            }
+            if (lane == 0) {
+                s_wave_total[wave] = carry;
+#pragma unroll
+                for (int r = 0; r < ROUNDS; ++r) s_tr[wave][r] = tr[r];
+            }
+        }
+        claim();
+        __syncthreads();  // (B) the stage, the wave totals, the next tile id
+        const uint64_t next = s_next;
+        if (next < ntiles) load(next);
+        if (wave == 0) tile_prefix<X, Op, WAVES, true, 1, true>(tile, st, op, prefix_dev, init, s_wave_total);
+        __syncthreads();  // (C) wave prefixes
+        if (threadIdx.x < WAVES * ROUNDS) {  // round prefixes: the wave's, then left to right
+            const int w = threadIdx.x / ROUNDS, rr = threadIdx.x % ROUNDS;
+            X rc = s_wave_total[w];
+            for (int q = 0; q < rr; ++q) rc = op(rc, s_tr[w][q]);
+            s_rp[w][rr] = rc;
+        }
+        __syncthreads();  // (D)
+        // write-out: tile-local vector v covers elements [v V, v V + V) of
+        // wave v V / WAVE_ELEMS, round (v V % WAVE_ELEMS) / ROUND_ELEMS
+        const bool full = tile_base + TILE <= n;
+#pragma unroll
+        for (int k = 0; k < static_cast<int>(TILE / V / kThreads); ++k) {
+            const uint32_t v = k * kThreads + threadIdx.x;
+            const uint32_t i0 = v * V;
+            const X rp = s_rp[i0 / WAVE_ELEMS][(i0 % WAVE_ELEMS) / ROUND_ELEMS];
+            const VT y = *reinterpret_cast<const VT*>(s_stage + i0);
+            if (full) {
+                VT z;
+#pragma unroll
+                for (int e = 0; e < V; ++e) z.v[e] = unwrap_value(op(rp, y.v[e]));
+                st_stream(reinterpret_cast<VT*>(out + tile_base) + v, z);
+            } else {
+#pragma unroll
+                for (int e = 0; e < V; ++e)
+                    if (tile_base + i0 + e < n) out[tile_base + i0 + e] = unwrap_value(op(rp, y.v[e]));
+            }
+        }
+        if (next >= ntiles) break;
+        tile = next;
+    }
+}
+
+}  // namespace scan_detail
+}  // namespace hpxhip
+
 template <typename T> struct idc { __device__ T operator()(T x) const { return x; } };
 
 template <typename T>
