@@ -233,7 +233,12 @@ __global__ __launch_bounds__(THREADS, MINW) void k_copy_if(const T* in, T* out, 
 // order, so every look-back waits only on tiles already claimed by running
 // workgroups (forward progress without co-residency).  Same tile shape,
 // look-back and output as k_copy_if<..., FIXED, ONEHOP>.
-template <typename T, typename Pred, int ROUNDS, typename SV, int MINW = 4>
+// OUT_ALIGN: the write-out starts its vectors at this output alignment
+// (the elements before it are stored one by one).  128 (a cache line): each
+// wave's 1-KiB store run covers whole lines, so two waves never write halves
+// of one line -- 2^30 int64 WRITE_SIZE 1.02 -> 1.0015x the hits, 1.985 ->
+// 1.96-1.97 ms (profiles/r05_ubench_copyif9_align128.log, r05_pmc_copy_if.txt).
+template <typename T, typename Pred, int ROUNDS, typename SV, int MINW = 4, int OUT_ALIGN = 128>
 __global__ __launch_bounds__(kThreads, MINW) void k_copy_if_pipe(const T* in, T* out, uint64_t n, Pred pred,
                                                                  uint64_t* count_dev, uint32_t* counter,
                                                                  tile_state<SV> st, uint64_t ntiles,
@@ -344,11 +349,12 @@ __global__ __launch_bounds__(kThreads, MINW) void k_copy_if_pipe(const T* in, T*
             }
         }
         __syncthreads();  // (C) the tile's output offset
-        // write-out: a head up to the output's next 16-B boundary, whole
-        // 16-B vectors, a tail
+        // write-out: a head up to the output's next OUT_ALIGN boundary,
+        // whole 16-B vectors, a tail
         T* o = out + s_prefix;
+        constexpr uintptr_t AM = OUT_ALIGN - 1;
         const uint32_t head =
-            agg ? min(agg, static_cast<uint32_t>(((16u - (reinterpret_cast<uintptr_t>(o) & 15u)) & 15u) / sizeof(T)))
+            agg ? min(agg, static_cast<uint32_t>(((OUT_ALIGN - (reinterpret_cast<uintptr_t>(o) & AM)) & AM) / sizeof(T)))
                 : 0u;
         const uint32_t nvec = (agg - head) / V;
         const uint32_t tail = agg - head - nvec * V;

@@ -34,7 +34,9 @@ struct harness {
   using P = pred_fn<HPXHIP_P_NOT_LT, T>;
   uint64_t N; T *in, *out, *ref_out; char* ws; uint32_t* err; uint64_t* cnt; unsigned long long* bad;
   hipEvent_t e0, e1; uint64_t ref = 0;
-  // kind 0: shipped k_copy_if; 1: k_copy_if_pipe, `per_cu` workgroups per CU
+  // kind 0: r04's k_copy_if; 1: k_copy_if_pipe with 16-B aligned vectors,
+  // `per_cu` workgroups per CU; 2: k_copy_if_pipe with its vectors 128-B
+  // aligned in the output (shipped after lease r5/ab)
   template <int KIND, int R = 8, int MINW = 4>
   void run(const char* name, int per_cu = 1) {
     using SV = uint32_t;
@@ -47,10 +49,14 @@ struct harness {
         constexpr bool W = sizeof(T) == 8;
         k_copy_if<T, P, true, R, 8, 0, SV, false, W, W ? 4 : 1, true, kThreads, W, W><<<ntiles, kThreads>>>(
             in, out, N, P{0}, cnt, reinterpret_cast<uint32_t*>(ws), st, ntiles);
+      } else if constexpr (KIND == 1) {
+        const uint64_t g = std::min<uint64_t>(ntiles, (uint64_t)g_cus * per_cu);
+        k_copy_if_pipe<T, P, R, SV, MINW, 16><<<g, kThreads>>>(in, out, N, P{0}, cnt, reinterpret_cast<uint32_t*>(ws),
+                                                               st, ntiles);
       } else {
         const uint64_t g = std::min<uint64_t>(ntiles, (uint64_t)g_cus * per_cu);
-        k_copy_if_pipe<T, P, R, SV, MINW><<<g, kThreads>>>(in, out, N, P{0}, cnt, reinterpret_cast<uint32_t*>(ws), st,
-                                                           ntiles);
+        k_copy_if_pipe<T, P, R, SV, MINW, 128><<<g, kThreads>>>(in, out, N, P{0}, cnt, reinterpret_cast<uint32_t*>(ws),
+                                                                st, ntiles);
       }
     };
     launch(); CK(hipDeviceSynchronize());
@@ -88,6 +94,7 @@ int main(int argc, char** argv) {
       k_fill<int64_t><<<((1ull << 30) + 255) / 256, 256>>>(h.in, h.N); CK(hipDeviceSynchronize());
       h.run<0>("T1024 R8 2/CU (shipped r04)");
       h.run<1>("pipe R8 1/CU");
+      h.run<2>("pipe R8 1/CU, 128-B aligned vectors");
       if (!quick) {
         h.run<1>("pipe R8 grid 2/CU (LDS-bound to 1)", 2);
         h.run<1, 4, 8>("pipe R4 1/CU", 1);
@@ -98,6 +105,7 @@ int main(int argc, char** argv) {
       harness<int64_t> h{(1ull << 30) - 3, (int64_t*)in, (int64_t*)out + 1, (int64_t*)ref_out, ws, err, cnt, bad, e0, e1};
       h.run<0>("n - 3, out 8 B mod 16: shipped");
       h.run<1>("n - 3, out 8 B mod 16: pipe R8");
+      h.run<2>("n - 3, out 8 B mod 16: pipe R8 128-B");
       harness<int64_t> hs{100003, (int64_t*)in, (int64_t*)out + 1, (int64_t*)ref_out, ws, err, cnt, bad, e0, e1};
       hs.run<0>("n 100003: shipped");
       hs.run<1>("n 100003: pipe R8");
@@ -105,6 +113,7 @@ int main(int argc, char** argv) {
       k_fill<int32_t><<<((1ull << 31) + 255) / 256, 256>>>(h4.in, h4.N); CK(hipDeviceSynchronize());
       h4.run<0>("T1024 R8 2/CU (shipped)");
       h4.run<1>("pipe R8 1/CU");
+      h4.run<2>("pipe R8 1/CU, 128-B aligned vectors");
       harness<int32_t> h5{(1ull << 31) - 5, (int32_t*)in, (int32_t*)out + 1, (int32_t*)ref_out, ws, err, cnt, bad, e0, e1};
       h5.run<0>("n - 5, out 4 B mod 16: shipped");
       h5.run<1>("n - 5, out 4 B mod 16: pipe R8");
