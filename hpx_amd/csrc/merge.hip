@@ -326,12 +326,13 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_merge(const U* __restrict__ i
         __syncthreads();
         nruns = nn;
     }
-    // write-out: a head up to the output's next 16-B boundary, 16-B vectors,
-    // a tail (out 16-B aligned when VEC)
+    // write-out: a head up to the output's next 128-B line, 16-B vectors, a
+    // tail (out 16-B aligned when VEC); line-aligned vectors keep two waves
+    // from writing halves of one line (copy_if_kernel.hpp OUT_ALIGN)
     U* o = out + pos;
     constexpr int V = 16 / sizeof(U);
     using VT = vec<U, V>;
-    const int head = VEC ? min(n, static_cast<int>(((16u - (reinterpret_cast<uintptr_t>(o) & 15u)) & 15u) / sizeof(U)))
+    const int head = VEC ? min(n, static_cast<int>(((128u - (reinterpret_cast<uintptr_t>(o) & 127u)) & 127u) / sizeof(U)))
                          : n;
     const int nvec = (n - head) / V;
     for (int e = threadIdx.x; e < head; e += kMwThreads) o[e] = s[mw_pad(e)];
