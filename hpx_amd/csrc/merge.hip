@@ -89,19 +89,26 @@ int run_merge(const void* a, uint64_t na, const void* b, uint64_t nb, void* out,
 //      keys strictly between v_k and v_{k+1} -- at most (q + p) S = CAP of
 //      them: run j holds fewer than (c_j + 1) S keys between two of its
 //      samples, and at most q samples lie strictly between two splitters --
-//      are staged in LDS and merged there by ceil(log2 p) merge-path rounds
-//      (outputs staged in registers: one LDS buffer, 16 KiB, so several
-//      workgroups share a CU), then written out.  Task k starts at output
+//      are staged in LDS (as ordered bits) and merged there by ceil(log2 p)
+//      merge-path rounds (outputs staged in registers: one LDS buffer,
+//      16 KiB, so several workgroups share a CU), then written out.  Task k starts at output
 //      position sum_j lower_bound_j(v_k); a repeated splitter leaves its
 //      equal keys to the last task holding it.
 // Keys only (equal keys are interchangeable), in the sort's key order.
-// Measured at 2^30 u64 (profiles/r05_merge_runs_probe.log): p = 4 5.8 ms
-// against 6.5 for two pairwise rounds, p = 8 8.5-9.0 against 9.6, p = 2 4.2
+// Measured at 2^30 u64 (profiles/r05_merge_runs_variants.log): p = 4 5.4 ms
+// against 6.5 for two pairwise rounds, p = 8 8.4 against 9.8, p = 2 3.8
 // against 3.3 -- the LDS rounds, not the bytes, bound it; the segmented sort
 // takes it for 4 <= p <= 8.
 inline size_t merge_scratch_bytes_for(uint64_t n) { return ((n + kTile - 1) / kTile + 1) * 8; }
 
-constexpr int kMwThreads = 256;
+// (HPXHIP_MW_THREADS / HPXHIP_MW_MINW: variant builds for the probes only)
+#ifndef HPXHIP_MW_THREADS
+#define HPXHIP_MW_THREADS 256
+#endif
+#ifndef HPXHIP_MW_MINW
+#define HPXHIP_MW_MINW 8
+#endif
+constexpr int kMwThreads = HPXHIP_MW_THREADS;
 constexpr int kMwItems = 8;
 constexpr int kMwCap = kMwThreads * kMwItems;  // keys strictly between two splitters, at most
 constexpr int kMwMaxRuns = 8;
@@ -184,9 +191,10 @@ __device__ __forceinline__ constexpr int mw_pad(int i) { return i + (i >> 3); }
 // then (after the barrier every thread reaches) writes them back.  The pair
 // state is set up by a merge-path search at the thread's first output and
 // restarted (at the pair's start, no search) when the outputs cross into
-// the next pair.
-template <typename U, typename X>
-__device__ __forceinline__ void mw_round(U* s, const int* b, int nruns, int total, X xf) {
+// the next pair.  s holds the keys' ordered bits (staged through xf), so the
+// rounds compare and move plain unsigned words for every dtype.
+template <typename U>
+__device__ __forceinline__ void mw_round(U* s, const int* b, int nruns, int total) {
     const int o0 = static_cast<int>(threadIdx.x) * kMwItems;
     U r[kMwItems];
     int a0 = 0, a1 = 0, b1 = 0, ia = 0, ib = 0, la = 0, lb = 0, pi = 0;
@@ -202,7 +210,7 @@ __device__ __forceinline__ void mw_round(U* s, const int* b, int nruns, int tota
         int lo = dk > lb ? dk - lb : 0, hi = dk < la ? dk : la;
         while (lo < hi) {  // a-elements among the pair's first dk outputs (a first on ties)
             const int mid = (lo + hi) >> 1;
-            if (!(xf(s[mw_pad(a1 + dk - mid - 1)]) < xf(s[mw_pad(a0 + mid)]))) lo = mid + 1;
+            if (!(s[mw_pad(a1 + dk - mid - 1)] < s[mw_pad(a0 + mid)])) lo = mid + 1;
             else hi = mid;
         }
         ia = lo;
@@ -220,7 +228,7 @@ __device__ __forceinline__ void mw_round(U* s, const int* b, int nruns, int tota
         const int o = o0 + q;
         if (o < total) {
             while (o == b1 && 2 * (pi + 1) < nruns) enter(pi + 1, 0);  // (skipping empty pairs)
-            const bool takeb = ia >= la || (ib < lb && xf(vb) < xf(va));
+            const bool takeb = ia >= la || (ib < lb && vb < va);
             if (takeb) {
                 r[q] = vb;
                 ++ib;
@@ -239,15 +247,21 @@ __device__ __forceinline__ void mw_round(U* s, const int* b, int nruns, int tota
     __syncthreads();
 }
 
-// (69 VGPRs, 7 waves per SIMD.  Forcing 8 with __launch_bounds__(256, 8)
-// spilled 22 SGPRs and the float64 instantiation then wrote wrong keys --
-// scripts/mw_debug.py, profiles/r05_merge_runs_debug.log -- so it keeps the
-// default bound.)
+// Keys are staged as ordered bits and turned back at the write-out.  (The
+// first version compared xf(a) < xf(b) inside the rounds; builds with other
+// register budgets -- __launch_bounds__(256, 8), 512 threads -- then wrote
+// some float64 keys in their transformed form, ~bits of the right key
+// (scripts/mw_debug.py, profiles/r05_merge_runs_debug.log): the round loop no
+// longer holds a key in two forms.)  8 waves per SIMD (40-58 VGPRs, no
+// scratch): p = 4 5.4 ms, p = 8 8.4 ms at 2^30 u64, against 5.7 / 8.9 with
+// the default bound and 6.2 / 9.5 with 512 threads
+// (profiles/r05_merge_runs_variants.log).
 template <typename U, typename X, bool VEC>
-__global__ __launch_bounds__(kMwThreads) void k_mw_merge(const U* __restrict__ in, mw_runs r,
-                                                         const uint64_t* __restrict__ LB,
-                                                         const uint64_t* __restrict__ UB, X xf, U* __restrict__ out,
-                                                         uint32_t* __restrict__ err) {
+__global__ __launch_bounds__(kMwThreads, HPXHIP_MW_MINW) void k_mw_merge(const U* __restrict__ in, mw_runs r,
+                                                                          const uint64_t* __restrict__ LB,
+                                                                          const uint64_t* __restrict__ UB, X xf,
+                                                                          U* __restrict__ out,
+                                                                          uint32_t* __restrict__ err) {
     __shared__ alignas(16) U s[mw_pad(kMwCap) + 1];  // (+1: a finished run's head reads one past)
     __shared__ int sbnd[kMwMaxRuns + 1];
     const uint64_t k = blockIdx.x;
@@ -302,12 +316,12 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_merge(const U* __restrict__ i
 #pragma unroll
                     for (int e = 0; e < V; ++e) {
                         const uint64_t i = v * V + e;
-                        if (i >= g0 && i < g1) s[mw_pad(c + static_cast<int>(i - g0))] = x.v[e];
+                        if (i >= g0 && i < g1) s[mw_pad(c + static_cast<int>(i - g0))] = xf(x.v[e]);
                     }
                 }
             } else {
                 const U* src = in + r.off[j] + lo[j];
-                for (int e = threadIdx.x; e < nj; e += kMwThreads) s[mw_pad(c + e)] = ld_stream(&src[e]);
+                for (int e = threadIdx.x; e < nj; e += kMwThreads) s[mw_pad(c + e)] = xf(ld_stream(&src[e]));
             }
             if (threadIdx.x == 0) sbnd[j] = c;
             c += nj;
@@ -317,7 +331,7 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_merge(const U* __restrict__ i
     const int n = c;
     int nruns = static_cast<int>(p);
     while (nruns > 1) {
-        mw_round(s, sbnd, nruns, n, xf);
+        mw_round(s, sbnd, nruns, n);
         const int nn = (nruns + 1) / 2;
         if (threadIdx.x == 0) {
             for (int i = 1; i < nn; ++i) sbnd[i] = sbnd[2 * i];
@@ -335,14 +349,14 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_merge(const U* __restrict__ i
     const int head = VEC ? min(n, static_cast<int>(((128u - (reinterpret_cast<uintptr_t>(o) & 127u)) & 127u) / sizeof(U)))
                          : n;
     const int nvec = (n - head) / V;
-    for (int e = threadIdx.x; e < head; e += kMwThreads) o[e] = s[mw_pad(e)];
+    for (int e = threadIdx.x; e < head; e += kMwThreads) o[e] = xf.inverse(s[mw_pad(e)]);
     for (int q = threadIdx.x; q < nvec; q += kMwThreads) {
         VT w;
 #pragma unroll
-        for (int e = 0; e < V; ++e) w.v[e] = s[mw_pad(head + q * V + e)];
+        for (int e = 0; e < V; ++e) w.v[e] = xf.inverse(s[mw_pad(head + q * V + e)]);
         st_stream(reinterpret_cast<VT*>(o + head) + q, w);
     }
-    for (int e = head + nvec * V + threadIdx.x; e < n; e += kMwThreads) o[e] = s[mw_pad(e)];
+    for (int e = head + nvec * V + threadIdx.x; e < n; e += kMwThreads) o[e] = xf.inverse(s[mw_pad(e)]);
 }
 
 // sample stride S for p runs: the bound (q + p) S <= kMwCap with q = kMwQ p
