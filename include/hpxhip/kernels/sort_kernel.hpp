@@ -960,8 +960,7 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 // planned buckets (bucket b by workgroup b mod gridDim), so a launch the plan
 // skips costs one gate read per workgroup instead of one dispatch per bucket.
 template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16, typename VAL = uint32_t,
-          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false, int MINW = 4, bool PRE16 = false,
-          int ONE = 0>
+          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false, int MINW = 4, bool PRE16 = false>
 __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
     void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf,
                        VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr,
@@ -984,21 +983,13 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     static_assert(THREADS >= kRadix, "one thread per digit in the offset scan");
     __shared__ alignas(16) U s_keys[THREADS * ITEMS];
     __shared__ alignas(16) VAL s_vals[HAS_VAL ? THREADS * ITEMS : 1];
-    // (ONE > 0: rows widened so that the one-pass form's bin counters, s_cnt,
-    // live in the same LDS -- the two are never used together)
-    constexpr int kWhRow = ONE > 0 && (1 << ONE) / WAVES > kRadix ? (1 << ONE) / WAVES : kRadix;
-    __shared__ alignas(16) uint16_t s_whist[WAVES][kWhRow];
+    __shared__ uint16_t s_whist[WAVES][kRadix];
     __shared__ uint32_t s_wsum[kRadix / kWave];
     __shared__ U s_ends[2];
     // PRE16 (r05): the second LDS pass also leaves each key's 16 sorted bits
     // here, so the run detection reads 8 prefixes per 16-B LDS load instead
     // of three 8-B keys per position
     __shared__ alignas(16) uint16_t s_pre[PRE16 ? THREADS * ITEMS + 16 : 1];
-    // ONE (r05): the one-pass form's bin counters, two 16-bit halves per word
-    static_assert(ONE == 0 || (!HAS_VAL && !PRE16 && ((1 << ONE) / 2) % (4 * THREADS) == 0),
-                  "one-pass ranking: keys only, whole 16-B counter groups per thread");
-    uint32_t* const s_cnt = reinterpret_cast<uint32_t*>(&s_whist[0][0]);
-    __shared__ uint32_t s_osum[ONE > 0 ? THREADS / kWave : 1];
 
     const int t_id = threadIdx.x;
     const int lane_ = lane_id();
@@ -1081,7 +1072,7 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     // one stable pass on the digit at `shift`: registers -> s_keys (ranked)
     auto pass = [&](int shift, bool keep_pre) {
         __syncthreads();  // earlier readers of s_keys / s_whist are done
-        for (int i = t; i < WAVES * kWhRow / 2; i += THREADS) reinterpret_cast<uint32_t*>(&s_whist[0][0])[i] = 0;
+        for (int i = t; i < WAVES * kRadix / 2; i += THREADS) reinterpret_cast<uint32_t*>(&s_whist[0][0])[i] = 0;
         __syncthreads();
         // ranks (< 2^16, static_assert above) packed two per register: the
         // kernel sits at the 128-VGPR bound of two workgroups per CU
@@ -1149,122 +1140,12 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
         }
     };
 
-    // ONE > 0 (r05, keys only): ONE pass ranks the keys on the ONE bits under
-    // `top` with LDS atomics on packed 16-bit bin counters (ds_add_rtn: the
-    // order inside a bin is the atomics', which equal-prefix keys do not
-    // need), an exclusive scan turns the counts into bin offsets, and each
-    // key lands at its bin's offset + its rank.  The bin's second arrival
-    // then sorts the bin's keys by insertion (for 4096 random keys in 2^13
-    // bins: 9 % of the bins hold 2 or more, rarely over 5).  A bin over
-    // kRunMax keys sends the segment on to the odd-even rounds.  Returns that
-    // flag, block-wide.  Replaces the two ranked 8-bit passes (wave match
-    // ballots, per-wave histograms) and the run-detection sweep.
-    auto onepass = [&]() -> int {
-        constexpr uint32_t NB = 1u << (ONE > 0 ? ONE : 12), NW = NB / 2;  // (ONE = 0: never called)
-        constexpr int WPT = static_cast<int>(NW) / THREADS;  // counter words per thread
-        using W4 = vec<uint32_t, 4>;
-        const int sh = top > ONE ? top - ONE : 0;
-        __syncthreads();  // s_ends / the previous bucket's s_keys readers are done
-        for (uint32_t i = t; i < NW / 4; i += THREADS) reinterpret_cast<W4*>(s_cnt)[i] = W4{{0u, 0u, 0u, 0u}};
-        __syncthreads();
-        uint32_t rank2[(ITEMS + 1) / 2];
-#pragma unroll
-        for (int r = 0; r < (ITEMS + 1) / 2; ++r) rank2[r] = 0;
-        uint32_t own = 0;  // bit r: key r was its bin's second arrival
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            const uint64_t act = active(r);
-            if (act == 0) break;  // uniform
-            if ((act >> lane) & 1u) {
-                const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> sh) & (NB - 1u);
-                const uint32_t hs = 16u * (d & 1u);
-                const uint32_t rk = (atomicAdd(&s_cnt[d >> 1], 1u << hs) >> hs) & 0xffffu;
-                rank2[r / 2] |= rk << (16 * (r & 1));
-                if (rk == 1) own |= 1u << r;
-            }
-        }
-        __syncthreads();
-        // counts -> exclusive offsets (< 2^16), bins in word order, low half first
-        W4 w[WPT / 4];
-        uint32_t sum = 0;
-#pragma unroll
-        for (int j = 0; j < WPT / 4; ++j) {
-            w[j] = reinterpret_cast<const W4*>(s_cnt)[t * (WPT / 4) + j];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) sum += (w[j].v[e] & 0xffffu) + (w[j].v[e] >> 16);
-        }
-        const uint32_t incl = wave_inclusive_scan(sum, op_plus{});
-        if (lane == kWave - 1) s_osum[wave] = incl;
-        __syncthreads();
-        uint32_t run = incl - sum;
-#pragma unroll
-        for (int v = 0; v < WAVES; ++v)
-            if (v < wave) run += s_osum[v];
-#pragma unroll
-        for (int j = 0; j < WPT / 4; ++j) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t lo = w[j].v[e] & 0xffffu, hi = w[j].v[e] >> 16;
-                w[j].v[e] = run | ((run + lo) << 16);
-                run += lo + hi;
-            }
-            reinterpret_cast<W4*>(s_cnt)[t * (WPT / 4) + j] = w[j];
-        }
-        __syncthreads();
-        auto bin_off = [&](uint32_t d) -> uint32_t {
-            return d < NB ? (s_cnt[d >> 1] >> (16u * (d & 1u))) & 0xffffu : m;
-        };
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            const uint64_t act = active(r);
-            if (act == 0) break;
-            if ((act >> lane) & 1u) {
-                const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> sh) & (NB - 1u);
-                s_keys[bin_off(d) + ((rank2[r / 2] >> (16 * (r & 1))) & 0xffffu)] = k[r];
-            }
-        }
-        __syncthreads();
-        int long_run = 0;
-        if (sh == 0) own = 0;  // the bins hold equal keys
-        // (an unrolled sweep over the owned keys: picking key j out of the
-        // registers by a runtime index put k[] in scratch)
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            if (!((own >> r) & 1u)) continue;
-            const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> sh) & (NB - 1u);
-            const uint32_t s0 = bin_off(d), e0 = bin_off(d + 1);
-            if (e0 - s0 > kRunMax) {
-                long_run = 1;
-                continue;
-            }
-            for (uint32_t p = s0 + 1; p < e0; ++p) {
-                const U x = s_keys[p];
-                uint32_t q = p;
-                while (q > s0 && xf(s_keys[q - 1]) > xf(x)) --q;
-                if (q == p) continue;
-                for (uint32_t c = p; c > q; --c) s_keys[c] = s_keys[c - 1];
-                s_keys[q] = x;
-            }
-        }
-        return __syncthreads_or(long_run);
-    };
-
     // pass schedule (one inlined copy of `pass`): the two passes under
-    // `top` (or, ONE > 0, the one-pass ranking), then -- only for a segment
-    // the odd-even rounds do not settle -- the full LSD over every bit under
-    // `top`
+    // `top`, then -- only for a segment the odd-even rounds do not settle --
+    // the full LSD over every bit under `top`
     bool lsd = false;
     int npass = 2;
     for (int q = 0; q < npass;) {
-        bool ranked = false;  // ONE: the one-pass ranking left a long bin
-        if constexpr (ONE > 0) {
-            if (!lsd) {
-                if (!onepass()) break;
-                q = npass;
-                ranked = true;
-            }
-        }
-        if (!ranked) {
         const int lo = lsd ? top - 8 * (npass - q) : top - 8 * (2 - q);
         pass(lo > 0 ? lo : 0, !lsd && q == 1 && top > 16);
         if (++q < npass) {
@@ -1350,7 +1231,6 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
                 }
             }
             if (!__syncthreads_or(long_run)) break;
-        }
         }
         bool settled = false;
         for (int it = 0; it < OE_MAX && !settled; ++it) {

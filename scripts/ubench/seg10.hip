@@ -6,6 +6,8 @@
 // low bits take only 64 values (long bins: the odd-even / LSD fallback).  The
 // fill is timed alone and subtracted; after each variant the keys are checked
 // sorted and their sum / xor against the fill's.
+// The ONE form lived in sort_kernel.hpp at commit cbbcee4 only (rejected,
+// profiles/r05_ubench_seg10_onepass.log); build against that tree.
 // build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../include seg10.hip -o seg10
 #include <hpxhip/kernels/sort_kernel.hpp>
 
