@@ -108,8 +108,20 @@ inline size_t merge_scratch_bytes_for(uint64_t n) { return ((n + kTile - 1) / kT
 #ifndef HPXHIP_MW_MINW
 #define HPXHIP_MW_MINW 8
 #endif
+#ifndef HPXHIP_MW_ITEMS
+#define HPXHIP_MW_ITEMS 8
+#endif
+// HPXHIP_MW_ROUND: 1 = branch-free merge step (one LDS read per output),
+// 0 = the two-sided step; HPXHIP_MW_ABLATE (probes only, wrong output): 1 =
+// no LDS rounds
+#ifndef HPXHIP_MW_ROUND
+#define HPXHIP_MW_ROUND 1
+#endif
+#ifndef HPXHIP_MW_ABLATE
+#define HPXHIP_MW_ABLATE 0
+#endif
 constexpr int kMwThreads = HPXHIP_MW_THREADS;
-constexpr int kMwItems = 8;
+constexpr int kMwItems = HPXHIP_MW_ITEMS;
 constexpr int kMwCap = kMwThreads * kMwItems;  // keys strictly between two splitters, at most
 constexpr int kMwMaxRuns = 8;
 constexpr uint32_t kMwQ = 3;  // splitters every kMwQ * p samples
@@ -228,6 +240,18 @@ __device__ __forceinline__ void mw_round(U* s, const int* b, int nruns, int tota
         const int o = o0 + q;
         if (o < total) {
             while (o == b1 && 2 * (pi + 1) < nruns) enter(pi + 1, 0);  // (skipping empty pairs)
+#if HPXHIP_MW_ROUND == 1
+            // one LDS read per output: the head of the side taken (an
+            // exhausted side's index reads the other run's first key or the
+            // pad element past the last run, never used)
+            const bool takeb = ib < lb && (ia >= la || vb < va);
+            r[q] = takeb ? vb : va;
+            ia += takeb ? 0 : 1;
+            ib += takeb ? 1 : 0;
+            const U nv = s[mw_pad(takeb ? a1 + ib : a0 + ia)];
+            va = takeb ? va : nv;
+            vb = takeb ? nv : vb;
+#else
             const bool takeb = ia >= la || (ib < lb && vb < va);
             if (takeb) {
                 r[q] = vb;
@@ -238,6 +262,7 @@ __device__ __forceinline__ void mw_round(U* s, const int* b, int nruns, int tota
                 ++ia;
                 va = s[mw_pad(a0 + (ia < la ? ia : 0))];
             }
+#endif
         }
     }
     __syncthreads();
@@ -300,7 +325,10 @@ __global__ __launch_bounds__(kMwThreads, HPXHIP_MW_MINW) void k_mw_merge(const U
         if (threadIdx.x == 0) raise_device_error(err, HPXHIP_DEVERR_RANGE);
         return;
     }
-    // stage the runs' middle parts back to back
+    // stage the runs' middle parts back to back (a loop per run: staging
+    // flattened over the runs -- every load issued before the first LDS
+    // store -- measured slower, r05 lease ai: p = 2 4.34 vs 3.65 ms, p = 8
+    // 7.74 vs 7.75)
     int c = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kMwMaxRuns; ++j)
@@ -329,7 +357,7 @@ __global__ __launch_bounds__(kMwThreads, HPXHIP_MW_MINW) void k_mw_merge(const U
     if (threadIdx.x == 0) sbnd[p] = c;
     __syncthreads();
     const int n = c;
-    int nruns = static_cast<int>(p);
+    int nruns = HPXHIP_MW_ABLATE ? 1 : static_cast<int>(p);
     while (nruns > 1) {
         mw_round(s, sbnd, nruns, n);
         const int nn = (nruns + 1) / 2;

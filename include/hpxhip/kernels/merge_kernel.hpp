@@ -106,21 +106,21 @@ __device__ __forceinline__ void merge_in_lds(T* s, int la, int lb, const Less& l
     }
     int ia = lo, ib = dk - lo;
     T r[kItems];
-    // the heads of both runs stay in registers (one LDS read per output)
+    // the heads of both runs stay in registers; branch-free step (r05, as
+    // hpxhip_merge_runs' mw_round): one LDS read per output, the head of the
+    // side taken (an exhausted side's index reads a key never used)
     T va = s[ia < la ? ia : 0];
     T vb = s[la + ib < len ? la + ib : 0];
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
-        const bool takeb = ia >= la || (ib < lb && less(vb, va));
-        if (takeb) {
-            r[k] = vb;
-            ++ib;
-            vb = s[la + ib < len ? la + ib : 0];
-        } else {
-            r[k] = va;
-            ++ia;
-            va = s[ia < la ? ia : 0];
-        }
+        const bool takeb = ib < lb && (ia >= la || less(vb, va));
+        r[k] = takeb ? vb : va;
+        ia += takeb ? 0 : 1;
+        ib += takeb ? 1 : 0;
+        const int ni = takeb ? la + ib : ia;
+        const T nv = s[ni < len ? ni : 0];
+        va = takeb ? va : nv;
+        vb = takeb ? nv : vb;
     }
     __syncthreads();
 #pragma unroll

@@ -34,6 +34,10 @@ __device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 
 #ifndef HPXHIP_MATCH_ASM
 #define HPXHIP_MATCH_ASM 1
 #endif
+// the segment sort's first LDS pass ranked by LDS atomics (k_bucket_sort)
+#ifndef HPXHIP_SEG_ATOM1
+#define HPXHIP_SEG_ATOM1 0
+#endif
 template <int BITS = 8>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
     uint32_t lo = static_cast<uint32_t>(active), hi = static_cast<uint32_t>(active >> 32);
@@ -1069,8 +1073,12 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     }
     if (top <= 0) return;  // all keys equal
 
-    // one stable pass on the digit at `shift`: registers -> s_keys (ranked)
-    auto pass = [&](int shift, bool keep_pre) {
+    // one stable pass on the digit at `shift`: registers -> s_keys (ranked).
+    // atom (HPXHIP_SEG_ATOM1, keys only): the first pass under `top` ranks by
+    // LDS atomics on the packed 16-bit per-wave counters instead of the
+    // wave match -- its order inside a digit is arbitrary, which the second
+    // (stable) pass and the insertion inside runs never depend on
+    auto pass = [&](int shift, bool keep_pre, bool atom) {
         __syncthreads();  // earlier readers of s_keys / s_whist are done
         for (int i = t; i < WAVES * kRadix / 2; i += THREADS) reinterpret_cast<uint32_t*>(&s_whist[0][0])[i] = 0;
         __syncthreads();
@@ -1084,6 +1092,15 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
             const uint64_t act = active(r);
             if (act == 0) break;  // uniform
             const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & 0xffu;
+            if (HPXHIP_SEG_ATOM1 && !HAS_VAL && atom) {
+                if ((act >> lane) & 1u) {
+                    const uint32_t sh = 16u * (d & 1u);
+                    const uint32_t old =
+                        atomicAdd(reinterpret_cast<uint32_t*>(&s_whist[wave][0]) + (d >> 1), 1u << sh);
+                    rank2[r / 2] |= ((old >> sh) & 0xffffu) << (16 * (r & 1));
+                }
+                continue;
+            }
             const uint64_t peers = match_digit(d, act);
             const uint32_t below = peers_below(peers);
             const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(peers));
@@ -1147,7 +1164,7 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     int npass = 2;
     for (int q = 0; q < npass;) {
         const int lo = lsd ? top - 8 * (npass - q) : top - 8 * (2 - q);
-        pass(lo > 0 ? lo : 0, !lsd && q == 1 && top > 16);
+        pass(lo > 0 ? lo : 0, !lsd && q == 1 && top > 16, !lsd && q == 0);
         if (++q < npass) {
             reload();
             continue;

