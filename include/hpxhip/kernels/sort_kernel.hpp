@@ -38,6 +38,10 @@ __device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 
 #ifndef HPXHIP_SEG_ATOM1
 #define HPXHIP_SEG_ATOM1 0
 #endif
+// the offset-fed first prefix pass ranked by LDS atomics (k_onesweep)
+#ifndef HPXHIP_OS_ATOM1
+#define HPXHIP_OS_ATOM1 0
+#endif
 template <int BITS = 8>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
     uint32_t lo = static_cast<uint32_t>(active), hi = static_cast<uint32_t>(active >> 32);
@@ -613,7 +617,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     // SEG: the segment table, loaded once per (persistent) workgroup, so a
     // tile's segment costs LDS reads, not a chain of global loads per tile
     __shared__ uint64_t s_sg[SEG ? 3 * kMaxBig + 2 : 1];
-    __shared__ CT s_whist[WAVES][R];
+    __shared__ alignas(16) CT s_whist[WAVES][R];
     __shared__ uint32_t s_local[R];
     __shared__ uint32_t s_wsum[R / kWave];
     __shared__ uint64_t s_adj[R];
@@ -735,6 +739,23 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
         const uint64_t i = wbase + r * kWave + lane;
         const bool valid = full || i < end;
         const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
+        if constexpr (HPXHIP_OS_ATOM1 && LBB < 0 && !HAS_VAL) {
+            // the offset-fed first prefix pass of a keys-only sort (its order
+            // inside a digit is never relied on: the second pass is stable
+            // and the segment sort orders every bucket completely) ranks by
+            // LDS atomics on the per-wave counters instead of the wave match
+            if (valid) {
+                if constexpr (sizeof(CT) == 2) {
+                    const uint32_t sh = 16u * (d & 1u);
+                    const uint32_t old =
+                        atomicAdd(reinterpret_cast<uint32_t*>(&s_whist[wave][0]) + (d >> 1), 1u << sh);
+                    rank[r] = (old >> sh) & 0xffffu;
+                } else {
+                    rank[r] = atomicAdd(reinterpret_cast<uint32_t*>(&s_whist[wave][d]), 1u);
+                }
+            }
+            continue;
+        }
         const uint64_t peers = match_digit<RB>(d, __ballot(valid));
         const uint32_t below = peers_below(peers);
         const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(peers));
@@ -987,7 +1008,7 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     static_assert(THREADS >= kRadix, "one thread per digit in the offset scan");
     __shared__ alignas(16) U s_keys[THREADS * ITEMS];
     __shared__ alignas(16) VAL s_vals[HAS_VAL ? THREADS * ITEMS : 1];
-    __shared__ uint16_t s_whist[WAVES][kRadix];
+    __shared__ alignas(16) uint16_t s_whist[WAVES][kRadix];
     __shared__ uint32_t s_wsum[kRadix / kWave];
     __shared__ U s_ends[2];
     // PRE16 (r05): the second LDS pass also leaves each key's 16 sorted bits
