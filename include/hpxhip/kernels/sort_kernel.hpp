@@ -34,13 +34,16 @@ __device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 
 #ifndef HPXHIP_MATCH_ASM
 #define HPXHIP_MATCH_ASM 1
 #endif
-// the segment sort's first LDS pass ranked by LDS atomics (k_bucket_sort)
+// the segment sort's first LDS pass ranked by LDS atomics (k_bucket_sort;
+// r05 lease ak, profiles/r05_merge_step_seg_atom1.log: no change, off)
 #ifndef HPXHIP_SEG_ATOM1
 #define HPXHIP_SEG_ATOM1 0
 #endif
-// the offset-fed first prefix pass ranked by LDS atomics (k_onesweep)
+// the offset-fed first prefix pass ranked by LDS atomics (k_onesweep; r05
+// lease al, profiles/r05_sort_os_atom1.log: 2^30 u32 12.16 -> 11.62 ms, u64
+// unchanged at 16.1)
 #ifndef HPXHIP_OS_ATOM1
-#define HPXHIP_OS_ATOM1 0
+#define HPXHIP_OS_ATOM1 1
 #endif
 template <int BITS = 8>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
