@@ -607,19 +607,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             // lines at the ends of their digit runs meet in the caches
             // r05: tiles in 8 contiguous regions, one per XCD (XREG): 4.75 ->
             // 3.81 ms at 2^30 u64 (profiles/r05_ubench_sortpass5.log)
-            if constexpr (!HAS_VAL && HPXHIP_PREFIX_PIPE && TS::threads == kXBins) {
-                // workgroups per CU: the LDS holds two (64-bit keys) or three
-                // (32-bit keys) of them; HPXHIP_PIPE_WG overrides (probes)
-                static const int env_wg = [] {
-                    const char* e = std::getenv("HPXHIP_PIPE_WG");
-                    return e ? std::atoi(e) : 0;
-                }();
-                const int wg = env_wg > 0 ? env_wg : (sizeof(U) == 8 ? 2 : 3);
-                const uint64_t pcap = static_cast<uint64_t>(wg) * current_device_info().cus;
-                hipLaunchKernelGGL((k_prefix_pipe<U, X, TS::threads, TS::items>),
-                                   dim3(static_cast<unsigned>(nt > pcap ? pcap : nt)), block, 0, s, kin, kout, n, 0,
-                                   counter, err, X{}, word, nt, pre);
-            } else if constexpr (!HAS_VAL)
+            if constexpr (!HAS_VAL)
                 hipLaunchKernelGGL((k_onesweep<U, VAL, false, uint32_t, X, TS::threads, TS::items, -1, 9, true, false,
                                                false, false, true>),
                                    grid, block, 0, s, kin, kout, vin, vout, n, 0, b9,

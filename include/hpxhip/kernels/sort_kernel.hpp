@@ -45,12 +45,6 @@ __device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 
 #ifndef HPXHIP_OS_ATOM1
 #define HPXHIP_OS_ATOM1 1
 #endif
-// the offset-fed first prefix pass of a keys-only sort as a pipelined
-// persistent kernel (k_prefix_pipe: the next tile's loads run under this
-// tile's write-out) instead of k_onesweep's one tile per workgroup
-#ifndef HPXHIP_PREFIX_PIPE
-#define HPXHIP_PREFIX_PIPE 0
-#endif
 template <int BITS = 8>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
     uint32_t lo = static_cast<uint32_t>(active), hi = static_cast<uint32_t>(active >> 32);
@@ -914,155 +908,6 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
         while (one()) __syncthreads();  // the tile's LDS readers are done before the next claim
     } else {
         one();
-    }
-}
-
-// ------------------------------------------- pipelined offset-fed prefix pass
-// The first 9-bit prefix pass of a keys-only 18-bit sort (k_onesweep with
-// LBB < 0 and XREG) as a persistent kernel, two workgroups per CU.  Its tiles
-// need no look-back -- every tile's destinations come precomputed from the
-// histogram read (k_tile_offsets) -- so a workgroup can claim its next tile
-// (from its XCD's region, as XREG does) and issue that tile's loads into the
-// key registers the moment the current tile sits ranked in LDS; the current
-// tile's write-out from LDS then runs under those loads, as the copy_if pipe
-// does (k_copy_if_pipe).  One tile per workgroup leaves the load and store
-// phases of a workgroup serial and overlaps them only across its CU's two
-// workgroups.  Ranking by LDS atomics on packed 16-bit per-wave counters (the
-// pass's order inside a digit is never relied on: the second prefix pass is
-// stable and the segment sort orders every bucket completely).
-template <typename U, typename X, int THREADS = 512, int ITEMS = 16>
-__global__ __launch_bounds__(THREADS) void k_prefix_pipe(const U* __restrict__ kin, U* __restrict__ kout, uint64_t n,
-                                                          int shift, uint32_t* __restrict__ counter,
-                                                          uint32_t* __restrict__ err, X xf,
-                                                          const int32_t* __restrict__ ctl, uint64_t ntiles,
-                                                          const uint32_t* __restrict__ pre) {
-    if (ctl) {
-        const int32_t sh = *ctl;
-        if (sh < 0) return;
-        shift = sh;
-    }
-    constexpr int R = kXBins;
-    constexpr uint32_t DMASK = R - 1;
-    constexpr int WAVES = THREADS / kWave;
-    constexpr int TILE = THREADS * ITEMS;
-    static_assert(THREADS == R, "one thread per digit");
-    static_assert(TILE < 65536, "16-bit per-wave counters");
-    __shared__ uint32_t s_tile;
-    __shared__ alignas(16) uint16_t s_whist[WAVES][R];
-    __shared__ uint32_t s_wsum[R / kWave];
-    __shared__ uint64_t s_adj[R];
-    __shared__ U s_keys[TILE];
-
-    // the next tile of this XCD's region (8 contiguous regions of tiles, one
-    // counter word per region 8 words apart, zeroed before the pass); a
-    // region that is done sends the workgroup on to the next; ~0 = all done
-    auto claim = [&]() -> uint32_t {
-        const uint32_t x = xcc_id();
-        const uint64_t per = (ntiles + 7) / 8;
-        for (uint32_t j = 0; j < 8; ++j) {
-            const uint32_t xr = (x + j) & 7u;
-            const uint64_t lo = xr * per;
-            const uint64_t cnt = lo < ntiles ? (ntiles - lo < per ? ntiles - lo : per) : 0;
-            if (cnt == 0) continue;
-            const uint32_t c = __hip_atomic_fetch_add(counter + 8 * xr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (c < cnt) return static_cast<uint32_t>(lo + c);
-        }
-        return 0xffffffffu;
-    };
-    U k[ITEMS];
-    auto load = [&](uint32_t tl, int t) {
-        const uint64_t wb = static_cast<uint64_t>(tl) * TILE + static_cast<uint64_t>(t / kWave) * (TILE / WAVES);
-        const int ln = t % kWave;
-        const bool full = (static_cast<uint64_t>(tl) + 1) * TILE <= n;
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            const uint64_t i = wb + r * kWave + ln;
-            k[r] = (full || i < n) ? kin[i] : U(0);
-        }
-    };
-    if (threadIdx.x == 0) s_tile = claim();
-    __syncthreads();
-    uint32_t tile = s_tile;
-    if (tile == 0xffffffffu) return;  // uniform
-    load(tile, threadIdx.x);
-    for (;;) {
-        // ids re-derived per tile (k_onesweep PERSIST: otherwise the compiler
-        // keeps every lane-dependent address of the body live across the loop)
-        int t = threadIdx.x, lane = lane_id();
-        asm volatile("" : "+v"(t), "+v"(lane));
-        const int wave = t / kWave;
-        const uint64_t tile_base = static_cast<uint64_t>(tile) * TILE;
-        const bool full = tile_base + TILE <= n;
-        const uint64_t wbase = tile_base + static_cast<uint64_t>(wave) * (TILE / WAVES);
-        for (int i = t; i < WAVES * R / 2; i += THREADS) reinterpret_cast<uint32_t*>(&s_whist[0][0])[i] = 0;
-        __syncthreads();
-        uint32_t rank[ITEMS];
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            const uint64_t i = wbase + r * kWave + lane;
-            rank[r] = 0;
-            if (full || i < n) {
-                const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
-                const uint32_t sh = 16u * (d & 1u);
-                const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(&s_whist[wave][0]) + (d >> 1), 1u << sh);
-                rank[r] = (old >> sh) & 0xffffu;
-            }
-        }
-        __syncthreads();
-        // thread t owns digit t: its count over the waves, the tile's
-        // exclusive prefix, the per-wave bases as tile positions
-        uint32_t tile_count = 0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) {
-            const uint32_t c = s_whist[w][t];
-            s_whist[w][t] = static_cast<uint16_t>(tile_count);
-            tile_count += c;
-        }
-        const uint32_t incl = wave_inclusive_scan(tile_count, op_plus{});
-        if (lane == kWave - 1) s_wsum[wave] = incl;
-        __syncthreads();
-        {
-            uint32_t p = 0;
-#pragma unroll
-            for (int w = 0; w < R / kWave; ++w)
-                if (w < wave) p += s_wsum[w];
-            const uint32_t loc = p + incl - tile_count;
-#pragma unroll
-            for (int w = 0; w < WAVES; ++w) s_whist[w][t] = static_cast<uint16_t>(s_whist[w][t] + loc);
-            s_adj[t] = static_cast<uint64_t>(pre[static_cast<uint64_t>(tile) * R + t]) - loc;
-        }
-        __syncthreads();
-        // counting sort of the tile into LDS
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            const uint64_t i = wbase + r * kWave + lane;
-            if (full || i < n) {
-                const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
-                s_keys[s_whist[wave][d] + rank[r]] = k[r];
-            }
-        }
-        if (t == 0) s_tile = claim();
-        __syncthreads();
-        const uint32_t next = s_tile;
-        // the next tile's loads go out before this tile's write-out
-        if (next != 0xffffffffu) load(next, t);
-        const uint32_t nvalid = full ? TILE : static_cast<uint32_t>(n - tile_base);
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            const uint32_t i = r * THREADS + t;
-            if (i < nvalid) {
-                const U key = s_keys[i];
-                const uint32_t d = static_cast<uint32_t>(xf(key) >> shift) & DMASK;
-                const uint64_t dst = s_adj[d] + i;
-                // as k_onesweep: a destination past the array (keys changed
-                // while the sort ran) is reported, never stored
-                if (dst < n) kout[dst] = key;
-                else raise_device_error(err, HPXHIP_DEVERR_RANGE);
-            }
-        }
-        if (next == 0xffffffffu) break;  // uniform: every wave leaves here
-        __syncthreads();  // this tile's LDS readers are done
-        tile = next;
     }
 }
 
