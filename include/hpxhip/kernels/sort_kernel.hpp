@@ -45,6 +45,16 @@ __device__ __forceinline__ G enc_incl(uint64_t v) { return static_cast<G>((v << 
 #ifndef HPXHIP_OS_ATOM1
 #define HPXHIP_OS_ATOM1 1
 #endif
+// k_onesweep's tile loads without per-key branches (r05 lease ap,
+// profiles/r05_sort_uncond_load.log: first prefix pass ~4.2 -> 3.95 ms, 2^30
+// u64 16.48-16.57 -> 15.92-16.06 ms, u32 11.65-11.70 -> 11.41-11.51)
+#ifndef HPXHIP_OS_UNCOND_LOAD
+#define HPXHIP_OS_UNCOND_LOAD 1
+#endif
+// ... and k_bucket_sort's segment loads
+#ifndef HPXHIP_SEG_UNCOND_LOAD
+#define HPXHIP_SEG_UNCOND_LOAD 0
+#endif
 template <int BITS = 8>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
     uint32_t lo = static_cast<uint32_t>(active), hi = static_cast<uint32_t>(active >> 32);
@@ -724,6 +734,21 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     U k[ITEMS];
     VAL v[HAS_VAL ? ITEMS : 1];
     const bool full = tile_base + TILE <= end;
+#if HPXHIP_OS_UNCOND_LOAD
+    // unconditional loads (a ragged tile's lanes past `end` load its last
+    // element, never ranked or stored): with one load per exec-masked branch
+    // the compiler waits for all of them (vmcnt(0)) before the first rank
+    {
+        const uint64_t last = end - 1;
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const uint64_t i = wbase + r * kWave + lane;
+            const uint64_t j = (full || i < end) ? i : last;
+            k[r] = kin[j];
+            if constexpr (HAS_VAL) v[r] = vin[j];
+        }
+    }
+#else
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = wbase + r * kWave + lane;
@@ -734,6 +759,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             k[r] = 0;
         }
     }
+#endif
 
     // ---- wave-level match ranking (stable: round-major, then lane order)
     uint32_t rank[ITEMS];
@@ -1065,12 +1091,24 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
 
     U k[ITEMS];
     VAL v[HAS_VAL ? ITEMS : 1];
+#if HPXHIP_SEG_UNCOND_LOAD
+    // unconditional loads, as k_onesweep's (lanes past the segment load its
+    // last key; every pass below gates them out by active())
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const bool on = (active(r) >> lane) & 1u;
+        const uint32_t j = on ? wbase + r * kWave + lane : m - 1;
+        k[r] = ld_stream(&gkeys[j]);
+        if constexpr (HAS_VAL) v[r] = ld_stream(&gvals[j]);
+    }
+#else
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const bool on = (active(r) >> lane) & 1u;
         k[r] = on ? ld_stream(&gkeys[wbase + r * kWave + lane]) : U(0);
         if constexpr (HAS_VAL) v[r] = on ? ld_stream(&gvals[wbase + r * kWave + lane]) : VAL(0);
     }
+#endif
     // The segment's first and last keys (their highest differing bit is the
     // top of the LDS passes) come from the registers just loaded, through
     // LDS: reading them from global memory first had put one more dependent
