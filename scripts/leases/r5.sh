@@ -759,4 +759,19 @@ lease_ar() {
   echo "rocprof ok" >> ${L}_status.log
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a aa ab ac ad ae ag ah ai aj ak al am an ao ap aq ar b c d e f g h i j k l m n o p q r s t u v w x y z"; fi
+# ---- lease as (added after the fold)
+lease_as() {
+  # round 5, lease as: PMC passes (one counter group per run) over the 2^30 u64 sort with the onesweep tile
+  # loads without per-key branches (the round's last sort) -- FETCH_SIZE, WRITE_SIZE, LDS / wave counters
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  i=0
+  for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"; do
+    i=$((i+1))
+    SORT_ONLY=u64 timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d gpurun_out/r5as_pmc_sort$i -o run -- python3 scripts/sort_probe.py 30 > gpurun_out/r5as_pmc_sort$i.log 2>&1 || exit 1
+  done
+  python3 scripts/pmc_summary.py gpurun_out/r5as_pmc_sort1 gpurun_out/r5as_pmc_sort2 gpurun_out/r5as_pmc_sort3 > gpurun_out/r5as_pmc_sort.txt 2>&1
+  echo ok
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a aa ab ac ad ae ag ah ai aj ak al am an ao ap aq ar b c d e f g h i j k l m n o p q r s t u v w x y z as"; fi
