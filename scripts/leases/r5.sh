@@ -774,4 +774,18 @@ lease_as() {
   echo ok
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a aa ab ac ad ae ag ah ai aj ak al am an ao ap aq ar b c d e f g h i j k l m n o p q r s t u v w x y z as"; fi
+# ---- lease at (added after the fold)
+lease_at() {
+  # round 5, lease at: the round's last sort over the size sweep (2^20..2^30, u64 / u32 / pairs) and the
+  # skewed cases at 2^28 (u64hot, u64corr, u64r16, u64r24) -- regression check of the branch-free tile loads
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r5at
+  timeout -k 10 300 python -u scripts/sort_probe.py 30 > ${L}_sweep.log 2>&1 || exit $?
+  for c in u64hot u64corr u64r16 u64r24; do
+    SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 28 > ${L}_$c.log 2>&1 || exit $?
+    echo "$c: $(grep -v '^#' ${L}_$c.log | tail -1)" >> ${L}_status.log
+  done
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a aa ab ac ad ae ag ah ai aj ak al am an ao ap aq ar b c d e f g h i j k l m n o p q r s t u v w x y z as at"; fi
