@@ -21,7 +21,7 @@ KHDR     := $(wildcard hpx_amd/csrc/*.hpp) $(wildcard include/hpxhip/kernels/*.h
 ORACLE   := oracle/_build/liboracle.so
 OFLAGS   := -O2 -fPIC -std=c++17 -ffp-contract=off -Wall -pthread
 
-.PHONY: all lib oracle clean cxxtests oracle-sanitize
+.PHONY: all lib oracle clean cxxtests oracle-sanitize mw-variants
 
 # C++ tests of include/hpx (plain g++ host code linked to the C ABI library)
 CXXT     := compute_api algorithms_known_answer stream_hip for_loop_merge stencil_partitioned call_overhead exception_list futures
@@ -31,7 +31,7 @@ TFLAGS   := -O2 -std=c++17 -Wall -Wextra -Wno-unused-parameter -pthread -Iinclud
 TLINK    := -Lhpx_amd -lhpxhip -Wl,-rpath,'$$ORIGIN/../../../hpx_amd' -Wl,-rpath,/opt/rocm/lib \
             -Wl,-rpath-link,/opt/rocm/lib
 
-all: lib oracle
+all: lib oracle mw-variants
 
 lib: $(LIB)
 oracle: $(ORACLE)
@@ -42,6 +42,38 @@ $(BUILD)/csrc/%.o: hpx_amd/csrc/%.hip $(KHDR)
 
 $(LIB): $(KOBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(KOBJ)
+
+# merge.hip: the multiway merge (k_mw_merge) must not spill SGPRs.  An
+# earlier form of it, built at 8 waves per SIMD with 20-22 SGPR spills, was
+# miscompiled (registers of live outputs reused as temporaries in a divergent
+# branch: float64 keys written in their ordered-bit form; DESIGN.md (e),
+# profiles/r06_mw_merge_miscompile.txt).  The build refuses a k_mw_merge
+# instantiation with spills instead of shipping one.
+define mw_spill_guard
+	@awk '/Function Name:/ {k = ($$0 ~ /k_mw_merge/)} k && /SGPRs Spill: [1-9]/ {bad = 1; print} \
+	     END {if (bad) {print "merge.hip: k_mw_merge spills SGPRs (see Makefile)"; exit 1}}' $(1)
+endef
+$(BUILD)/csrc/merge.o: hpx_amd/csrc/merge.hip $(KHDR)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $(BUILD)/csrc/merge.usage || \
+	    (cat $(BUILD)/csrc/merge.usage; rm -f $@; exit 1)
+	$(call mw_spill_guard,$(BUILD)/csrc/merge.usage) || (rm -f $@; exit 1)
+
+# Variant builds of the multiway merge kept in the standing test matrix
+# (tests/test_gpu_merge_sort.py::test_merge_runs_variant_builds):
+# 512-thread tasks, and 256 threads at the default occupancy bound.  Each is
+# library of its own (hpx_amd/variants/<name>/), the shipped objects but merge.o.
+MWVAR    := mw512 mwminw4
+MWVAR_mw512   := -DHPXHIP_MW_THREADS=512 -DHPXHIP_MW_MINW=4
+MWVAR_mwminw4 := -DHPXHIP_MW_MINW=4
+mw-variants: $(MWVAR:%=hpx_amd/variants/%/libhpxhip.so)
+hpx_amd/variants/%/libhpxhip.so: hpx_amd/csrc/merge.hip $(filter-out $(BUILD)/csrc/merge.o,$(KOBJ)) $(KHDR)
+	@mkdir -p $(dir $@) $(BUILD)/variants/$*
+	$(HIPCC) $(HIPFLAGS) $(MWVAR_$*) -Rpass-analysis=kernel-resource-usage -c $< -o $(BUILD)/variants/$*/merge.o \
+	    2> $(BUILD)/variants/$*/merge.usage || (cat $(BUILD)/variants/$*/merge.usage; exit 1)
+	$(call mw_spill_guard,$(BUILD)/variants/$*/merge.usage)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(filter-out $(BUILD)/csrc/merge.o,$(KOBJ)) \
+	    $(BUILD)/variants/$*/merge.o
 
 $(ORACLE): oracle/oracle.cpp oracle/oracle.h
 	@mkdir -p $(dir $@)
@@ -75,4 +107,4 @@ tests/cxx/bin/dataflow_stencil: tests/cxx/dataflow_stencil.hip $(CXXHDR) $(LIB) 
 	$(HIPCC) $(HTFLAGS) $< -o $@ $(TLINK) -Loracle/_build -loracle -Wl,-rpath,'$$ORIGIN/../../../oracle/_build'
 
 clean:
-	rm -rf $(BUILD) $(LIB) oracle/_build tests/cxx/bin
+	rm -rf $(BUILD) $(LIB) oracle/_build tests/cxx/bin hpx_amd/variants

@@ -152,6 +152,8 @@ def main(argv=None, comm_tgt=None):
     ap.add_argument("--cpu-logn", type=int, default=27)
     ap.add_argument("--stencil-logn", type=int, default=32, help="1d_stencil points (total over the ranks)")
     ap.add_argument("--stencil-steps", type=int, default=100)
+    ap.add_argument("--strong-logn", type=int, default=32,
+                    help="segmented reduce / scan strong-scaling row: elements in total over the ranks")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--triad-only", action="store_true", help=argparse.SUPPRESS)  # PMC child mode
     # launcher check without a GPU: the ranks rendezvous over gloo and report
@@ -344,6 +346,7 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
                             "pct_peak": pct(12 * n / ms / 1e6), "hits": hits,
                             "gbs_actual_bytes": round((8 * n + 8 * hits) / ms / 1e6, 1)}
     res["segmented_reduce_int64"] = seg_reduce_row(S, F, comm, tgt, pol, x)
+    res["strong_2p32_int64"] = strong_row(S, F, comm, tgt, pol, args.strong_logn)
     res["double_reduce_scan"] = double_row(hpx, L, P, F, tgt, pol, tpol, n)
     res["stream_2p30"] = stream_row(hpx, L, P, F, tgt, pol, n)
     # sort of 2^30 uint64 keys (8 GiB + 8 GiB workspace)
@@ -357,8 +360,7 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
     res["sort_uint64"] = {"ms": round(ms_sort, 3), "gkeys_per_s": round(n / ms_sort / 1e6, 3),
                           "path": "hybrid: 2 x 9-bit prefix passes + LDS segment sort of ~4096-key buckets",
                           "gbs_executed_56B": round(56 * n / ms_sort / 1e6, 1),
-                          "pct_peak": pct(56 * n / ms_sort / 1e6),
-                          "gbs_lsd_equivalent_136B": round(136 * n / ms_sort / 1e6, 1)}
+                          "pct_peak": pct(56 * n / ms_sort / 1e6)}
     res["sort_uint64"].update(sort_check(P, F, pol, tgt, keys, regen))
     keys.free()
     # 32-bit keys: the hybrid (4 B/key histogram + two 8 B/key prefix passes +
@@ -369,7 +371,7 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
     ms32 = timed(L, tgt, lambda: (regen32(), P.sort(pol, k32.begin(), k32.end())), reps=2) - ms_gen
     res["sort_uint32"] = {"keys": n, "ms": round(ms32, 3), "gkeys_per_s": round(n / ms32 / 1e6, 3),
                           "path": "hybrid (18-bit prefix: two 9-bit passes + LDS segment sort)", "gbs_executed_28B": round(28 * n / ms32 / 1e6, 1),
-                          "gbs_lsd_equivalent_36B": round(36 * n / ms32 / 1e6, 1)}
+                          "pct_peak": pct(28 * n / ms32 / 1e6)}
     k32.free()
     nkv = n // 4
     kk = hpx.vector(nkv, dtype=np.uint64, tgt=tgt)
@@ -385,7 +387,7 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
     res["sort_by_key_u64_u64"] = {"pairs": nkv, "ms": round(mskv, 3), "gpairs_per_s": round(nkv / mskv / 1e6, 3),
                                   "path": "hybrid: 2 prefix passes + LDS segment sort (values staged beside keys)",
                                   "gbs_executed_104B": round(104 * nkv / mskv / 1e6, 1),
-                                  "gbs_lsd_equivalent_264B": round(264 * nkv / mskv / 1e6, 1), "keys_sorted": ok}
+                                  "pct_peak": pct(104 * nkv / mskv / 1e6), "keys_sorted": ok}
     kk.free()
     vv.free()
     # 1d_stencil heat: 2^32 points, 100 steps (BASELINE.md plan), through the
@@ -515,6 +517,54 @@ def seg_reduce_row(S, F, comm, tgt, pol, x, reps=5):
             "pct_peak_per_rank": pct(per_rank), "value": int(r)}
 
 
+def strong_row(S, F, comm, tgt, pol, logn, reps=5):
+    """Strong scaling of the segmented algorithms (2^32 int64 in
+    total, the north star's >= 7x node-scaling target is stated on segmented
+    reduce): one int64 partitioned_vector of 2^logn elements over the ranks,
+    segmented reduce (segmented_algorithms/reduce.hpp:112-209) and segmented
+    inclusive_scan (detail/scan.hpp:527-696), each `reps` back-to-back calls
+    under the plain par policy (reduce returns its value: a host round trip
+    per call) between barriers, max over ranks.  Bytes: 8 B/elem (reduce), 16
+    B/elem at N = 1 and 24 at N > 1 (scan: the totals pass, the reference's
+    step 1).  Check: the scan's last element == the reduce (int64 exact) on
+    the last rank, max-over-ranks agreed."""
+    import time
+    n = 1 << logn
+    x = S.partitioned_vector(n, np.int64, comm=comm, tgt=tgt)
+    y = S.partitioned_vector(n, np.int64, comm=comm, tgt=tgt)
+    S.algorithms.generate(pol, x.begin(), x.end(), "range", 0x5EED, -(1 << 20), 1 << 20)
+    tgt.synchronize()
+
+    def run(fn):
+        fn()
+        tgt.synchronize()
+        comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn()
+        tgt.synchronize()
+        comm.barrier()
+        return max_over_ranks(comm, (time.perf_counter() - t0) / reps), r
+
+    t_red, total = run(lambda: S.algorithms.reduce(pol, x.begin(), x.end(), 0, F.plus))
+    t_scan, _ = run(lambda: S.algorithms.inclusive_scan(pol, x.begin(), x.end(), y.begin(), F.plus, 0))
+    ok = True
+    if comm.rank == comm.size - 1 and len(y.local):
+        ok = int(y.local[len(y.local) - 1]) == int(total)
+    ok = bool(max_over_ranks(comm, 0.0 if ok else 1.0) == 0.0)
+    x.local.free()
+    y.local.free()
+    scan_b = 16 if comm.size == 1 else 24
+    return {"elements_total": n, "elements_per_rank": n // comm.size, "ranks": comm.size, "scaling": "strong",
+            "reduce_ms": round(1e3 * t_red, 4), "reduce_gbs_total": round(8 * n / t_red / 1e9, 1),
+            "reduce_pct_peak_per_rank": pct(8 * n / t_red / 1e9 / comm.size),
+            "scan_ms": round(1e3 * t_scan, 4), "scan_bytes_per_elem": scan_b,
+            "scan_gbs_total": round(scan_b * n / t_scan / 1e9, 1),
+            "scan_pct_peak_per_rank": pct(scan_b * n / t_scan / 1e9 / comm.size),
+            "reduce_elements_per_s": round(n / t_red, 1), "scan_elements_per_s": round(n / t_scan, 1),
+            "scan_last_equals_reduce": ok}
+
+
 STENCIL_SEED = 0xC0FFEE
 
 
@@ -563,8 +613,13 @@ def stencil_row(S, comm, tgt, nx, nt):
     ok = bool(max_over_ranks(comm, 0.0 if ok else 1.0) == 0.0)
     for v in hs.U + [hs.H]:
         v.free()
+    # executed HBM traffic: one 16-B/point read + write per fused pass of
+    # halo_width steps (the unfused per-step model, 16 B per point-step, is
+    # not a roofline: the fused passes never move those bytes)
+    passes = -(-nt // max(1, hs.W))
     return {"points": nx, "ranks": comm.size, "steps": nt, "ms": round(1e3 * el, 3),
-            "gpoint_steps_per_s": round(nx * nt / el / 1e9, 2), "gbs_model_16B": round(16 * nx * nt / el / 1e9, 1),
+            "gpoint_steps_per_s": round(nx * nt / el / 1e9, 2),
+            "gbs_executed_16B_per_pass": round(16 * nx * passes / el / 1e9, 1),
             "init": "splitmix64(seed ^ i) in [0, 1)", "window_check_bit_exact": ok, "steps_checked": 2 * nt,
             "points_checked_rank0": checked, "halo_width": hs.W}
 
@@ -574,8 +629,12 @@ def dist_extras(S, F, comm, tgt, pol, x, n_local, world, args):
     wall time between barriers):
       * segmented reduce of the step's int64 partitioned_vector (GB/s per
         rank and in total);
+      * strong scaling of segmented reduce and inclusive_scan over 2^32 int64
+        in total (strong_row);
       * segmented sort of 2^logn uint64 keys per GPU (weak scaling): local
-        radix sort, exact global cut, one RCCL all-to-all, pairwise merges;
+        radix sort, exact global cut, one RCCL all-to-all, then the received
+        runs merged (hpxhip_merge_runs in one pass for 4 <= p <= 8, pairwise
+        merge-path rounds otherwise);
         checked on the device: every partition sorted (is_sorted) and the
         partitions ordered across ranks (first/last keys all-gathered);
       * 1d_stencil heat, 2^32 points over the ranks, 100 steps (strong
@@ -589,6 +648,7 @@ def dist_extras(S, F, comm, tgt, pol, x, n_local, world, args):
 
     n = n_local * world
     x.local.free()
+    res["strong_2p32_int64"] = strong_row(S, F, comm, tgt, pol, args.strong_logn)
     keys = S.partitioned_vector(n, np.uint64, comm=comm, tgt=tgt)
     best = None
     for rep in range(3):
@@ -609,8 +669,7 @@ def dist_extras(S, F, comm, tgt, pol, x, n_local, world, args):
     ok = ok and all(g[r, 1] <= g[r + 1, 0] for r in range(world - 1))
     ok = bool(tmax(0.0 if ok else 1.0) == 0.0)
     res["segmented_sort_uint64"] = {"keys_per_gpu": n_local, "keys_total": n, "ms": round(1e3 * best, 3),
-                                    "gkeys_per_s": round(n / best / 1e9, 3), "gbs_model_136B_per_rank":
-                                    round(136 * n_local / best / 1e9, 1), "sorted_and_ordered": ok}
+                                    "gkeys_per_s": round(n / best / 1e9, 3), "sorted_and_ordered": ok}
     loc.free()
     res["stencil_heat_dist"] = stencil_row(S, comm, tgt, 1 << args.stencil_logn, args.stencil_steps)
     return res
@@ -679,8 +738,20 @@ def cpu_baseline(logn):
     leaves) and the 1d_stencil heat solver (1d_stencil_4_parallel.cpp:87-156
     restated) on 2^(logn-3) points x 20 steps."""
     from oracle import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    # cores this process may run on (affinity, not the machine's count), the
+    # threads used (OMP_NUM_THREADS caps them: 16 on the GPU box), the model
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
+    threads = max(1, min(threads, affinity))
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
     n = 1 << logn
     t_triad = O.par_triad(n, threads, reps=3)
     x = O.generate(np.int64, "range", n, 0x5EED, -(1 << 20), 1 << 20)
@@ -704,6 +775,7 @@ def cpu_baseline(logn):
         stream[name] = {"best_gbs": round(nbytes * n / best / 1e9, 2), "min_ms": round(1e3 * best, 3),
                         "avg_ms": round(1e3 * avg, 3)}
     return {"value": round(gbs, 2), "unit": "GB/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "affinity_cpus": affinity, "machine_cpus": os.cpu_count(),
             "sample": f"2^{logn} elements: triad f64 + reduce int64 + inclusive_scan int64, best of 3, "
                       f"HPX par chunking (4*cores chunks) on {threads} std::threads",
             "triad_gbs": round(24 * n / t_triad / 1e9, 2), "reduce_gbs": round(8 * n / t_red / 1e9, 2),
@@ -711,8 +783,7 @@ def cpu_baseline(logn):
             "extras": {"copy_if_int64": {"elements": n, "ms": round(1e3 * t_cif, 2),
                                          "gbs_model_12B": round(12 * n / t_cif / 1e9, 2)},
                        "sort_uint64": {"keys": ns, "ms": round(1e3 * t_sort, 2),
-                                       "gkeys_per_s": round(ns / t_sort / 1e9, 4),
-                                       "gbs_model_136B": round(136 * ns / t_sort / 1e9, 2)},
+                                       "gkeys_per_s": round(ns / t_sort / 1e9, 4)},
                        "stencil_heat": {"points": nx, "steps": nt, "ms": round(1e3 * t_st, 2),
                                         "gpoint_steps_per_s": round(nx * nt / t_st / 1e9, 3),
                                         "gbs_model_16B": round(16 * nx * nt / t_st / 1e9, 2)},

@@ -289,38 +289,40 @@ __global__ __launch_bounds__(kMwThreads, HPXHIP_MW_MINW) void k_mw_merge(const U
                                                                           uint32_t* __restrict__ err) {
     __shared__ alignas(16) U s[mw_pad(kMwCap) + 1];  // (+1: a finished run's head reads one past)
     __shared__ int sbnd[kMwMaxRuns + 1];
+    // run j: keys == v_k at [eq_j, lo_j), keys strictly between at [lo_j, hi_j)
+    // (round 6: the per-run bounds live in LDS, one thread per run loads
+    // them -- held in scalar registers they had pushed the kernel to 20-24
+    // SGPR spills, the regime in which an earlier form was miscompiled, see
+    // DESIGN.md (e); the build refuses SGPR spills here, Makefile)
+    __shared__ uint64_t s_eq[kMwMaxRuns], s_lo[kMwMaxRuns], s_hi[kMwMaxRuns], s_go[kMwMaxRuns];
     const uint64_t k = blockIdx.x;
     const uint32_t p = r.p;
-    // run j: keys == v_k at [eq_j, lo_j), keys strictly between at [lo_j, hi_j)
-    uint64_t eq[kMwMaxRuns], lo[kMwMaxRuns], hi[kMwMaxRuns];
-    uint64_t pos = 0;  // sum_j lower_bound_j(v_k): where the task's output starts
-    bool dup = false;
-#pragma unroll
-    for (uint32_t j = 0; j < kMwMaxRuns; ++j)
-        if (j < p) {
-            eq[j] = LB[k * p + j];
-            lo[j] = UB[k * p + j];
-            hi[j] = LB[(k + 1) * p + j];
-            dup = dup || hi[j] < lo[j];
-            pos += eq[j];
-        }
+    if (threadIdx.x < p) {
+        const uint32_t j = threadIdx.x;
+        const uint64_t e = LB[k * p + j], l = UB[k * p + j], h = LB[(k + 1) * p + j];
+        s_eq[j] = e;
+        s_lo[j] = l;
+        s_hi[j] = h;
+        s_go[j] = r.off[j];
+    }
+    __syncthreads();
     // v_{k+1} == v_k (a repeated splitter: some run holds keys equal to v_k
     // before lower_bound(v_{k+1})): the last task with this splitter copies
     // its equal keys, this one has nothing to do
+    bool dup = false;
+    for (uint32_t j = 0; j < p; ++j) dup = dup || s_hi[j] < s_lo[j];
     if (dup) return;
+    uint64_t pos = 0;  // sum_j lower_bound_j(v_k): where the task's output starts
+    for (uint32_t j = 0; j < p; ++j) pos += s_eq[j];
     // the keys equal to v_k, run after run
-#pragma unroll
-    for (uint32_t j = 0; j < kMwMaxRuns; ++j)
-        if (j < p) {
-            const uint64_t ne = lo[j] - eq[j];
-            const U* src = in + r.off[j] + eq[j];
-            for (uint64_t e = threadIdx.x; e < ne; e += kMwThreads) out[pos + e] = src[e];
-            pos += ne;
-        }
+    for (uint32_t j = 0; j < p; ++j) {
+        const uint64_t ne = s_lo[j] - s_eq[j];
+        const U* src = in + s_go[j] + s_eq[j];
+        for (uint64_t e = threadIdx.x; e < ne; e += kMwThreads) out[pos + e] = src[e];
+        pos += ne;
+    }
     uint64_t total = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kMwMaxRuns; ++j)
-        if (j < p) total += hi[j] - lo[j];
+    for (uint32_t j = 0; j < p; ++j) total += s_hi[j] - s_lo[j];
     if (total > static_cast<uint64_t>(kMwCap)) {  // cannot happen with consistent keys (see above)
         if (threadIdx.x == 0) raise_device_error(err, HPXHIP_DEVERR_RANGE);
         return;
@@ -330,30 +332,36 @@ __global__ __launch_bounds__(kMwThreads, HPXHIP_MW_MINW) void k_mw_merge(const U
     // store -- measured slower, r05 lease ai: p = 2 4.34 vs 3.65 ms, p = 8
     // 7.74 vs 7.75)
     int c = 0;
+    for (uint32_t j = 0; j < p; ++j) {
+        const int nj = static_cast<int>(s_hi[j] - s_lo[j]);
+        if constexpr (VEC) {  // 16-B loads of the aligned vectors covering the part
+            constexpr int V = 16 / sizeof(U);
+            using VT = vec<U, V>;
+            const uint64_t g0 = s_go[j] + s_lo[j], g1 = s_go[j] + s_hi[j];
+            const VT* vs = reinterpret_cast<const VT*>(in);
+            // whole vectors below g1 only (round 6, ADVICE r05: the vector
+            // holding g1 - 1 also holds keys past the last run, which may
+            // be past the buffer -- scripts/diag/mw_host caught the read
+            // under ASan); the ragged tail by scalar loads
+            const uint64_t vend = g1 / V;
+            for (uint64_t v = g0 / V + threadIdx.x; v < vend; v += kMwThreads) {
+                const VT x = ld_stream(&vs[v]);
 #pragma unroll
-    for (uint32_t j = 0; j < kMwMaxRuns; ++j)
-        if (j < p) {
-            const int nj = static_cast<int>(hi[j] - lo[j]);
-            if constexpr (VEC) {  // 16-B loads of the aligned vectors covering the part
-                constexpr int V = 16 / sizeof(U);
-                using VT = vec<U, V>;
-                const uint64_t g0 = r.off[j] + lo[j], g1 = r.off[j] + hi[j];
-                const VT* vs = reinterpret_cast<const VT*>(in);
-                for (uint64_t v = g0 / V + threadIdx.x; v < (g1 + V - 1) / V; v += kMwThreads) {
-                    const VT x = ld_stream(&vs[v]);
-#pragma unroll
-                    for (int e = 0; e < V; ++e) {
-                        const uint64_t i = v * V + e;
-                        if (i >= g0 && i < g1) s[mw_pad(c + static_cast<int>(i - g0))] = xf(x.v[e]);
-                    }
+                for (int e = 0; e < V; ++e) {
+                    const uint64_t i = v * V + e;
+                    if (i >= g0) s[mw_pad(c + static_cast<int>(i - g0))] = xf(x.v[e]);
                 }
-            } else {
-                const U* src = in + r.off[j] + lo[j];
-                for (int e = threadIdx.x; e < nj; e += kMwThreads) s[mw_pad(c + e)] = xf(ld_stream(&src[e]));
             }
-            if (threadIdx.x == 0) sbnd[j] = c;
-            c += nj;
+            const uint64_t t0 = vend * V > g0 ? vend * V : g0;
+            for (uint64_t i = t0 + threadIdx.x; i < g1; i += kMwThreads)
+                s[mw_pad(c + static_cast<int>(i - g0))] = xf(in[i]);
+        } else {
+            const U* src = in + s_go[j] + s_lo[j];
+            for (int e = threadIdx.x; e < nj; e += kMwThreads) s[mw_pad(c + e)] = xf(ld_stream(&src[e]));
         }
+        if (threadIdx.x == 0) sbnd[j] = c;
+        c += nj;
+    }
     if (threadIdx.x == 0) sbnd[p] = c;
     __syncthreads();
     const int n = c;

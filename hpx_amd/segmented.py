@@ -277,12 +277,17 @@ class TorchComm:
             self.mem.retire()  # the old tensors may still be read by stream-ordered work
             self._send = self.torch.zeros(words, dtype=self.torch.int64, device=self.device)
             self._recv = self.torch.zeros(words * self.size, dtype=self.torch.int64, device=self.device)
+        if self.size == 1:  # a one-rank all-gather is the identity: recv is send
+            return self.mem.handle(self._send), self.mem.handle(self._send)
         return self.mem.handle(self._send), self.mem.handle(self._recv)
 
     def allgather(self, nbytes: int, stream):
         """Packed all-gather: recv bytes [r*nbytes, (r+1)*nbytes) <- rank r's
         send[0:nbytes] (nbytes a multiple of 8, sized by slots()), so the
-        segment values sit contiguously for hpxhip_fold."""
+        segment values sit contiguously for hpxhip_fold.  One rank: nothing
+        to move (slots() handed out one buffer for both)."""
+        if self.size == 1:
+            return None
         words = max(1, nbytes // 8)
         with self.mem.ctx(stream):
             self.dist.all_gather_into_tensor(self._recv[:self.size * words], self._send[:words])
@@ -346,11 +351,12 @@ class HipEngine:
     def stream(self):
         return self.tgt.stream
 
-    def reduce_into(self, vec, lo, hi, op, conv, acc_dt, out_ptr):
-        """out_ptr <- identity (op) conv(x[lo]) ... (op) conv(x[hi-1])."""
-        ident = _identity(op.kind, acc_dt)
+    def reduce_into(self, vec, lo, hi, op, conv, acc_dt, out_ptr, init=None):
+        """out_ptr <- init (op) conv(x[lo]) ... (op) conv(x[hi-1]); init
+        defaults to op's identity (a segment total, detail/reduce.hpp:43-62)."""
+        seed = _identity(op.kind, acc_dt) if init is None else init
         L.call("hpxhip_transform_reduce", vec.dtype, acc_dt, op.kind, conv.kind, L.scalars_buf(acc_dt, conv.scalars),
-               L.scalar_buf(acc_dt, ident), ctypes.c_void_p(vec.data() + lo * vec.value_size), hi - lo,
+               L.scalar_buf(acc_dt, seed), ctypes.c_void_p(vec.data() + lo * vec.value_size), hi - lo,
                ctypes.c_void_p(out_ptr), self.stream, None, 0)
 
     def fold(self, dt, op, init, values_ptr, count, out_ptr):
@@ -799,9 +805,22 @@ class segmented:
         eng, comm = self.engine(pv), pv.comm
         from .algorithms import _acc_dtype, _slots_for
         adt = _acc_dtype(pv.dtype, init)
-        recv, cmax = self._segment_totals(pv, a, b, red_op, conv_op, adt, eng, comm)  # S_k, one all-gather
         dev, _ = _slots_for(pv.tgt).next() if isinstance(eng, HipEngine) else (eng.scratch(), None)
-        eng.fold(adt, red_op, init, recv, comm.size * cmax, dev)         # init (op) S_0 (op) ... in order
+        if (isinstance(eng, HipEngine) and comm.size == 1 and pv.layout.max_segments() == 1
+                and np_dtype(adt).kind in "iu"):
+            # one segment in the whole container, integer accumulation:
+            # init (op) S_0 == the segment reduced from init (exact for every
+            # integer op), so one reduce launch replaces the total, the
+            # identity all-gather and the fold (round 6: per-call overhead
+            # of the 8-GPU strong-scaling row)
+            lo, hi = pv.local_range(a, b)
+            if hi > lo:
+                eng.reduce_into(pv.local, lo, hi, red_op, conv_op, adt, dev, init=init)
+            else:
+                eng.put(dev, adt, init)
+        else:
+            recv, cmax = self._segment_totals(pv, a, b, red_op, conv_op, adt, eng, comm)  # S_k, one all-gather
+            eng.fold(adt, red_op, init, recv, comm.size * cmax, dev)         # init (op) S_0 (op) ... in order
         if getattr(pol, "is_task", False):
             # par(task): future<T> resolved by the stream, no host round trip
             # inside the pipeline (segmented_algorithms/reduce.hpp:112-209

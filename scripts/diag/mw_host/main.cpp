@@ -1,0 +1,115 @@
+// main.cpp -- drives the extracted multiway-merge kernels (see shim.hpp) on
+// the host: sorted runs of float64 / uint64 keys laid back to back after
+// `lead` keys, samples, sample order, splitter bounds, then every task of
+// k_mw_merge as one 256-thread block; checks the output bit for bit against
+// std::sort of the union.  Exit code 1 on a mismatch.
+#include "shim.hpp"
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+
+#include "extracted.inc"
+
+template <typename T>
+static std::vector<T> gen(size_t n, uint64_t seed) {
+    std::mt19937_64 g(seed);
+    std::vector<T> x(n);
+    if constexpr (std::is_floating_point_v<T>) {
+        std::normal_distribution<T> d;
+        for (auto& v : x) v = d(g);
+        for (size_t i = 0; n > 40 && i < n; i += 13) x[i] = T(0);
+        for (size_t i = 0; n > 40 && i < n; i += 11) x[i] = -T(0);
+    } else {
+        for (auto& v : x) v = static_cast<T>(g() % (seed % 3 == 0 ? 1000 : ~0ull));
+    }
+    return x;
+}
+
+template <typename T, bool VEC>
+static int run_case(uint32_t p, std::vector<uint64_t> lens, uint64_t seed, size_t lead) {
+    using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
+    using X = ordered_bits<T, false>;
+    X xf;
+    auto less = [&](U a, U b) { return xf(a) < xf(b); };
+    std::vector<U> all;
+    uint64_t n = 0;
+    for (auto l : lens) n += l;
+    // exactly sized (ASan sees a read past the last run), 16-B aligned base
+    void* raw = nullptr;
+    if (posix_memalign(&raw, 16, (lead + n) * sizeof(U) + (lead + n == 0))) return 1;
+    U* buf = static_cast<U*>(raw);
+    size_t at = lead;
+    for (size_t i = 0; i < lead; ++i) buf[i] = 0;
+    mw_runs r{};
+    r.p = p;
+    r.stride = mw_stride(p);
+    r.q = kMwQ * p;
+    for (uint32_t j = 0; j < p; ++j) {
+        auto v = gen<T>(lens[j], seed * 977 + j);
+        std::vector<U> u(v.size());
+        if (!v.empty()) std::memcpy(u.data(), v.data(), v.size() * sizeof(U));
+        std::sort(u.begin(), u.end(), less);
+        std::copy(u.begin(), u.end(), buf + at);
+        all.insert(all.end(), u.begin(), u.end());
+        r.off[j + 1] = r.off[j] + lens[j];
+        r.soff[j + 1] = r.soff[j] + (lens[j] + r.stride - 1) / r.stride;
+        at += lens[j];
+    }
+    const U* ui = buf + lead;
+    const uint64_t M = r.soff[p];
+    std::vector<U> samp(M ? M : 1);
+    for (uint64_t i = 0; i < M; ++i) {
+        blockIdx.x = static_cast<unsigned>(i / 256);
+        threadIdx.x = static_cast<unsigned>(i % 256);
+        k_mw_samples<U>(ui, r, samp.data());
+    }
+    std::vector<U> sorted(samp.begin(), samp.begin() + M);
+    std::stable_sort(sorted.begin(), sorted.end(), less);
+    uint64_t K = (M + r.q - 1) / r.q;
+    if (K == 0) K = 1;
+    std::vector<uint64_t> LB((K + 1) * p), UB((K + 1) * p);
+    for (uint64_t i = 0; i < (K + 1) * p; ++i) {
+        blockIdx.x = static_cast<unsigned>(i / 256);
+        threadIdx.x = static_cast<unsigned>(i % 256);
+        k_mw_bounds<U, X>(ui, r, samp.data(), sorted.data(), K, xf, LB.data(), UB.data());
+    }
+    if (posix_memalign(&raw, 16, n * sizeof(U) + (n == 0))) return 1;
+    U* out = static_cast<U*>(raw);
+    uint32_t err = 0;
+    for (uint64_t k = 0; k < K; ++k)
+        run_block(static_cast<unsigned>(k), kMwThreads, [&] { k_mw_merge<U, X, VEC>(ui, r, LB.data(), UB.data(), xf, out, &err); });
+    std::sort(all.begin(), all.end(), less);
+    uint64_t bad = 0, first = n;
+    for (uint64_t i = 0; i < n; ++i)
+        if (out[i] != all[i]) {
+            if (first == n) first = i;
+            ++bad;
+        }
+    std::printf("%s p=%u n=%llu lead=%zu vec=%d K=%llu err=%u mismatches=%llu", sizeof(T) == 8 && std::is_floating_point_v<T> ? "float64" : "uint64",
+                p, (unsigned long long)n, lead, int(VEC), (unsigned long long)K, err, (unsigned long long)bad);
+    if (bad) std::printf(" first=%llu", (unsigned long long)first);
+    std::printf("\n");
+    std::free(buf);
+    std::free(out);
+    return bad || err ? 1 : 0;
+}
+
+int main(int argc, char** argv) {
+    int rc = 0;
+    // the failing shape of lease r5/ad (p = 2, lens 251272 / 78483), then
+    // p = 3..8 with ragged, empty and repeating runs
+    rc |= run_case<double, false>(2, {251272, 78483}, 2, 3);
+    rc |= run_case<double, true>(2, {251272, 78483}, 2, 0);
+    rc |= run_case<uint64_t, false>(2, {251272, 78483}, 2, 3);
+    const bool quick = argc > 1;
+    for (uint32_t p = 3; p <= 8 && !quick; ++p) {
+        std::mt19937_64 g(p);
+        std::vector<uint64_t> lens(p);
+        for (auto& l : lens) l = g() % 60000;
+        if (p % 2) lens[1] = 0;
+        rc |= run_case<double, true>(p, lens, p, 0);
+        rc |= run_case<uint64_t, true>(p, lens, 3 * p, 0);  // seed % 3 == 0: keys below 1000, long repeats
+        rc |= run_case<uint64_t, false>(p, lens, 3 * p + 1, 5);
+    }
+    return rc;
+}

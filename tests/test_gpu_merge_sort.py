@@ -133,6 +133,55 @@ def test_merge_runs_bit_exact(gpu_target, p, dt):
                                           err_msg=f"{shape} desc={desc}")
 
 
+def merge_runs_with(lib_path, gpu_target, runs, dt, desc, lead=3):
+    """hpxhip_merge_runs of another build of the library (a variant under
+    hpx_amd/variants/, loaded RTLD_LOCAL beside the shipped one), on buffers
+    and the stream of the shipped library."""
+    import ctypes
+    import os
+    lib = ctypes.CDLL(lib_path, mode=os.RTLD_LOCAL)
+    fn = lib.hpxhip_merge_runs
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_void_p,
+                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    src = np.concatenate([np.zeros(lead, dt)] + [np.asarray(r, dt) for r in runs])
+    offsets = [lead] + list(lead + np.cumsum([len(r) for r in runs]))
+    d = hpx.vector.from_host(src if src.size else np.zeros(1, dt), gpu_target)
+    out = hpx.vector(max(1, offsets[-1] - lead + 1), dtype=dt, tgt=gpu_target)
+    offs = (ctypes.c_uint64 * len(offsets))(*[int(o) for o in offsets])
+    it = np.dtype(dt).itemsize
+    rc = fn(dtype_code(dt), d.data(), offs, len(offsets) - 1, out.data() + it, 1 if desc else 0,
+            gpu_target.stream, None, 0)
+    assert rc == 0, f"{lib_path}: hpxhip_merge_runs returned {rc}"
+    gpu_target.synchronize()
+    return out.to_host()[1:1 + offsets[-1] - lead]
+
+
+VARIANTS = ["mw512", "mwminw4"]
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("dt", [np.uint64, np.int32, np.float64])
+def test_merge_runs_variant_builds(gpu_target, variant, dt):
+    """the multiway merge built with 512-thread tasks and at the
+    default occupancy bound (Makefile mw-variants) stays bit-exact beside
+    the shipped 256-thread, 8-waves-per-SIMD build -- float64 included, the
+    dtype an earlier form was miscompiled for.  The shapes of
+    test_merge_runs_bit_exact, the failing one of lease r5/ad first."""
+    import os
+    path = os.path.join(os.path.dirname(hpx.__file__), "variants", variant, "libhpxhip.so")
+    assert os.path.exists(path), f"{path} missing: build() builds it (make mw-variants)"
+    for p in (2, 3, 8):
+        rng = np.random.default_rng(p)
+        lens = rng.integers(0, 300000, p)
+        runs = [O.sort(np.asarray(rnd(dt, int(n), 10 + j), dt)) for j, n in enumerate(lens)]
+        for desc in (False, True):
+            rs = [O.sort(r, desc) for r in runs]
+            got = merge_runs_with(path, gpu_target, rs, dt, desc)
+            np.testing.assert_array_equal(bits(got), bits(O.sort(np.concatenate(rs), desc)),
+                                          err_msg=f"{variant} p={p} desc={desc}")
+
+
 @pytest.mark.parametrize("case", ["all_equal", "two_values", "one_long_run", "tiny"])
 def test_merge_runs_edge_cases(gpu_target, case):
     """All keys equal (one task copies them), two values, one run holding
