@@ -89,6 +89,7 @@ static int run_case(uint32_t p, std::vector<uint64_t> lens, uint64_t seed, size_
                 p, (unsigned long long)n, lead, int(VEC), (unsigned long long)K, err, (unsigned long long)bad);
     if (bad) std::printf(" first=%llu", (unsigned long long)first);
     std::printf("\n");
+    std::fflush(stdout);
     std::free(buf);
     std::free(out);
     return bad || err ? 1 : 0;
@@ -98,10 +99,13 @@ int main(int argc, char** argv) {
     int rc = 0;
     // the failing shape of lease r5/ad (p = 2, lens 251272 / 78483), then
     // p = 3..8 with ragged, empty and repeating runs
-    rc |= run_case<double, false>(2, {251272, 78483}, 2, 3);
-    rc |= run_case<double, true>(2, {251272, 78483}, 2, 0);
-    rc |= run_case<uint64_t, false>(2, {251272, 78483}, 2, 3);
+    // (quick: the r5/ad calls only -- out offset by one element, so the
+    // scalar-staging instantiation, VEC = false)
     const bool quick = argc > 1;
+    rc |= run_case<double, false>(2, {251272, 78483}, 2, 3);
+    rc |= run_case<uint64_t, false>(2, {251272, 78483}, 2, 3);
+    rc |= run_case<double, false>(2, {251272, 78483}, 2, 0);
+    if (!quick) rc |= run_case<double, true>(2, {251272, 78483}, 2, 0);
     for (uint32_t p = 3; p <= 8 && !quick; ++p) {
         std::mt19937_64 g(p);
         std::vector<uint64_t> lens(p);
