@@ -6,7 +6,8 @@ lease_a() {
   # round 6, lease a: the r05 multiway-merge miscompile reproduced with today's toolchain
   # (scripts/diag/mw_repro.py over the commit-8a18d38 builds, the shipped build and its variants),
   # the merge tests (variant builds included), the bench with the new strong-scaling rows, and a
-  # baseline 2^30 u64 / u32 sort per kernel (rocprofv3 --kernel-trace --stats)
+  # baseline 2^30 u64 / u32 sort per kernel (rocprofv3 --kernel-trace --stats), and the prefix passes
+  # with 4096- / 6144- / 8192-key tiles (scripts/ubench/sortpass7.hip)
   cd $GRAFT_REPO_ROOT
   export TMPDIR=/tmp
   L=gpurun_out/r6a
@@ -16,6 +17,7 @@ lease_a() {
   timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_merge_sort.py \
     > ${L}_merge_tests.log 2>&1 || exit $?
   timeout -k 10 900 python -u bench.py > ${L}_bench.log 2>&1 || exit $?
+  timeout -k 10 300 ./scripts/ubench/sortpass7 > ${L}_sortpass7.log 2>&1 || exit $?
   for c in u64 u32; do
     SORT_ONLY=$c timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6a_prof_$c -o run -- \
       python3 -u scripts/sort_probe.py 30 > ${L}_sort_$c.log 2>&1 || exit $?
