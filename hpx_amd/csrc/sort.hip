@@ -722,7 +722,8 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                                        reinterpret_cast<const unsigned long long*>(base + L.bs2),
                                        reinterpret_cast<G*>(base + L.lb), counter, err, X{}, ctl + C_B9, nt,
                                        static_cast<const uint32_t*>(nullptr),
-                                       reinterpret_cast<const seg_table*>(base + L.segs2));
+                                       reinterpret_cast<const seg_table*>(base + L.segs2),
+                                       static_cast<const unsigned long long*>(xstart));
                 };
                 if (L.wide) launch((unsigned long long)0);
                 else launch(uint32_t(0));

@@ -593,6 +593,16 @@ __global__ __launch_bounds__(256) void k_seg_copy(const E* __restrict__ src, E* 
 // and LSD passes); a persistent grid leaves after one read per workgroup.
 // SEG (r05, with PERSIST): the tiles of a seg_table; bin_start holds
 // [segment][pass][256] bin starts, and each segment is sorted on its own.
+// REGION_ATOM (r06; the 18-bit form's second prefix pass, XREG + SEG over
+// the 8 field regions, keys only): a wave whose tile lies inside ONE field
+// bin -- no bin of its region starts strictly inside the tile, checked
+// against prev_starts, the field's bin starts -- ranks by LDS atomics like
+// the offset-fed first pass.  Stability is only owed to the field order of
+// the input, and every key of such a tile has the same field; tiles that
+// straddle a field bin boundary keep the stable wave match.
+#ifndef HPXHIP_REGION_ATOM
+#define HPXHIP_REGION_ATOM 1
+#endif
 template <typename U, typename VAL, bool HAS_VAL, typename G, typename X, int THREADS = 512, int ITEMS = 16,
           int LBB = 8, int RB = 8, bool STAGE = true, bool DYN_ID = HPXHIP_TILE_DYN_ID, bool PERSIST = false,
           bool SEG = false, bool XREG = false>
@@ -604,7 +614,8 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
                                                        uint32_t* __restrict__ err, X xf,
                                                        const int32_t* __restrict__ ctl = nullptr, uint64_t ntiles = 0,
                                                        const uint32_t* __restrict__ pre = nullptr,
-                                                       const seg_table* __restrict__ segs = nullptr) {
+                                                       const seg_table* __restrict__ segs = nullptr,
+                                                       const unsigned long long* __restrict__ prev_starts = nullptr) {
     static_assert(!PERSIST || STAGE, "the persistent form keeps the LDS-staged write-out");
     static_assert(!SEG || ((PERSIST || XREG) && LBB > 0), "segmented passes: look-back passes, persistent or XREG");
     static_assert(!XREG || !PERSIST, "XCD regions: one tile per block");
@@ -761,6 +772,18 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
     }
 #endif
 
+    // REGION_ATOM: does the tile lie inside one bin of the previous pass's
+    // field?  Lane l of every wave checks bin 64 x + l of the tile's region x
+    // (its 64 field digits), one L2-resident load issued behind the tile's
+    // key loads; the ballot is wave-uniform
+    bool atom_rank = false;
+    if constexpr (HPXHIP_REGION_ATOM && XREG && SEG && RB == 9 && !HAS_VAL && LBB > 0) {
+        if (prev_starts) {
+            const uint64_t bs = prev_starts[64u * s_seg + static_cast<uint32_t>(lane)];
+            const uint64_t tile_hi = full ? tile_base + TILE : end;
+            atom_rank = __ballot(bs > tile_base && bs < tile_hi) == 0;
+        }
+    }
     // ---- wave-level match ranking (stable: round-major, then lane order)
     uint32_t rank[ITEMS];
 #pragma unroll
@@ -768,6 +791,14 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
         const uint64_t i = wbase + r * kWave + lane;
         const bool valid = full || i < end;
         const uint32_t d = static_cast<uint32_t>(xf(k[r]) >> shift) & DMASK;
+        if (RB == 9 && atom_rank) {  // (REGION_ATOM, see above)
+            if (valid) {
+                const uint32_t sh = 16u * (d & 1u);
+                const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(&s_whist[wave][0]) + (d >> 1), 1u << sh);
+                rank[r] = (old >> sh) & 0xffffu;
+            }
+            continue;
+        }
         if constexpr (HPXHIP_OS_ATOM1 && LBB < 0 && !HAS_VAL) {
             // the offset-fed first prefix pass of a keys-only sort (its order
             // inside a digit is never relied on: the second pass is stable

@@ -24,4 +24,24 @@ lease_a() {
   done
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a"; fi
+lease_b() {
+  # round 6, lease b: second prefix pass ranked by LDS atomics on tiles inside one field bin
+  # (HPXHIP_REGION_ATOM): sort tests, then A/B against the ballot-ranked build (seglib noratom)
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6b
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sort_hybrid.py \
+    tests/test_gpu_parity.py -k "sort" > ${L}_tests.log 2>&1 || exit $?
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_fullsize.py -k sort \
+    > ${L}_fullsize.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for lib in hpx_amd/libhpxhip.so scripts/ubench/seglib/noratom/libhpxhip.so; do
+      for c in u64 u32; do
+        echo "== $lib $c rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 30 >> ${L}_ab.log 2>&1 || exit $?
+      done
+    done
+  done
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b"; fi
