@@ -175,6 +175,12 @@ constexpr uint64_t kCapKV = static_cast<uint64_t>(kSegThreads16) * kSegItemsKV;
 // the 8192-key 512 x 18 shape, profiles/r04_ubench_segment_occupancy.log).
 constexpr int kSegItems18 = 9;
 constexpr uint64_t kCap18 = static_cast<uint64_t>(kSegThreads17) * kSegItems18;
+// r06: the one-pass segment sort (k_bucket_sort ONEB) bound to three
+// workgroups per CU (6 waves per SIMD: <= 80 VGPRs); unbounded it took 119
+#ifndef HPXHIP_SEG_MINW18
+#define HPXHIP_SEG_MINW18 6
+#endif
+constexpr int kSegMinW18 = HPXHIP_SEG_MINW18;
 // the 9-bit field under the top byte: bits [47, 56) of a 64-bit key, [15, 24) of a 32-bit one
 template <typename U>
 constexpr int field17_shift() { return static_cast<int>(8 * sizeof(U)) - 17; }
@@ -228,7 +234,8 @@ enum : int {
     C_SEGC = 38,       // {on, nb, top_single}: 512 x 9 segment sort (18-bit form)
     C_SEGLSD = 44,     // hybrid-sized sorts: the LSD passes run over the segment table
     C_SEGHIST = 45,    // ... whose histograms are counted first (the oversized-bucket finish)
-    C_WORDS = 46
+    C_REDO = 46,       // buckets the one-pass segment sort handed to the two-pass form (ids in the lb scratch)
+    C_WORDS = 47
 };
 static_assert(C_WORDS * 4 <= 256, "plan words fit their slot");
 
@@ -767,14 +774,27 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             // fell back to the 16-bit form) strides over all of them
             const uint64_t want18 = 2 * (n / 4096 + 1);
             const uint32_t g18 = static_cast<uint32_t>(want18 > kMaxBuckets ? kMaxBuckets : want18);
-            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true>),
+            // r06: the one-pass form (HPXHIP_SEG_ONE bits, k_bucket_sort ONEB);
+            // buckets with a bin too large for it are listed (ctl[C_REDO], ids
+            // in the look-back scratch, free after the prefix passes) and
+            // sorted by the two-pass form in a third, striding launch
+            auto* redo_n = reinterpret_cast<uint32_t*>(ctl + C_REDO);
+            auto* redo_ids = reinterpret_cast<uint32_t*>(base + L.lb);  // lb_bytes >= 576 x 2 KiB > 4 x 2^18
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true, false,
+                                              kSegMinW18, false, HPXHIP_SEG_ONE>),
                                dim3(g18), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
-                               ctl + C_SEGC, 0u, big);
+                               ctl + C_SEGC, 0u, big, redo_n, HPXHIP_SEG_ONE > 0 ? redo_ids : nullptr);
             HPXHIP_CHECK_LAUNCH();
             if (g18 < kMaxBuckets)
+                hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true, true,
+                                                  kSegMinW18, false, HPXHIP_SEG_ONE>),
+                                   dim3(3 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
+                                   oversized, ctl + C_SEGC, g18, big, redo_n, HPXHIP_SEG_ONE > 0 ? redo_ids : nullptr);
+            HPXHIP_CHECK_LAUNCH();
+            if (HPXHIP_SEG_ONE > 0)
                 hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true, true>),
                                    dim3(3 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
-                                   oversized, ctl + C_SEGC, g18, big);
+                                   oversized, ctl + C_SEGC, 0u, big, redo_n, redo_ids);
             HPXHIP_CHECK_LAUNCH();
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true, true>),
                                dim3(2 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,

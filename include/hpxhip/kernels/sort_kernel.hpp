@@ -1044,14 +1044,35 @@ __global__ __launch_bounds__(256) void k_bucket_bounds(const U* __restrict__ key
 // PERSIST (device-planned sort, BOUNDS only): a fixed grid strides over the
 // planned buckets (bucket b by workgroup b mod gridDim), so a launch the plan
 // skips costs one gate read per workgroup instead of one dispatch per bucket.
+// ONEB (r06, keys only): the one-pass form.  One ranking pass by LDS atomics
+// on 2^ONEB block-wide bins (packed 16-bit counters) of the ONEB bits under
+// `top`, one scan of the bins, one scatter; then every key of a bin holding
+// more than one key finds its place inside the bin by counting the bin's
+// keys below it (ties broken by the scatter position), all keys in parallel,
+// and moves there.  For 2^30 random u64 keys (~4096-key buckets, ONEB = 13)
+// a key's bin holds 1.5 keys on average.  Replaces the two ranked 8-bit
+// passes, whose second (stable, wave-match) pass left the kernel
+// compute-bound: with one LDS pass the segment sort had run as fast as a bare
+// load + store through LDS (profiles/r05_ubench_seg5_phases.log, ABL2 vs
+// ABL4).  The r05 one-pass attempt (seg10) ordered the bins by serial
+// insertion, one thread per bin, and lost.  A segment with a bin over
+// kOneBinMax keys (low-entropy keys) takes the two-pass path below from the
+// same registers.
+constexpr uint32_t kOneBinMax = 24;
+#ifndef HPXHIP_SEG_ONE
+#define HPXHIP_SEG_ONE 13
+#endif
 template <typename U, typename X, int THREADS = 1024, int ITEMS = 18, int OE_MAX = 16, typename VAL = uint32_t,
-          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false, int MINW = 4, bool PRE16 = false>
+          bool HAS_VAL = false, bool BOUNDS = false, bool PERSIST = false, int MINW = 4, bool PRE16 = false,
+          int ONEB = 0>
 __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or two 512-thread blocks per CU
     void k_bucket_sort(U* __restrict__ keys, const uint64_t* __restrict__ seg, int top_single, X xf,
                        VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr,
                        const int32_t* __restrict__ ctl = nullptr, uint32_t first_bucket = 0,
-                       uint32_t* __restrict__ big = nullptr) {
+                       uint32_t* __restrict__ big = nullptr, uint32_t* __restrict__ redo_n = nullptr,
+                       uint32_t* __restrict__ redo_ids = nullptr) {
     static_assert(!PERSIST || BOUNDS, "the persistent form strides over bucket bounds");
+    static_assert(ONEB == 0 || (!HAS_VAL && BOUNDS && ONEB >= 9 && ONEB <= 14), "one-pass form: keys, bucket bounds");
     // device-planned sort: ctl = {on, buckets, top_single}; the grid covers
     // the largest bucket count (or strides over it), blocks past the planned
     // count return
@@ -1061,6 +1082,10 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
         nbk = static_cast<uint32_t>(ctl[1]);
         top_single = ctl[2];
     }
+    // the two-pass form over the buckets a one-pass launch handed on
+    // (redo_ids[0, *redo_n)); the one-pass form appends to that list
+    const bool listed = ONEB == 0 && PERSIST && redo_ids != nullptr;
+    if (listed) nbk = *redo_n;
     constexpr int WAVES = THREADS / kWave;
     constexpr int CHUNK = ITEMS * kWave;
     constexpr int BITS = static_cast<int>(sizeof(U) * 8);
@@ -1068,8 +1093,13 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     static_assert(THREADS >= kRadix, "one thread per digit in the offset scan");
     __shared__ alignas(16) U s_keys[THREADS * ITEMS];
     __shared__ alignas(16) VAL s_vals[HAS_VAL ? THREADS * ITEMS : 1];
-    __shared__ alignas(16) uint16_t s_whist[WAVES][kRadix];
-    __shared__ uint32_t s_wsum[kRadix / kWave];
+    // the per-wave 16-bit digit counters of the two-pass form; the one-pass
+    // form's 2^ONEB bins share their LDS (the larger of the two)
+    constexpr int kWhistWords = WAVES * kRadix / 2;
+    constexpr int kAuxWords = (ONEB > 0 && (1 << (ONEB - 1)) > kWhistWords) ? (1 << (ONEB - 1)) : kWhistWords;
+    __shared__ alignas(16) uint32_t s_aux[kAuxWords];
+    uint16_t (*s_whist)[kRadix] = reinterpret_cast<uint16_t (*)[kRadix]>(s_aux);
+    __shared__ uint32_t s_wsum[(kRadix / kWave) > WAVES ? kRadix / kWave : WAVES];
     __shared__ U s_ends[2];
     // PRE16 (r05): the second LDS pass also leaves each key's 16 sorted bits
     // here, so the run detection reads 8 prefixes per 16-B LDS load instead
@@ -1166,6 +1196,120 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     }
     if (top <= 0) return;  // all keys equal
 
+    // ---- the one-pass form (ONEB, see above)
+    if constexpr (ONEB > 0) {
+        constexpr uint32_t NB = 1u << ONEB;
+        constexpr int WPT = static_cast<int>(NB / 2) / THREADS;  // packed counter words per thread
+        static_assert(WPT >= 4 && WPT % 4 == 0 && WPT * THREADS * 2 == static_cast<int>(NB), "bins per thread");
+        using W4 = vec<uint32_t, 4>;
+        const int sh0 = top > ONEB ? top - ONEB : 0;
+        auto digit = [&](const U& x) { return static_cast<uint32_t>(xf(x) >> sh0) & (NB - 1u); };
+        auto bin_off = [&](uint32_t d) { return (s_aux[d >> 1] >> (16u * (d & 1u))) & 0xffffu; };
+#pragma unroll
+        for (int j = 0; j < WPT / 4; ++j) reinterpret_cast<W4*>(s_aux)[j * THREADS + t] = W4{{0u, 0u, 0u, 0u}};
+        __syncthreads();
+        // ranks inside the bins (LDS atomics; the order inside a bin is
+        // settled by the in-bin ranking below), two 16-bit ranks per register
+        uint32_t slot[(ITEMS + 1) / 2];
+#pragma unroll
+        for (int r = 0; r < (ITEMS + 1) / 2; ++r) slot[r] = 0;
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const uint64_t act = active(r);
+            if (act == 0) break;  // uniform
+            if ((act >> lane) & 1u) {
+                const uint32_t d = digit(k[r]);
+                const uint32_t sh = 16u * (d & 1u);
+                const uint32_t old = atomicAdd(&s_aux[d >> 1], 1u << sh);
+                slot[r / 2] |= ((old >> sh) & 0xffffu) << (16 * (r & 1));
+            }
+        }
+        __syncthreads();
+        // exclusive scan of the bins: thread t owns bins [2 WPT t, 2 WPT (t + 1))
+        uint32_t w[WPT];
+#pragma unroll
+        for (int j = 0; j < WPT / 4; ++j) {
+            const W4 q = reinterpret_cast<const W4*>(s_aux)[t * (WPT / 4) + j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[4 * j + i] = q.v[i];
+        }
+        uint32_t sum = 0, mx = 0;
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+            const uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
+            sum += lo + hi;
+            mx = lo > mx ? lo : mx;
+            mx = hi > mx ? hi : mx;
+        }
+        const uint32_t incl = wave_inclusive_scan(sum, op_plus{});
+        if (lane == kWave - 1) s_wsum[wave] = incl;
+        if (__syncthreads_or(mx > kOneBinMax)) {
+            // a bin too large for the in-bin ranking: the bucket goes to the
+            // two-pass launch that follows (its keys are still in place)
+            if (t == 0) redo_ids[atomicAdd(redo_n, 1u)] = bk;
+            return;
+        }
+        {
+            uint32_t run = incl - sum;
+#pragma unroll
+            for (int ww = 0; ww < WAVES; ++ww)
+                if (ww < wave) run += s_wsum[ww];
+#pragma unroll
+            for (int j = 0; j < WPT; ++j) {
+                const uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
+                w[j] = run | ((run + lo) << 16);  // offsets <= m < 2^16
+                run += lo + hi;
+            }
+#pragma unroll
+            for (int j = 0; j < WPT / 4; ++j)
+                reinterpret_cast<W4*>(s_aux)[t * (WPT / 4) + j] = W4{{w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]}};
+            __syncthreads();
+            // scatter into the bins; slot: rank -> position
+#pragma unroll
+            for (int r = 0; r < ITEMS; ++r) {
+                const uint64_t act = active(r);
+                if (act == 0) break;
+                if ((act >> lane) & 1u) {
+                    const uint32_t pos = bin_off(digit(k[r])) + ((slot[r / 2] >> (16 * (r & 1))) & 0xffffu);
+                    s_keys[pos] = k[r];
+                    slot[r / 2] = (slot[r / 2] & (0xffff0000u >> (16 * (r & 1)))) | (pos << (16 * (r & 1)));
+                }
+            }
+            __syncthreads();
+            // a bin's keys agree on every bit at or above sh0; with sh0 = 0
+            // they are equal and the scatter is the sorted order
+            if (sh0 > 0) {
+#pragma unroll
+                for (int r = 0; r < ITEMS; ++r) {
+                    const uint64_t act = active(r);
+                    if (act == 0) break;
+                    if ((act >> lane) & 1u) {
+                        const uint32_t d = digit(k[r]);
+                        const uint32_t s = bin_off(d), e = d + 1 < NB ? bin_off(d + 1) : m;
+                        if (e - s > 1) {
+                            const uint32_t pos = (slot[r / 2] >> (16 * (r & 1))) & 0xffffu;
+                            const U xk = xf(k[r]);
+                            uint32_t c = 0;
+                            for (uint32_t j = s; j < e; ++j) {
+                                const U y = xf(s_keys[j]);
+                                c += (y < xk || (y == xk && j < pos)) ? 1u : 0u;
+                            }
+                            slot[r / 2] = (slot[r / 2] & (0xffff0000u >> (16 * (r & 1)))) | ((s + c) << (16 * (r & 1)));
+                        }
+                    }
+                }
+                __syncthreads();  // every bin read before any key moves
+#pragma unroll
+                for (int r = 0; r < ITEMS; ++r) {
+                    const uint64_t act = active(r);
+                    if (act == 0) break;
+                    if ((act >> lane) & 1u) s_keys[(slot[r / 2] >> (16 * (r & 1))) & 0xffffu] = k[r];
+                }
+                __syncthreads();
+            }
+        }
+    }
+
     // one stable pass on the digit at `shift`: registers -> s_keys (ranked).
     // atom (HPXHIP_SEG_ATOM1, keys only): the first pass under `top` ranks by
     // LDS atomics on the packed 16-bit per-wave counters instead of the
@@ -1255,7 +1399,7 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     // the full LSD over every bit under `top`
     bool lsd = false;
     int npass = 2;
-    for (int q = 0; q < npass;) {
+    for (int q = 0; ONEB == 0 && q < npass;) {
         const int lo = lsd ? top - 8 * (npass - q) : top - 8 * (2 - q);
         pass(lo > 0 ? lo : 0, !lsd && q == 1 && top > 16, !lsd && q == 0);
         if (++q < npass) {
@@ -1405,7 +1549,7 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     // launch sized for the typical plan, then a striding one for the rest)
     if constexpr (PERSIST) {
         for (uint32_t bk = first_bucket + blockIdx.x; bk < nbk; bk += gridDim.x) {
-            one(bk);
+            one(listed ? redo_ids[bk] : bk);
             __syncthreads();  // s_keys / s_vals read out before the next bucket's passes
         }
     } else if (first_bucket + blockIdx.x < nbk) {

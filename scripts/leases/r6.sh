@@ -44,4 +44,27 @@ lease_b() {
   done
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b"; fi
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c"; fi
+
+lease_c() {
+  # round 6, lease c: the one-pass segment sort (k_bucket_sort ONEB = 13, in-bin ranking by counting,
+  # long bins handed to the two-pass form): sort tests, then A/B against ONE = 0 (the r05 two-pass form)
+  # and ONE = 12, u64 / u32 / u64hot at 2^30 / 2^28, and a kernel trace of the u64 sort
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6c
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sort_hybrid.py \
+    tests/test_gpu_fullsize.py -k "sort" > ${L}_tests.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for lib in hpx_amd/libhpxhip.so scripts/ubench/seglib/one0/libhpxhip.so scripts/ubench/seglib/one12/libhpxhip.so; do
+      for c in u64 u32; do
+        echo "== $lib $c rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 30 >> ${L}_ab.log 2>&1 || exit $?
+      done
+      echo "== $lib u64hot rep $rep" >> ${L}_ab.log
+      HPXHIP_LIB=$lib SORT_ONLY=u64hot timeout -k 10 200 python -u scripts/sort_probe.py 28 >> ${L}_ab.log 2>&1 || exit $?
+    done
+  done
+  SORT_ONLY=u64 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6c_prof_u64 -o run -- \
+    python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
+}
