@@ -75,11 +75,17 @@ constexpr uint64_t kTileChunk = 256;
 struct sort_layout {
     uint64_t ntiles;
     size_t alt_keys, alt_vals, hist, xhist, thist, joint, bits, start, xstart, tstart, bounds, ctl, counter, lb,
-        lb_bytes, tcount, csum, nchunks, segs, big, shist, sstart, segs2, bs2, total;
+        lb_bytes, tcount, csum, nchunks, segs, big, shist, sstart, segs2, bs2, pad, pad_keys, total;
     bool wide;  // 64-bit granules
 };
 
 bool takes_pre18(uint64_t n, size_t vsize, int tile);
+// r06: the padded second pass (k_pad_scatter); 0: the look-back pass (A/B builds)
+#ifndef HPXHIP_SORT_PAD
+#define HPXHIP_SORT_PAD 1
+#endif
+// the 18-bit form's segment capacity (kCap18 below), the padded pass's largest slot
+constexpr uint64_t kPadSlotMax = 512 * 9;
 constexpr uint64_t kHybridMin = 1ull << 22;
 
 sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
@@ -143,6 +149,13 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     off = align_up(off + (pre ? sizeof(seg_table) : 0), 256);
     L.bs2 = off;
     off = align_up(off + (pre ? 8 * kXBins * 8 : 0), 256);
+    // r06: the padded second pass's bucket slots (k_pad_scatter): room for
+    // the plan's buckets x slot capacity, at most 2^18 x kCap18 (9.7 GB at
+    // 2^30 u64 keys); the slot counters live at the start of lb (free until
+    // the look-back pass that replaces a padded pass whose slot overflowed)
+    L.pad_keys = pre ? std::min<uint64_t>(n + n / 4 + kPadSlotMax, static_cast<uint64_t>(kMaxBuckets) * kPadSlotMax) : 0;
+    L.pad = off;
+    off = align_up(off + L.pad_keys * ksize, 256);
     L.total = off;
     return L;
 }
@@ -175,6 +188,7 @@ constexpr uint64_t kCapKV = static_cast<uint64_t>(kSegThreads16) * kSegItemsKV;
 // the 8192-key 512 x 18 shape, profiles/r04_ubench_segment_occupancy.log).
 constexpr int kSegItems18 = 9;
 constexpr uint64_t kCap18 = static_cast<uint64_t>(kSegThreads17) * kSegItems18;
+static_assert(kCap18 == kPadSlotMax, "padded slots hold a segment");
 // r06: the one-pass segment sort (k_bucket_sort ONEB) bound to three
 // workgroups per CU (6 waves per SIMD: <= 80 VGPRs); unbounded it took 119
 #ifndef HPXHIP_SEG_MINW18
@@ -235,7 +249,10 @@ enum : int {
     C_SEGLSD = 44,     // hybrid-sized sorts: the LSD passes run over the segment table
     C_SEGHIST = 45,    // ... whose histograms are counted first (the oversized-bucket finish)
     C_REDO = 46,       // buckets the one-pass segment sort handed to the two-pass form (ids in the lb scratch)
-    C_WORDS = 47
+    C_PAD = 47,        // r06: slot capacity of the padded second pass (k_pad_scatter), 0 = not taken
+    C_B9P = 48,        // ... its top-9 shift, -1 = not run
+    C_PADOVF = 49,     // ... raised when a slot overflowed (the look-back pass runs instead)
+    C_WORDS = 50
 };
 static_assert(C_WORDS * 4 <= 256, "plan words fit their slot");
 
@@ -273,7 +290,7 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
                             const unsigned long long* __restrict__ thist,
                             const unsigned long long* __restrict__ bits, uint64_t n, int passes, int first, int mode,
                             int has_val, int stage, int32_t* __restrict__ ctl, seg_table* __restrict__ segs = nullptr,
-                            uint32_t* __restrict__ big = nullptr, int tile = 0) {
+                            uint32_t* __restrict__ big = nullptr, int tile = 0, uint64_t pad_keys = 0) {
     if (blockIdx.x != 0) return;
     // 18-bit form: the statistics of the two 9-bit histograms, by the 64
     // threads of the launch (r05; one thread reading 9 x 512 bins took ~0.1
@@ -282,13 +299,19 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
     // hot bins (over twice the mean) of both and their excess keys
     __shared__ double s_mtop, s_mt, s_et, s_ef, s_mg[10], s_mgn[10];
     __shared__ int s_ht, s_hf;
+    // r06: the field histogram staged in LDS first -- the group sums below
+    // had walked it in global memory, one dependent load after another (the
+    // plan took 85-140 us of every 2^30 sort, profiles/r06_sort_kernel_stats_u64_a.csv)
+    __shared__ double s_x[kXBins];
     if (mode == 18 && !has_val && stage == 0 && thist) {
         const int t = threadIdx.x;
+        for (int i = t; i < kXBins; i += 64) s_x[i] = static_cast<double>(xhist[i]);
+        __syncthreads();
         const double mean = static_cast<double>(n) / kXBins;
         double mtop = 0, mt = mean, et = 0, ef = 0;
         int ht = 0, hf = 0;
         for (int i = t; i < kXBins; i += 64) {
-            const double a = static_cast<double>(thist[i]), b = static_cast<double>(xhist[i]);
+            const double a = static_cast<double>(thist[i]), b = s_x[i];
             mtop = a > mtop ? a : mtop;
             if (a > 2 * mean) ++ht, et += a - mean;
             else mt = a > mt ? a : mt;
@@ -303,7 +326,7 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
                 double sum = 0;
                 bool hot = false;
                 for (int k = 0; k < g; ++k) {
-                    const double b = static_cast<double>(xhist[i + k]);
+                    const double b = s_x[i + k];
                     sum += b;
                     hot = hot || b > 2 * mean;
                 }
@@ -338,6 +361,7 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
         for (int i = 0; i < C_WORDS; ++i) ctl[i] = 0;
         for (int i = 0; i < 11; ++i) ctl[i] = -1;
         ctl[C_B9] = -1;
+        ctl[C_B9P] = -1;
         ctl[C_FIRST] = first;
         if (big) big[0] = 0;
     }
@@ -383,12 +407,24 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
     if (mode == 18 && !has_val && stage == 0 && top_two) {
         // top 9 bits [8P - 9, 8P), field [8P - 18, 8P - 9): b2 <= 9 bits of the field
         const int fs = 8 * passes - 18;
-        for (int b2 = 1; b2 <= 9; ++b2)
-            if (fits(s_mtop * s_mg[b2] / dn, kCap18)) {
+        for (int b2 = 1; b2 <= 9; ++b2) {
+            const double est = s_mtop * s_mg[b2] / dn;
+            if (fits(est, kCap18)) {
                 ctl[C_A9] = fs;
-                ctl[C_B9] = 8 * passes - 9;
+                // r06: the padded second pass when its slots -- the estimated
+                // largest bucket + 7 sigma, whole 64-key lines -- fit the scratch
+                const uint32_t nb = 512u << b2;
+                uint32_t cap = (static_cast<uint32_t>(est + 7.0 * sqrt(est) + 1.0) + 63u) & ~63u;
+                cap = cap < kCap18 ? cap : static_cast<uint32_t>(kCap18);
+                if (pad_keys > 0 && static_cast<uint64_t>(nb) * cap <= pad_keys) {
+                    ctl[C_B9P] = 8 * passes - 9;
+                    ctl[C_PAD] = static_cast<int32_t>(cap);
+                } else {
+                    ctl[C_B9] = 8 * passes - 9;
+                }
                 return plan(8 * passes - 9, fs + 9 - b2, b2, C_SEGC, 9);
             }
+        }
         // r05: skew concentrated in a few buckets -- a few hot top-9 bins
         // whose excess keys sit in a few hot field bins (the same keys: the
         // excess masses match) -- is left to the bounded finish of the
@@ -493,6 +529,20 @@ __global__ __launch_bounds__(256) void k_zero_gated(uint4* __restrict__ p, uint6
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n16; i += stride)
         p[i] = make_uint4(0, 0, 0, 0);
+}
+
+// After the padded second pass (r06): a slot overflowed -> the look-back
+// pass runs from the same input, the bounds come from the binary search and
+// the segment sort reads the keys; else the bounds come from the slot counts
+// (k_pad_bounds) and the segment sort reads the slots.
+__global__ void k_pad_check(int32_t* __restrict__ ctl) {
+    if (threadIdx.x != 0 || blockIdx.x != 0 || ctl[C_B9P] < 0) return;
+    if (ctl[C_PADOVF]) {
+        ctl[C_B9] = ctl[C_B9P];
+        ctl[C_PAD] = 0;
+    } else {
+        ctl[C_BOUNDS] = 0;
+    }
 }
 
 // dst[0, n) = src[0, n), run iff *gate != 0.
@@ -680,7 +730,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     auto* segs = mode ? reinterpret_cast<seg_table*>(base + L.segs) : nullptr;
     auto* big = mode ? reinterpret_cast<uint32_t*>(base + L.big) : nullptr;
     hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, thist, bits, n, passes, first, mode,
-                       HAS_VAL ? 1 : 0, 0, ctl, segs, big, TS::tile);
+                       HAS_VAL ? 1 : 0, 0, ctl, segs, big, TS::tile, static_cast<uint64_t>(HPXHIP_SORT_PAD ? L.pad_keys : 0));
     HPXHIP_CHECK_LAUNCH();
     if (first > 0) {
         if ((rc = count_rest(ctl + C_HIST_A))) return rc;
@@ -711,11 +761,27 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         if ((rc = pass(ka, kc, va, vc, 8, ctl + C_B, mode == 18))) return rc;
         if constexpr (!HAS_VAL) {
             if (mode == 18 && pre18) {
+                // r06: the padded second pass (k_pad_scatter), iff planned:
+                // slot counters zeroed (with the tile counter), the pass, and
+                // the check that hands a sort whose slots overflowed to the
+                // look-back pass below
+                const uint64_t nt = L.ntiles + 8;
+                auto* pcnt = reinterpret_cast<uint32_t*>(base + L.lb);
+                const uint64_t pz = align_up(256 + 4ull * kMaxBuckets, 16);
+                hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(pz / 16, 2048)), dim3(256), 0, s,
+                                   reinterpret_cast<uint4*>(counter), pz / 16, ctl + C_B9P);
+                HPXHIP_CHECK_LAUNCH();
+                hipLaunchKernelGGL((k_pad_scatter<U, X, TS::threads, TS::items>), dim3(static_cast<unsigned>(nt)),
+                                   dim3(TS::threads), 0, s, ka, reinterpret_cast<U*>(base + L.pad), ctl + C_B9P,
+                                   ctl + C_BOUNDS, ctl + C_PAD, reinterpret_cast<const seg_table*>(base + L.segs2),
+                                   counter, pcnt, ctl + C_PADOVF, X{});
+                HPXHIP_CHECK_LAUNCH();
+                hipLaunchKernelGGL(k_pad_check, dim3(1), dim3(64), 0, s, ctl);
+                HPXHIP_CHECK_LAUNCH();
                 // r05: the top-9 pass over the field-ordered keys in 8 field
                 // regions, one per XCD, each with its own look-back and bin
                 // starts (k_region_plan): consecutive tiles' digit runs meet in
                 // one L2, as in the first pass (XREG + SEG)
-                const uint64_t nt = L.ntiles + 8;
                 const uint64_t zbytes = align_up(256 + nt * kXBins * (L.wide ? 8 : 4), 16);
                 hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
                                    reinterpret_cast<uint4*>(counter), zbytes / 16, ctl + C_B9);
@@ -742,6 +808,11 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         hipLaunchKernelGGL((k_bucket_bounds<U, X>), dim3((kMaxBuckets + 1 + 255) / 256), dim3(256), 0, s, kc, n, 0, 0,
                            0, 0u, X{}, bounds, ctl + C_BOUNDS);
         HPXHIP_CHECK_LAUNCH();
+        if (!HAS_VAL && mode == 18 && pre18) {  // the padded pass's bounds: a scan of its slot counts
+            hipLaunchKernelGGL(k_pad_bounds, dim3(1), dim3(1024), 0, s, reinterpret_cast<const uint32_t*>(base + L.lb),
+                               ctl + C_BOUNDS, ctl + C_PAD, bounds);
+            HPXHIP_CHECK_LAUNCH();
+        }
         auto* oversized = reinterpret_cast<uint32_t*>(ctl + C_OVERSIZED);
         // The segment sort the plan usually takes: one workgroup per bucket
         // over the buckets a typical plan has (twice n / 8192, at most the
@@ -780,21 +851,25 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
             // sorted by the two-pass form in a third, striding launch
             auto* redo_n = reinterpret_cast<uint32_t*>(ctl + C_REDO);
             auto* redo_ids = reinterpret_cast<uint32_t*>(base + L.lb);  // lb_bytes >= 576 x 2 KiB > 4 x 2^18
+            // (the padded pass's slot counters there are read by k_pad_bounds, before)
+            const U* padp = L.pad_keys ? reinterpret_cast<const U*>(base + L.pad) : nullptr;
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true, false,
                                               kSegMinW18, false, HPXHIP_SEG_ONE>),
                                dim3(g18), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr, oversized,
-                               ctl + C_SEGC, 0u, big, redo_n, HPXHIP_SEG_ONE > 0 ? redo_ids : nullptr);
+                               ctl + C_SEGC, 0u, big, redo_n, HPXHIP_SEG_ONE > 0 ? redo_ids : nullptr,
+                               padp, ctl + C_PAD);
             HPXHIP_CHECK_LAUNCH();
             if (g18 < kMaxBuckets)
                 hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true, true,
                                                   kSegMinW18, false, HPXHIP_SEG_ONE>),
                                    dim3(3 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
-                                   oversized, ctl + C_SEGC, g18, big, redo_n, HPXHIP_SEG_ONE > 0 ? redo_ids : nullptr);
+                                   oversized, ctl + C_SEGC, g18, big, redo_n, HPXHIP_SEG_ONE > 0 ? redo_ids : nullptr,
+                                   padp, ctl + C_PAD);
             HPXHIP_CHECK_LAUNCH();
             if (HPXHIP_SEG_ONE > 0)
                 hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems18, 16, uint32_t, false, true, true>),
                                    dim3(3 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,
-                                   oversized, ctl + C_SEGC, 0u, big, redo_n, redo_ids);
+                                   oversized, ctl + C_SEGC, 0u, big, redo_n, redo_ids, padp, ctl + C_PAD);
             HPXHIP_CHECK_LAUNCH();
             hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItems, 16, uint32_t, false, true, true>),
                                dim3(2 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, nullptr,

@@ -984,6 +984,216 @@ __device__ __forceinline__ uint32_t bucket_of(U k, int s1, int s2, int b2, X xf,
     return (static_cast<uint32_t>(u >> s1) & tmask) << b2 | (static_cast<uint32_t>(u >> s2) & ((1u << b2) - 1u));
 }
 
+// ---------------------------------------------- padded second pass (r06)
+// The 18-bit form's second prefix pass without a look-back.  Its input is
+// ordered by the field (the first pass), and what it must produce is every
+// bucket -- (top 9 bits, top b2 bits of the field) -- contiguous: the order
+// of the keys INSIDE a bucket is never relied on (keys only; the segment sort
+// orders each bucket completely).  So each bucket gets a slot of `cap` keys
+// in a padded buffer (pad[bucket * cap ...], cap >= the plan's largest
+// bucket estimate + 7 sigma), and a tile claims its run of each bucket with
+// one global atomic on the bucket's counter (pcnt) instead of walking back
+// over its predecessors: no tile waits for another.  The look-back pass took
+// 4.9-5.0 ms at 2^30 u64 against 3.8-3.9 for the offset-fed first pass
+// (profiles/r06_sort_kernel_stats_u64_c.csv).  The bucket bounds are then the
+// exclusive scan of the slot counts (k_pad_bounds), and the segment sort
+// reads each bucket from its slot and writes it to its place in the keys.
+// Tiles: as the look-back pass (XREG regions of the field, 8192 keys, one
+// workgroup per tile claimed from its XCD's region, so consecutive tiles --
+// which append to the same slots -- meet in one L2).  A tile's keys span a
+// non-decreasing range of field parts fb; local bin = (fb - fb of the tile's
+// first key) * 512 + top-9 digit for the first two fb values (block-wide LDS
+// atomics, 1024 bins), and keys further on (a tile over three or more field
+// parts: small or skewed field bins) claim their slot places one by one.  A
+// bucket whose slot overflows raises *ovf: sort.hip then runs the look-back
+// pass from the same input (left intact) instead.
+template <typename U, typename X, int THREADS = 512, int ITEMS = 16>
+__global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict__ kin, U* __restrict__ pad,
+                                                          const int32_t* __restrict__ g_s1,
+                                                          const int32_t* __restrict__ g_bounds,
+                                                          const int32_t* __restrict__ g_cap,
+                                                          const seg_table* __restrict__ segs,
+                                                          uint32_t* __restrict__ counter, uint32_t* __restrict__ pcnt,
+                                                          int32_t* __restrict__ ovf, X xf) {
+    const int s1 = *g_s1;  // the top-9 digit's shift, -1: the plan does not take this pass
+    if (s1 < 0) return;
+    const int s2 = g_bounds[3], b2 = g_bounds[4];
+    const uint32_t cap = static_cast<uint32_t>(*g_cap);
+    const uint32_t bmask = (1u << b2) - 1u;
+    constexpr int TILE = THREADS * ITEMS;
+    constexpr int WAVES = THREADS / kWave;
+    constexpr uint32_t NL = 1024;  // local bins; bin NL: keys placed one by one
+    static_assert(THREADS == 512, "one thread per two local bins");
+    __shared__ uint32_t s_tile, s_seg;
+    __shared__ uint64_t s_sg[3 * kMaxBig + 2];
+    __shared__ uint32_t s_cnt[NL + 1];
+    __shared__ uint32_t s_adj[NL];
+    __shared__ uint32_t s_wsum[WAVES];
+    __shared__ U s_keys[TILE];
+    const int t = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = t / kWave;
+    for (int i = t; i <= 8; i += THREADS) {
+        if (i < 8) {
+            s_sg[i] = segs->start[i];
+            s_sg[kMaxBig + i] = segs->len[i];
+        }
+        s_sg[2 * kMaxBig + i] = segs->tile0[i];
+    }
+    if (t == 0) {
+        s_sg[3 * kMaxBig + 1] = segs->nseg;
+        // the next tile of this XCD's region (see k_onesweep XREG)
+        const uint32_t x = xcc_id();
+        uint32_t tl = 0xffffffffu, sg = 0;
+        const uint32_t nseg = segs->nseg;
+        for (uint32_t k = 0; k < 8 && tl == 0xffffffffu; ++k) {
+            const uint32_t xr = (x + k) & 7u;
+            if (xr >= nseg) continue;
+            const uint64_t lo = segs->tile0[xr], cnt = segs->tile0[xr + 1] - lo;
+            if (cnt == 0) continue;
+            const uint32_t c = __hip_atomic_fetch_add(counter + 8 * xr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c < cnt) {
+                tl = static_cast<uint32_t>(lo + c);
+                sg = xr;
+            }
+        }
+        s_tile = tl;
+        s_seg = sg;
+    }
+    for (uint32_t i = t; i <= NL; i += THREADS) s_cnt[i] = 0;
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    if (tile == 0xffffffffu) return;
+    const uint32_t j = s_seg;
+    const uint64_t seg_lo = s_sg[j], end = seg_lo + s_sg[kMaxBig + j];
+    const uint64_t tile_base = seg_lo + (tile - s_sg[2 * kMaxBig + j]) * TILE;
+    const bool full = tile_base + TILE <= end;
+    const uint64_t wbase = tile_base + static_cast<uint64_t>(wave) * (TILE / WAVES);
+    const uint32_t fb0 = static_cast<uint32_t>(xf(kin[tile_base]) >> s2) & bmask;
+    auto local_bin = [&](const U& key) {
+        const U u = xf(key);
+        const uint32_t rel = (static_cast<uint32_t>(u >> s2) & bmask) - fb0;
+        return rel < 2u ? rel * 512u + (static_cast<uint32_t>(u >> s1) & 511u) : NL;
+    };
+    U k[ITEMS];
+    {
+        const uint64_t last = end - 1;
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const uint64_t i = wbase + r * kWave + lane;
+            k[r] = kin[(full || i < end) ? i : last];
+        }
+    }
+    // ranks inside the local bins (LDS atomics: no order is owed inside a bucket)
+    uint32_t rank[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const uint64_t i = wbase + r * kWave + lane;
+        if (full || i < end) rank[r] = atomicAdd(&s_cnt[local_bin(k[r])], 1u);
+    }
+    __syncthreads();
+    // local starts (thread t: bins 2t, 2t + 1; the one-by-one bin last) and
+    // each bin's run of its bucket's slot
+    {
+        const uint32_t c0 = s_cnt[2 * t], c1 = s_cnt[2 * t + 1];
+        const uint32_t sum = c0 + c1;
+        const uint32_t incl = wave_inclusive_scan(sum, op_plus{});
+        if (lane == kWave - 1) s_wsum[wave] = incl;
+        __syncthreads();
+        uint32_t pre = incl - sum;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w)
+            if (w < wave) pre += s_wsum[w];
+        const uint32_t ls[2] = {pre, pre + c0}, cs[2] = {c0, c1};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t lb = 2 * t + h;
+            if (cs[h]) {
+                const uint32_t bucket = ((lb & 511u) << b2) | (fb0 + (lb >> 9));
+                const uint32_t base = __hip_atomic_fetch_add(&pcnt[bucket], cs[h], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+                if (base + cs[h] <= cap) {
+                    s_adj[lb] = bucket * cap + base - ls[h];  // mod 2^32: pad index of local position ls
+                } else {
+                    s_adj[lb] = 0xffffffffu;
+                    __hip_atomic_store(ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            s_cnt[lb] = ls[h];
+        }
+        if (t == THREADS - 1) s_cnt[NL] = pre + sum;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const uint64_t i = wbase + r * kWave + lane;
+        if (full || i < end) s_keys[s_cnt[local_bin(k[r])] + rank[r]] = k[r];
+    }
+    __syncthreads();
+    const uint32_t nvalid = full ? TILE : static_cast<uint32_t>(end - tile_base);
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const uint32_t i = r * THREADS + t;
+        if (i < nvalid) {
+            const U key = s_keys[i];
+            const uint32_t lb = local_bin(key);
+            if (lb < NL) {
+                const uint32_t a = s_adj[lb];
+                if (a != 0xffffffffu) pad[a + i] = key;
+            } else {
+                const U u = xf(key);
+                const uint32_t bucket = ((static_cast<uint32_t>(u >> s1) & 511u) << b2) |
+                                        (static_cast<uint32_t>(u >> s2) & bmask);
+                const uint32_t base = __hip_atomic_fetch_add(&pcnt[bucket], 1u, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+                if (base < cap) pad[bucket * cap + base] = key;
+                else __hip_atomic_store(ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
+// off[v] = sum of the slot counts of buckets < v (v = 0..nb): the bucket
+// bounds of the padded pass, one workgroup; runs iff *g_cap > 0 (the padded
+// pass ran and no slot overflowed).  g_bounds = {on, nb, ...}.
+__global__ __launch_bounds__(1024) void k_pad_bounds(const uint32_t* __restrict__ pcnt,
+                                                      const int32_t* __restrict__ g_bounds,
+                                                      const int32_t* __restrict__ g_cap, uint64_t* __restrict__ off) {
+    if (*g_cap <= 0) return;
+    const uint32_t nb = static_cast<uint32_t>(g_bounds[1]);
+    const int t = threadIdx.x;
+    const int lane = lane_id(), wave = t / kWave;
+    __shared__ uint64_t s_w[1024 / kWave];
+    // thread t: buckets [t * per, (t + 1) * per), read as 16-B vectors (nb is
+    // a power of two >= 1024, so every range is whole vectors)
+    const uint32_t per = ((nb + 1023) / 1024 + 3) & ~3u;
+    const uint32_t lo = t * per < nb ? t * per : nb, hi = lo + per < nb ? lo + per : nb;
+    const uint4* p4 = reinterpret_cast<const uint4*>(pcnt + lo);
+    const uint32_t n4 = (hi - lo) / 4;
+    uint64_t sum = 0;
+#pragma unroll 8
+    for (uint32_t q = 0; q < n4; ++q) {
+        const uint4 c = p4[q];
+        sum += static_cast<uint64_t>(c.x) + c.y + c.z + c.w;
+    }
+    const uint64_t incl = wave_inclusive_scan(sum, op_plus{});
+    if (lane == kWave - 1) s_w[wave] = incl;
+    __syncthreads();
+    uint64_t run = incl - sum;
+    for (int w = 0; w < wave; ++w) run += s_w[w];
+#pragma unroll 4
+    for (uint32_t q = 0; q < n4; ++q) {
+        const uint4 c = p4[q];
+        const uint32_t v = lo + 4 * q;
+        off[v] = run;
+        off[v + 1] = run + c.x;
+        off[v + 2] = run + c.x + c.y;
+        off[v + 3] = run + c.x + c.y + c.z;
+        run += static_cast<uint64_t>(c.x) + c.y + c.z + c.w;
+    }
+    if (t == 1023) off[nb] = run;
+}
+
 // off[v] = first index whose prefix is >= v (v = 0..nb): a lower_bound per
 // bucket over the prefix-ordered keys instead of a pass over all of them.
 // ctl (device-planned sort): {on, nb, s1, s2, b2} read on the device.
@@ -1070,7 +1280,8 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
                        VAL* __restrict__ vals = nullptr, uint32_t* __restrict__ oversized = nullptr,
                        const int32_t* __restrict__ ctl = nullptr, uint32_t first_bucket = 0,
                        uint32_t* __restrict__ big = nullptr, uint32_t* __restrict__ redo_n = nullptr,
-                       uint32_t* __restrict__ redo_ids = nullptr) {
+                       uint32_t* __restrict__ redo_ids = nullptr, const U* __restrict__ pad = nullptr,
+                       const int32_t* __restrict__ pad_cap = nullptr) {
     static_assert(!PERSIST || BOUNDS, "the persistent form strides over bucket bounds");
     static_assert(ONEB == 0 || (!HAS_VAL && BOUNDS && ONEB >= 9 && ONEB <= 14), "one-pass form: keys, bucket bounds");
     // device-planned sort: ctl = {on, buckets, top_single}; the grid covers
@@ -1096,7 +1307,8 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     // the per-wave 16-bit digit counters of the two-pass form; the one-pass
     // form's 2^ONEB bins share their LDS (the larger of the two)
     constexpr int kWhistWords = WAVES * kRadix / 2;
-    constexpr int kAuxWords = (ONEB > 0 && (1 << (ONEB - 1)) > kWhistWords) ? (1 << (ONEB - 1)) : kWhistWords;
+    constexpr int kOneWords = ONEB > 0 ? (1 << (ONEB > 0 ? ONEB - 1 : 0)) : 0;
+    constexpr int kAuxWords = kOneWords > kWhistWords ? kOneWords : kWhistWords;
     __shared__ alignas(16) uint32_t s_aux[kAuxWords];
     uint16_t (*s_whist)[kRadix] = reinterpret_cast<uint16_t (*)[kRadix]>(s_aux);
     __shared__ uint32_t s_wsum[(kRadix / kWave) > WAVES ? kRadix / kWave : WAVES];
@@ -1146,6 +1358,13 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     const uint64_t tail_mask = (have % kWave) ? (~0ull >> (kWave - have % kWave)) : 0ull;
     auto active = [&](int r) -> uint64_t { return r < nfull ? ~0ull : (r == nfull ? tail_mask : 0ull); };
     U* gkeys = keys + b;
+    // r06: a bucket of the padded second pass is read from its slot
+    // (k_pad_scatter) and written to its place in the keys
+    const U* gsrc = gkeys;
+    if (!HAS_VAL && BOUNDS && pad) {
+        const int32_t pc = *pad_cap;
+        if (pc > 0) gsrc = pad + static_cast<uint64_t>(bk) * static_cast<uint32_t>(pc);
+    }
     U* lkeys = s_keys + wbase;
     VAL* gvals = HAS_VAL ? vals + b : nullptr;
     VAL* lvals = s_vals + (HAS_VAL ? wbase : 0);
@@ -1159,14 +1378,14 @@ __global__ __launch_bounds__(THREADS, MINW)  // 4 waves per SIMD: one 1024- or t
     for (int r = 0; r < ITEMS; ++r) {
         const bool on = (active(r) >> lane) & 1u;
         const uint32_t j = on ? wbase + r * kWave + lane : m - 1;
-        k[r] = ld_stream(&gkeys[j]);
+        k[r] = ld_stream(&gsrc[j]);
         if constexpr (HAS_VAL) v[r] = ld_stream(&gvals[j]);
     }
 #else
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const bool on = (active(r) >> lane) & 1u;
-        k[r] = on ? ld_stream(&gkeys[wbase + r * kWave + lane]) : U(0);
+        k[r] = on ? ld_stream(&gsrc[wbase + r * kWave + lane]) : U(0);
         if constexpr (HAS_VAL) v[r] = on ? ld_stream(&gvals[wbase + r * kWave + lane]) : VAL(0);
     }
 #endif

@@ -44,7 +44,6 @@ lease_b() {
   done
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c"; fi
 
 lease_c() {
   # round 6, lease c: the one-pass segment sort (k_bucket_sort ONEB = 13, in-bin ranking by counting,
@@ -68,3 +67,31 @@ lease_c() {
   SORT_ONLY=u64 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6c_prof_u64 -o run -- \
     python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
 }
+
+lease_d() {
+  # round 6, lease d: the padded second prefix pass (k_pad_scatter: bucket slots claimed by global atomics,
+  # no look-back) + the one-pass segment sort reading the slots: sort tests (all hybrid forms, oversized /
+  # overflow fallbacks, 2^30 element-exact), then A/B against pad0 (look-back pass) and one0pad0 (r05 form),
+  # u64 / u32 / u64hot / u64corr, and a kernel trace of the u64 sort
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6d
+  timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sort_hybrid.py \
+    tests/test_gpu_fullsize.py -k "sort" > ${L}_tests.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for lib in hpx_amd/libhpxhip.so scripts/ubench/seglib/pad0/libhpxhip.so scripts/ubench/seglib/one0pad0/libhpxhip.so; do
+      for c in u64 u32; do
+        echo "== $lib $c rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 30 >> ${L}_ab.log 2>&1 || exit $?
+      done
+      for c in u64hot u64corr; do
+        echo "== $lib $c rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 28 >> ${L}_ab.log 2>&1 || exit $?
+      done
+    done
+  done
+  SORT_ONLY=u64 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6d_prof_u64 -o run -- \
+    python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d"; fi
