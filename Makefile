@@ -87,7 +87,7 @@ tests/cxx/bin/oracle_sanitize: tests/cxx/oracle_sanitize.cpp oracle/oracle.cpp o
 	$(CXX) $(SANFLAGS) tests/cxx/oracle_sanitize.cpp oracle/oracle.cpp -o $@
 
 # ... and the hipcc-compiled ones (device closures, HPX_HOST_DEVICE lambdas)
-HIPT     := device_closures partitioned_vector closure_algorithms closure_timing dataflow_stencil
+HIPT     := device_closures partitioned_vector closure_algorithms closure_timing dataflow_stencil bench_targets
 HIPTBIN  := $(HIPT:%=tests/cxx/bin/%)
 HTFLAGS  := -O2 -std=c++17 --offload-arch=$(ARCH) --offload-compress -Wall -Wno-unused-parameter -Iinclude
 

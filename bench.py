@@ -349,6 +349,7 @@ def extras(hpx, L, ex, F, S, comm, tgt, pol, x, y, n_local, world, args):
     res["strong_2p32_int64"] = strong_row(S, F, comm, tgt, pol, args.strong_logn)
     res["double_reduce_scan"] = double_row(hpx, L, P, F, tgt, pol, tpol, n)
     res["stream_2p30"] = stream_row(hpx, L, P, F, tgt, pol, n)
+    res["cxx_drop_in"] = cxx_drop_in_row(args, world)
     # sort of 2^30 uint64 keys (8 GiB + 8 GiB workspace)
     keys = hpx.vector(n, dtype=np.uint64, tgt=tgt)
     regen = lambda: P.generate(pol, keys.begin(), keys.end(), "bits", 7)  # noqa: E731
@@ -638,7 +639,9 @@ def dist_extras(S, F, comm, tgt, pol, x, n_local, world, args):
         checked on the device: every partition sorted (is_sorted) and the
         partitions ordered across ranks (first/last keys all-gathered);
       * 1d_stencil heat, 2^32 points over the ranks, 100 steps (strong
-        scaling), halo ring over RCCL send/recv overlapped with the interior."""
+        scaling), halo ring over RCCL send/recv overlapped with the interior;
+      * the C++ drop-in (cxx_drop_in_row): partitioned_vector over every
+        local GPU from one process, run by rank 0."""
     import time
     from hpx_amd import parallel as P
     res = {"segmented_reduce_int64": seg_reduce_row(S, F, comm, tgt, pol, x)}
@@ -672,6 +675,12 @@ def dist_extras(S, F, comm, tgt, pol, x, n_local, world, args):
                                     "gkeys_per_s": round(n / best / 1e9, 3), "sorted_and_ordered": ok}
     loc.free()
     res["stencil_heat_dist"] = stencil_row(S, comm, tgt, 1 << args.stencil_logn, args.stencil_steps)
+    # the C++ drop-in over every local GPU, run by rank 0 while the others wait
+    tgt.synchronize()
+    comm.barrier()
+    if comm.rank == 0:
+        res["cxx_drop_in"] = cxx_drop_in_row(args, world)
+    comm.barrier()
     return res
 
 
@@ -728,6 +737,36 @@ def pmc_traffic(logn):
     return round(fetch + write), {"FETCH_SIZE_kb_raw": vals["FETCH_SIZE"], "WRITE_SIZE_kb": vals["WRITE_SIZE"],
                                   "read_bytes_corrected": round(fetch), "write_bytes": round(write),
                                   "algorithmic_bytes": 24 * (1 << logn)}
+
+
+def cxx_drop_in_row(args, world):
+    """The C++ drop-in path as an HPX program calls it (tests/cxx/bench_targets.hip,
+    VERDICT r05 item 7): partitioned_vector over hip::target_layout(targets),
+    the step (triad + reduce + inclusive_scan under par(task)) and the
+    heat_solver ring, through include/hpx and the C ABI in a process of its
+    own.  One GPU: 4 targets on device 0 of 2^(logn-2) elements each (the
+    step's 2^logn in total; every cross-target hand-off runs, without peer
+    copies); N GPUs (rank 0, the other ranks idle at a barrier): one target
+    per local GPU, 2^logn each, peer copies included.  Returns the program's
+    JSON row, or an error entry (never a made-up number)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cxx", "bin", "bench_targets")
+    if not os.path.exists(exe):
+        return {"error": "tests/cxx/bin/bench_targets not built (make cxxtests)"}
+    if world == 1:
+        cmd = [exe, "--targets", "4", "--logn", str(args.logn - 2), "--heat-logn", "26"]
+    else:
+        cmd = [exe, "--logn", str(args.logn), "--heat-logn", "28"]
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    except Exception as e:  # noqa: BLE001 -- report, never fake a number
+        return {"error": f"{type(e).__name__}"}
+    for line in out.stdout.splitlines():
+        if line.startswith("{\"cxx_drop_in\""):
+            row = json.loads(line)["cxx_drop_in"]
+            row["command"] = " ".join(["tests/cxx/bin/bench_targets"] + cmd[1:])
+            return row
+    return {"error": f"rc={out.returncode}", "stderr_tail": out.stderr[-400:]}
 
 
 def cpu_baseline(logn):

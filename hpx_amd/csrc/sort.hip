@@ -809,8 +809,13 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                            0, 0u, X{}, bounds, ctl + C_BOUNDS);
         HPXHIP_CHECK_LAUNCH();
         if (!HAS_VAL && mode == 18 && pre18) {  // the padded pass's bounds: a scan of its slot counts
-            hipLaunchKernelGGL(k_pad_bounds, dim3(1), dim3(1024), 0, s, reinterpret_cast<const uint32_t*>(base + L.lb),
-                               ctl + C_BOUNDS, ctl + C_PAD, bounds);
+            const auto* pcnt = reinterpret_cast<const uint32_t*>(base + L.lb);
+            auto* bsum = reinterpret_cast<uint64_t*>(base + L.lb + 4ull * kMaxBuckets);  // lb_bytes > 4 x 2^18 + 2 KiB
+            const dim3 grid(kMaxBuckets / 1024);  // blocks past the plan's buckets leave
+            hipLaunchKernelGGL(k_pad_sums, grid, dim3(256), 0, s, pcnt, ctl + C_BOUNDS, ctl + C_PAD, bsum);
+            HPXHIP_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_pad_bounds, grid, dim3(256), 0, s, pcnt, ctl + C_BOUNDS, ctl + C_PAD,
+                               static_cast<const uint64_t*>(bsum), bounds);
             HPXHIP_CHECK_LAUNCH();
         }
         auto* oversized = reinterpret_cast<uint32_t*>(ctl + C_OVERSIZED);

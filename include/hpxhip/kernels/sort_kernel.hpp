@@ -984,6 +984,9 @@ __device__ __forceinline__ uint32_t bucket_of(U k, int s1, int s2, int b2, X xf,
     return (static_cast<uint32_t>(u >> s1) & tmask) << b2 | (static_cast<uint32_t>(u >> s2) & ((1u << b2) - 1u));
 }
 
+#ifndef HPXHIP_PAD_ABL
+#define HPXHIP_PAD_ABL 0
+#endif
 // ---------------------------------------------- padded second pass (r06)
 // The 18-bit form's second prefix pass without a look-back.  Its input is
 // ordered by the field (the first pass), and what it must produce is every
@@ -1110,8 +1113,12 @@ __global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict_
             const uint32_t lb = 2 * t + h;
             if (cs[h]) {
                 const uint32_t bucket = ((lb & 511u) << b2) | (fb0 + (lb >> 9));
+#if HPXHIP_PAD_ABL  // ablation (timing only, wrong output): no atomics, a spread of fixed claims
+                const uint32_t base = (tile * 16u) % (cap - 64u);
+#else
                 const uint32_t base = __hip_atomic_fetch_add(&pcnt[bucket], cs[h], __ATOMIC_RELAXED,
                                                              __HIP_MEMORY_SCOPE_AGENT);
+#endif
                 if (base + cs[h] <= cap) {
                     s_adj[lb] = bucket * cap + base - ls[h];  // mod 2^32: pad index of local position ls
                 } else {
@@ -1154,44 +1161,60 @@ __global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict_
 }
 
 // off[v] = sum of the slot counts of buckets < v (v = 0..nb): the bucket
-// bounds of the padded pass, one workgroup; runs iff *g_cap > 0 (the padded
-// pass ran and no slot overflowed).  g_bounds = {on, nb, ...}.
-__global__ __launch_bounds__(1024) void k_pad_bounds(const uint32_t* __restrict__ pcnt,
-                                                      const int32_t* __restrict__ g_bounds,
-                                                      const int32_t* __restrict__ g_cap, uint64_t* __restrict__ off) {
+// bounds of the padded pass, in two launches over blocks of 1024 buckets
+// (k_pad_sums: each block's total into bsum; k_pad_bounds: each block adds
+// the totals before it and scans its own); run iff *g_cap > 0 (the padded
+// pass ran and no slot overflowed).  g_bounds = {on, nb, ...}; nb is a power
+// of two >= 1024.  (A one-workgroup scan walking 256 buckets per thread took
+// 0.21 ms, profiles/r06_sort_kernel_stats_u64_d.csv.)
+__global__ __launch_bounds__(256) void k_pad_sums(const uint32_t* __restrict__ pcnt,
+                                                   const int32_t* __restrict__ g_bounds,
+                                                   const int32_t* __restrict__ g_cap, uint64_t* __restrict__ bsum) {
     if (*g_cap <= 0) return;
     const uint32_t nb = static_cast<uint32_t>(g_bounds[1]);
-    const int t = threadIdx.x;
-    const int lane = lane_id(), wave = t / kWave;
-    __shared__ uint64_t s_w[1024 / kWave];
-    // thread t: buckets [t * per, (t + 1) * per), read as 16-B vectors (nb is
-    // a power of two >= 1024, so every range is whole vectors)
-    const uint32_t per = ((nb + 1023) / 1024 + 3) & ~3u;
-    const uint32_t lo = t * per < nb ? t * per : nb, hi = lo + per < nb ? lo + per : nb;
-    const uint4* p4 = reinterpret_cast<const uint4*>(pcnt + lo);
-    const uint32_t n4 = (hi - lo) / 4;
-    uint64_t sum = 0;
-#pragma unroll 8
-    for (uint32_t q = 0; q < n4; ++q) {
-        const uint4 c = p4[q];
-        sum += static_cast<uint64_t>(c.x) + c.y + c.z + c.w;
+    if (blockIdx.x * 1024u >= nb) return;
+    __shared__ uint64_t s_w[4];
+    const uint4 c = reinterpret_cast<const uint4*>(pcnt)[blockIdx.x * 256u + threadIdx.x];
+    const uint64_t x = wave_reduce(static_cast<uint64_t>(c.x) + c.y + c.z + c.w, op_plus{});
+    if (lane_id() == 0) s_w[threadIdx.x / kWave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) bsum[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+__global__ __launch_bounds__(256) void k_pad_bounds(const uint32_t* __restrict__ pcnt,
+                                                     const int32_t* __restrict__ g_bounds,
+                                                     const int32_t* __restrict__ g_cap,
+                                                     const uint64_t* __restrict__ bsum, uint64_t* __restrict__ off) {
+    if (*g_cap <= 0) return;
+    const uint32_t nb = static_cast<uint32_t>(g_bounds[1]);
+    const uint32_t b = blockIdx.x;
+    if (b * 1024u >= nb) return;
+    const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
+    __shared__ uint64_t s_w[4];
+    __shared__ uint64_t s_base;
+    if (wave == 0) {  // the totals of the blocks before this one (<= 256: four per lane)
+        uint64_t x = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t j = static_cast<uint32_t>(lane) * 4u + i;
+            if (j < b) x += bsum[j];
+        }
+        x = wave_reduce(x, op_plus{});
+        if (lane == 0) s_base = x;
     }
+    const uint4 c = reinterpret_cast<const uint4*>(pcnt)[b * 256u + t];
+    const uint64_t sum = static_cast<uint64_t>(c.x) + c.y + c.z + c.w;
     const uint64_t incl = wave_inclusive_scan(sum, op_plus{});
     if (lane == kWave - 1) s_w[wave] = incl;
     __syncthreads();
-    uint64_t run = incl - sum;
-    for (int w = 0; w < wave; ++w) run += s_w[w];
-#pragma unroll 4
-    for (uint32_t q = 0; q < n4; ++q) {
-        const uint4 c = p4[q];
-        const uint32_t v = lo + 4 * q;
-        off[v] = run;
-        off[v + 1] = run + c.x;
-        off[v + 2] = run + c.x + c.y;
-        off[v + 3] = run + c.x + c.y + c.z;
-        run += static_cast<uint64_t>(c.x) + c.y + c.z + c.w;
-    }
-    if (t == 1023) off[nb] = run;
+    uint64_t run = s_base + incl - sum;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+        if (w < wave) run += s_w[w];
+    const uint32_t v = b * 1024u + 4u * t;
+    using V2 = vec<uint64_t, 2>;
+    reinterpret_cast<V2*>(off + v)[0] = V2{{run, run + c.x}};
+    reinterpret_cast<V2*>(off + v)[1] = V2{{run + c.x + c.y, run + c.x + c.y + c.z}};
+    if (v + 4 == nb) off[nb] = run + sum;
 }
 
 // off[v] = first index whose prefix is >= v (v = 0..nb): a lower_bound per

@@ -94,4 +94,45 @@ lease_d() {
     python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d"; fi
+lease_e() {
+  # round 6, lease e: why the padded pass is 4.7 ms against 3.9 for the offset-fed first pass -- kernel
+  # trace of the no-atomics ablation (padabl: fixed claims, wrong output, timing only), and PMC passes
+  # (FETCH_SIZE, WRITE_SIZE, SQ group) over the shipped u64 sort
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6e
+  HPXHIP_LIB=scripts/ubench/seglib/padabl/libhpxhip.so SORT_ONLY=u64 timeout -k 10 200 rocprofv3 --kernel-trace \
+    --stats -d gpurun_out/r6e_prof_abl -o run -- python3 -u scripts/sort_probe.py 30 > ${L}_abl.log 2>&1 || exit $?
+  i=0
+  for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"; do
+    i=$((i+1))
+    SORT_ONLY=u64 timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d gpurun_out/r6e_pmc_sort$i -o run -- \
+      python3 scripts/sort_probe.py 30 > gpurun_out/r6e_pmc_sort$i.log 2>&1 || exit 1
+  done
+  python3 scripts/pmc_summary.py gpurun_out/r6e_pmc_sort1 gpurun_out/r6e_pmc_sort2 gpurun_out/r6e_pmc_sort3 \
+    > gpurun_out/r6e_pmc_sort.txt 2>&1
+}
+
+lease_f() {
+  # round 6, lease f: padded pass with the two-launch bounds scan: sort tests, A/B against pad0, kernel
+  # trace; the C++ drop-in bench program alone; then bench.py (its cxx_drop_in row included)
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6f
+  timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sort_hybrid.py \
+    tests/test_gpu_fullsize.py -k "sort" > ${L}_tests.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for lib in hpx_amd/libhpxhip.so scripts/ubench/seglib/pad0/libhpxhip.so; do
+      for c in u64 u32; do
+        echo "== $lib $c rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 30 >> ${L}_ab.log 2>&1 || exit $?
+      done
+    done
+  done
+  SORT_ONLY=u64 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6f_prof_u64 -o run -- \
+    python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
+  timeout -k 10 300 ./tests/cxx/bin/bench_targets --targets 4 --logn 28 --heat-logn 26 > ${L}_cxx.log 2>&1 || exit $?
+  timeout -k 10 900 python -u bench.py > ${L}_bench.log 2>&1 || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f"; fi
