@@ -69,8 +69,8 @@ struct tile_shape {
     static constexpr int tile = threads * items;
 };
 
-// k_hist_tiles' grid: two workgroups per CU, at most this many
-constexpr uint64_t kHistTilesMaxWG = 1024;
+// tiles per chunk of the per-tile offset scan (k_chunk_sums, k_tile_offsets)
+constexpr uint64_t kTileChunk = 256;
 
 struct sort_layout {
     uint64_t ntiles;
@@ -128,9 +128,7 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     // the first prefix pass, and the chunk totals (k_hist_tiles); reserved
     // only when the sort takes that pass (2 KiB per 8192-key tile)
     const bool pre = takes_pre18(n, vsize, tile);
-    // r06: csum holds k_hist_tiles' per-workgroup totals -> bases (one row per
-    // workgroup of its grid, at most kHistTilesMaxWG)
-    L.nchunks = pre ? std::min<uint64_t>(L.ntiles, kHistTilesMaxWG) : 0;
+    L.nchunks = pre ? (L.ntiles + kTileChunk - 1) / kTileChunk : 0;
     L.tcount = off;
     off = align_up(off + (pre ? L.ntiles * kXBins * 4 : 0), 256);
     L.csum = off;
@@ -625,11 +623,6 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     // running every pass persistent instead cost far more (26.3 ms: the
     // segment sort and the prefix passes lose the dispatcher's overlap of a
     // leaving workgroup with a starting one; profiles/r03_sort_probe_persistent.log).
-    // r06: k_hist_tiles' grid (two workgroups per CU) and its per-workgroup
-    // totals -> bases (csum), which the offset-fed first pass adds
-    const uint32_t hist_wg = static_cast<uint32_t>(
-        std::min<uint64_t>(std::min<uint64_t>(L.ntiles, 2ull * current_device_info().cus), kHistTilesMaxWG));
-    auto* csum = reinterpret_cast<uint32_t*>(base + L.csum);
     auto pass = [&](const U* kin, U* kout, const VAL* vin, VAL* vout, int rb, const int32_t* word,
                     bool persist, const unsigned long long* bs9 = nullptr, const uint32_t* pre = nullptr) -> int {
         const unsigned long long* b9 = bs9 ? bs9 : xstart;  // a 9-bit pass's bin starts
@@ -675,9 +668,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                 hipLaunchKernelGGL((k_onesweep<U, VAL, false, uint32_t, X, TS::threads, TS::items, -1, 9, true, false,
                                                false, false, true>),
                                    grid, block, 0, s, kin, kout, vin, vout, n, 0, b9,
-                                   reinterpret_cast<uint32_t*>(base + L.lb), counter, err, X{}, word, nt, pre,
-                                   static_cast<const seg_table*>(nullptr), static_cast<const unsigned long long*>(nullptr),
-                                   static_cast<const uint32_t*>(csum), hist_wg);
+                                   reinterpret_cast<uint32_t*>(base + L.lb), counter, err, X{}, word, nt, pre);
         } else if (rb == 9) {
             if constexpr (!HAS_VAL) {
                 if (L.wide) launch((unsigned long long)0, R9{});
@@ -701,12 +692,14 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     // -> 17.58-17.68 ms, u32 13.17-13.26 -> 12.55-12.62 against the look-back pass)
     const bool pre18 = takes_pre18(n, HAS_VAL ? sizeof(VAL) : 0, TS::tile);
     auto* tcount = reinterpret_cast<uint32_t*>(base + L.tcount);
-    // (r05: tiles strided over 2 workgroups per CU; r06: each workgroup
-    // leaves its tiles' running prefixes and its totals, csum)
+    auto* csum = reinterpret_cast<uint32_t*>(base + L.csum);
+    // (r05: tiles strided over 2 workgroups per CU; the chunk totals for the
+    // offsets come from k_chunk_sums)
     if (pre18)
-        hipLaunchKernelGGL((k_hist_tiles<U, X, 8192, kXBins>), dim3(hist_wg), dim3(kXBins), 0, s, kc, n, L.ntiles,
-                           X{}, field18_shift<U>(), top9_shift<U>(), tcount, xhist, thist, bits,
-                           reinterpret_cast<unsigned long long*>(base + L.joint), csum);
+        hipLaunchKernelGGL((k_hist_tiles<U, X, 8192, kXBins>),
+                           dim3(static_cast<unsigned>(std::min<uint64_t>(L.ntiles, 2ull * current_device_info().cus))),
+                           dim3(kXBins), 0, s, kc, n, L.ntiles, X{}, field18_shift<U>(), top9_shift<U>(), tcount, xhist,
+                           thist, bits, reinterpret_cast<unsigned long long*>(base + L.joint));
     else if (mode == 18)  // the field and the top 9 bits; no byte digit
         hipLaunchKernelGGL((k_hist<U, X, kHistThreads, 4, 2, true>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n,
                            first, passes, X{}, hist, bits, field18_shift<U>(), xhist,
@@ -748,12 +741,14 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
 
     // ---- hybrid: prefix passes (keys -> alt -> keys), bucket bounds, per-bucket LDS sort
     if (mode) {
-        if (pre18) {  // the first prefix pass's workgroup bases, iff the plan takes it
-            // (r06: the pass adds them to k_hist_tiles' running prefixes; the
-            // per-tile offset scan -- k_chunk_sums + k_tile_offsets, 0.14 ms
-            // at 2^30 -- is gone)
-            hipLaunchKernelGGL(k_tile_chunk_scan, dim3(1), dim3(kXBins), 0, s, csum, static_cast<uint64_t>(hist_wg),
-                               xstart, ctl + C_A9);
+        if (pre18) {  // the first prefix pass's tile offsets, iff the plan takes it
+            hipLaunchKernelGGL(k_chunk_sums, dim3(static_cast<unsigned>(L.nchunks)), dim3(kXBins), 0, s, tcount,
+                               L.ntiles, static_cast<uint32_t>(kTileChunk), csum, ctl + C_A9);
+            HPXHIP_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_tile_chunk_scan, dim3(1), dim3(kXBins), 0, s, csum, L.nchunks, xstart, ctl + C_A9);
+            HPXHIP_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_tile_offsets, dim3(static_cast<unsigned>(L.nchunks)), dim3(kXBins), 0, s, tcount,
+                               L.ntiles, static_cast<uint32_t>(kTileChunk), csum, ctl + C_A9);
             HPXHIP_CHECK_LAUNCH();
         }
         if (!HAS_VAL && (mode == 17 || mode == 18) &&

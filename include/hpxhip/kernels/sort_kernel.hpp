@@ -235,8 +235,7 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
                                                          unsigned long long* __restrict__ xhist,
                                                          unsigned long long* __restrict__ thist,
                                                          unsigned long long* __restrict__ bits,
-                                                         unsigned long long* __restrict__ joint,
-                                                         uint32_t* __restrict__ wtot) {
+                                                         unsigned long long* __restrict__ joint) {
     static_assert(THREADS == kXBins, "one thread per field digit");
     constexpr int V = 16 / static_cast<int>(sizeof(U));
     constexpr int VPT = TILE / V / THREADS;  // 16-B vectors per thread per tile
@@ -347,12 +346,8 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
         cc0 = cc1 = ~0u;
         cn0 = cn1 = 0;
         __syncthreads();  // the tile's counts are complete; the other array was flushed a tile ago
-        // r06: the workgroup's running prefix, not the tile's count: the
-        // first pass takes its tiles workgroup by workgroup (wg_tile), so a
-        // tile's offset is its workgroup's base (wtot, scanned by
-        // k_tile_chunk_scan) + this prefix -- no per-tile scan kernels
         const uint32_t c = ct[d];
-        tcount[t * kXBins + d] = csum_d;
+        tcount[t * kXBins + d] = c;
         csum_d += c;
         ct[d] = 0;  // counted into again two tiles on, after the next barrier
         buf ^= 1;
@@ -362,7 +357,6 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
         }
     }
     if (csum_d) atomicAdd(&xhist[d], static_cast<unsigned long long>(csum_d));
-    wtot[static_cast<uint64_t>(blockIdx.x) * kXBins + d] = csum_d;
     uint32_t tc = 0;
 #pragma unroll
     for (int x = 0; x < 8; ++x) {
@@ -575,27 +569,6 @@ __global__ __launch_bounds__(256) void k_seg_copy(const E* __restrict__ src, E* 
     }
 }
 
-// r06: the first prefix pass's tile order.  k_hist_tiles' workgroup w (of
-// G) counts the input tiles w, w + G, w + 2G, ...; the pass writes every
-// field bin's keys workgroup by workgroup -- order index o = (tiles of the
-// workgroups before w) + j for tile w + jG -- which no later step relies on
-// (the second pass only needs each field bin contiguous).  Input tile of
-// order index o (ntiles tiles; the first ntiles % G workgroups count one
-// tile more).
-__device__ __forceinline__ uint64_t wg_tile(uint64_t o, uint64_t ntiles, uint32_t g) {
-    const uint64_t j0 = ntiles / g, r = ntiles % g;
-    const uint64_t big = r * (j0 + 1);
-    uint64_t w, j;
-    if (o < big) {
-        w = o / (j0 + 1);
-        j = o % (j0 + 1);
-    } else {
-        w = r + (o - big) / j0;
-        j = (o - big) % j0;
-    }
-    return w + j * g;
-}
-
 // ----------------------------------------------------------------- onesweep
 // One 8-bit LSD pass over TILE = THREADS*ITEMS keys per workgroup; the whole
 // tile is counting-sorted in LDS and written out coalesced.
@@ -642,9 +615,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
                                                        const int32_t* __restrict__ ctl = nullptr, uint64_t ntiles = 0,
                                                        const uint32_t* __restrict__ pre = nullptr,
                                                        const seg_table* __restrict__ segs = nullptr,
-                                                       const unsigned long long* __restrict__ prev_starts = nullptr,
-                                                       const uint32_t* __restrict__ pre_base = nullptr,
-                                                       uint32_t pre_g = 0) {
+                                                       const unsigned long long* __restrict__ prev_starts = nullptr) {
     static_assert(!PERSIST || STAGE, "the persistent form keeps the LDS-staged write-out");
     static_assert(!SEG || ((PERSIST || XREG) && LBB > 0), "segmented passes: look-back passes, persistent or XREG");
     static_assert(!XREG || !PERSIST, "XCD regions: one tile per block");
@@ -730,8 +701,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             if (cnt == 0) continue;
             const uint32_t c = __hip_atomic_fetch_add(counter + 8 * xr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (c < cnt) {
-                // the offset-fed pass with workgroup bases: order index -> input tile
-                tl = static_cast<uint32_t>((!SEG && pre_g) ? wg_tile(lo + c, ntiles, pre_g) : lo + c);
+                tl = static_cast<uint32_t>(lo + c);
                 sg = xr;
             }
         }
@@ -945,10 +915,8 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
             __hip_atomic_store(&my[t], enc_incl<G>(excl + tile_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         s_adj[t] = static_cast<uint64_t>(bstart[t]) + excl - (STAGE ? s_local[t] : 0u);
-        if constexpr (LBB < 0) {  // PRE: the tile's destination offsets, precomputed (k_hist_tiles)
-            const uint32_t wb = pre_g ? pre_base[(tile % pre_g) * R + t] : 0u;  // r06: + its workgroup's base
-            s_adj[t] = static_cast<uint64_t>(pre[tile * R + t]) + wb - (STAGE ? s_local[t] : 0u);
-        }
+        if constexpr (LBB < 0)  // PRE: the tile's destination offsets, precomputed (k_tile_offsets)
+            s_adj[t] = static_cast<uint64_t>(pre[tile * R + t]) - (STAGE ? s_local[t] : 0u);
     }
     __syncthreads();
     if constexpr (!STAGE) {

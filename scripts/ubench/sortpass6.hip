@@ -1,4 +1,3 @@
-// (r06: k_hist_tiles now leaves per-workgroup running prefixes + totals; build this against commit 3ccc1cc)
 // Microbenchmark (round 5): the 18-bit sort's SECOND prefix pass (the top 9
 // bits of 2^30 random u64 keys, over the first pass's field-ordered output)
 // as shipped in r05 -- 8 field regions, one per XCD (k_onesweep XREG + SEG),

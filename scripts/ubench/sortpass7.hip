@@ -1,4 +1,3 @@
-// (r06: k_hist_tiles now leaves per-workgroup running prefixes + totals; build this against commit 3ccc1cc)
 // Microbenchmark (round 6): both prefix passes of the 18-bit sort at 2^30
 // random u64 keys with 8192-key tiles (512 x 16, shipped: two workgroups per
 // CU by LDS) against 4096-key tiles (512 x 8: ~45 KiB of LDS, three per CU),
