@@ -138,8 +138,12 @@ int hpx_main(int, char**) {
         heat_ms = (now_s() - s) * 1e3;
         // the ramp's sum is conserved by the periodic update up to rounding
         const std::vector<double> u = hs.to_host();
-        double sum = 0;
-        for (double v : u) sum += v;
+        double sum = 0, comp = 0;  // compensated: 2^28 plain additions alone drift by ~1e-8
+        for (double v : u) {
+            const double y = v - comp, t = sum + y;
+            comp = (t - sum) - y;
+            sum = t;
+        }
         const double want = 0.5 * double(nx) * double(nx - 1);
         heat_ok = std::fabs(sum - want) <= 1e-9 * want;
     }
