@@ -135,4 +135,30 @@ lease_f() {
   timeout -k 10 900 python -u bench.py > ${L}_bench.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f"; fi
+lease_g() {
+  # round 6, lease g: counters behind two claims.
+  # 1. triad placement: six fresh processes of scripts/ubench/triad_place (each its own placement), each
+  #    under two PMC passes (TCC_EA0_RDREQ, TCC_EA0_WRREQ) with the rocpd output (per-instance rows kept);
+  # 2. the fused stencil's VALU load: SQ VALU counters over scripts/stencil_probe.py 30.
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6g
+  timeout -s KILL 60 rocprofv3 -L > ${L}_counters.txt 2>&1 || true
+  for i in 1 2 3 4 5 6; do
+    timeout -k 10 60 ./scripts/ubench/triad_place 30 >> ${L}_triad_plain.log 2>&1 || exit $?
+  done
+  for i in 1 2 3; do
+    for pmc in TCC_EA0_RDREQ TCC_EA0_WRREQ; do
+      echo "== run $i $pmc" >> ${L}_triad_pmc.log
+      timeout -s KILL 120 rocprofv3 --pmc $pmc -d gpurun_out/r6g_triad_${i}_${pmc} -o run -- \
+        ./scripts/ubench/triad_place 30 >> ${L}_triad_pmc.log 2>&1 || exit 1
+    done
+  done
+  timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
+    SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 --output-format csv -d gpurun_out/r6g_heat_sq \
+    -o run -- python3 scripts/stencil_probe.py 30 > ${L}_heat_sq.log 2>&1 || exit 1
+  timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/r6g_heat_fetch -o run -- \
+    python3 scripts/stencil_probe.py 30 > ${L}_heat_fetch.log 2>&1 || exit 1
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g"; fi
