@@ -161,4 +161,19 @@ lease_g() {
     python3 scripts/stencil_probe.py 30 > ${L}_heat_fetch.log 2>&1 || exit 1
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g"; fi
+lease_h() {
+  # round 6, lease h: triad placement below the L2 (lease g: the L2 channels get exactly equal request
+  # counts in fast and slow runs) -- eight fresh processes of scripts/ubench/triad_place, each under one
+  # PMC pass of the fabric-side queue levels and DRAM credit stalls (per instance in the rocpd database)
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6h
+  for i in 1 2 3 4 5 6 7 8; do
+    echo "== run $i" >> ${L}_triad_pmc.log
+    timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_LEVEL TCC_EA0_WRREQ_LEVEL TCC_EA0_RDREQ_DRAM_CREDIT_STALL \
+      TCC_EA0_WRREQ_DRAM_CREDIT_STALL -d gpurun_out/r6h_triad_$i -o run -- ./scripts/ubench/triad_place 30 \
+      >> ${L}_triad_pmc.log 2>&1 || exit 1
+  done
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h"; fi
