@@ -80,6 +80,10 @@ struct sort_layout {
 };
 
 bool takes_pre18(uint64_t n, size_t vsize, int tile);
+// r06: sort_by_key may plan 512 x 9 pair segments (k_bucket_sort C_SEGD); 0: A/B builds
+#ifndef HPXHIP_SORT_KV512
+#define HPXHIP_SORT_KV512 1
+#endif
 // r06: the padded second pass (k_pad_scatter); 0: the look-back pass (A/B builds)
 #ifndef HPXHIP_SORT_PAD
 #define HPXHIP_SORT_PAD 1
@@ -182,6 +186,11 @@ constexpr uint64_t kCap17 = static_cast<uint64_t>(kSegThreads17) * kSegItems;
 // workgroup per CU).
 constexpr int kSegItemsKV = 9;
 constexpr uint64_t kCapKV = static_cast<uint64_t>(kSegThreads16) * kSegItemsKV;
+// r06: pairs in 512 x 9 segments (72 KiB of keys and 8-B values: two
+// workgroups per CU, so one's loads and stores overlap the other's LDS
+// passes; the 1024 x 9 segment holds 144 KiB and runs alone on its CU),
+// planned when the buckets fit -- e.g. 2^28 pairs with 2^16 buckets
+constexpr uint64_t kCapKV2 = static_cast<uint64_t>(kSegThreads17) * kSegItemsKV;
 // 18-bit form (keys, HPXHIP_SORT_HYBRID=18): two 9-bit prefix passes (the
 // field [P-18, P-9), then the top 9 bits) and ~4096-key buckets sorted by
 // 512 x 9 workgroups, three per CU (2^30 u64: 5.26 ms against 6.43-6.59 for
@@ -252,7 +261,8 @@ enum : int {
     C_PAD = 47,        // r06: slot capacity of the padded second pass (k_pad_scatter), 0 = not taken
     C_B9P = 48,        // ... its top-9 shift, -1 = not run
     C_PADOVF = 49,     // ... raised when a slot overflowed (the look-back pass runs instead)
-    C_WORDS = 50
+    C_SEGD = 50,       // r06: {on, nb, top_single}: 512 x 9 pairs segment sort (sort_by_key, buckets <= 4608)
+    C_WORDS = 53
 };
 static_assert(C_WORDS * 4 <= 256, "plan words fit their slot");
 
@@ -463,6 +473,13 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
         }
         const double m_top = bin_max(hist + live[0] * kRadix, kRadix, 1);
         const unsigned long long* h2 = hist + live[1] * kRadix;
+        if (has_val && HPXHIP_SORT_KV512)
+            for (int b2 = 1; b2 <= 8; ++b2)
+                if (fits(m_top * bin_max(h2, kRadix, 1 << (8 - b2)) / dn, kCapKV2)) {
+                    ctl[C_A8] = 8 * live[1];
+                    ctl[C_B] = 8 * live[0];
+                    return plan(8 * live[0], 8 * live[1] + 8 - b2, b2, C_SEGD);
+                }
         for (int b2 = 1; b2 <= 8; ++b2)
             if (fits(m_top * bin_max(h2, kRadix, 1 << (8 - b2)) / dn, has_val ? kCapKV : kCap17)) {
                 ctl[C_A8] = 8 * live[1];
@@ -844,6 +861,19 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                 hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads16, kSegItemsKV, 16, VAL, true, true, true>),
                                    dim3(cus), dim3(kSegThreads16), 0, s, kc, bounds, 0, X{}, vc, oversized,
                                    ctl + C_SEGA, g0, big);
+            HPXHIP_CHECK_LAUNCH();
+            // r06: the 512 x 9 pairs segments (C_SEGD): one workgroup per
+            // expected bucket, then a striding grid over the rest
+            constexpr uint64_t kMax16 = uint64_t(1) << 16;
+            const uint64_t wantd = 2 * (n / 4096 + 1);
+            const uint32_t gd = static_cast<uint32_t>(wantd > kMax16 ? kMax16 : wantd);
+            hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItemsKV, 16, VAL, true, true>), dim3(gd),
+                               dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, vc, oversized, ctl + C_SEGD, 0u, big);
+            HPXHIP_CHECK_LAUNCH();
+            if (gd < kMax16)
+                hipLaunchKernelGGL((k_bucket_sort<U, X, kSegThreads17, kSegItemsKV, 16, VAL, true, true, true>),
+                                   dim3(2 * cus), dim3(kSegThreads17), 0, s, kc, bounds, 0, X{}, vc, oversized,
+                                   ctl + C_SEGD, gd, big);
         } else if (mode == 18) {
             // the 18-bit form's ~4096-key buckets: one workgroup per expected
             // bucket, then a striding grid; the 512 x 18 segment (a plan that

@@ -176,4 +176,23 @@ lease_h() {
   done
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h"; fi
+lease_i() {
+  # round 6, lease i: sort_by_key in 512 x 9 pair segments (C_SEGD, two workgroups per CU) when the buckets
+  # fit: the sort tests (all pairs cases in every hybrid form, parity, 2^30 element-exact), then A/B against
+  # kv0 (the 1024 x 9 segments only), 2^28 pairs, and a kernel trace
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6i
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sort_hybrid.py \
+    tests/test_gpu_parity.py tests/test_gpu_fullsize.py -k "sort" > ${L}_tests.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for lib in hpx_amd/libhpxhip.so scripts/ubench/seglib/kv0/libhpxhip.so; do
+      echo "== $lib pairs rep $rep" >> ${L}_ab.log
+      HPXHIP_LIB=$lib SORT_ONLY=pairs timeout -k 10 200 python -u scripts/sort_probe.py 28 >> ${L}_ab.log 2>&1 || exit $?
+    done
+  done
+  SORT_ONLY=pairs timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6i_prof_pairs -o run -- \
+    python3 -u scripts/sort_probe.py 28 > ${L}_prof.log 2>&1 || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i"; fi
