@@ -300,7 +300,8 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
                             const unsigned long long* __restrict__ thist,
                             const unsigned long long* __restrict__ bits, uint64_t n, int passes, int first, int mode,
                             int has_val, int stage, int32_t* __restrict__ ctl, seg_table* __restrict__ segs = nullptr,
-                            uint32_t* __restrict__ big = nullptr, int tile = 0, uint64_t pad_keys = 0) {
+                            uint32_t* __restrict__ big = nullptr, int tile = 0, uint64_t pad_keys = 0,
+                            const unsigned long long* __restrict__ joint = nullptr) {
     if (blockIdx.x != 0) return;
     // 18-bit form: the statistics of the two 9-bit histograms, by the 64
     // threads of the launch (r05; one thread reading 9 x 512 bins took ~0.1
@@ -308,6 +309,7 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
     // group of 2^(9-b2) field bins (all, and those without a hot bin); the
     // hot bins (over twice the mean) of both and their excess keys
     __shared__ double s_mtop, s_mt, s_et, s_ef, s_mg[10], s_mgn[10];
+    __shared__ int s_jover[10];
     __shared__ int s_ht, s_hf;
     // r06: the field histogram staged in LDS first -- the group sums below
     // had walked it in global memory, one dependent load after another (the
@@ -357,9 +359,40 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
                 mgn[b2] = mx(mgn[b2], __shfl_xor(mgn[b2], o));
             }
         }
+        // r06: the joint (field region x top-9) histogram bounds the buckets
+        // from below, which the marginals cannot: per field width b2, the
+        // cells that must hold a bucket over the segment -- b2 <= 3: a bucket
+        // is exactly (top-9 digit, 2^(3 - b2) regions), its size the joint
+        // sum; b2 > 3: a region's 2^(b2 - 3) buckets of one top-9 digit
+        // share joint[r][t], so one holds at least joint / 2^(b2 - 3).  A
+        // field correlated with the top bits (u64corr: every bucket oversized
+        // while the marginals are uniform) had run the prefix passes and the
+        // segment sorts for nothing before the whole-array LSD.
+        int jover[10];
+        for (int b2 = 1; b2 <= 9; ++b2) jover[b2] = 0;
+        if (joint) {
+            for (int tt = t; tt < kXBins; tt += 64) {
+                double j[8];
+                for (int r = 0; r < 8; ++r) j[r] = static_cast<double>(joint[r * kXBins + tt]);
+                for (int b2 = 1; b2 <= 9; ++b2) {
+                    if (b2 <= 3) {
+                        const int g = 1 << (3 - b2);
+                        for (int r0 = 0; r0 < 8; r0 += g) {
+                            double sum = 0;
+                            for (int r = r0; r < r0 + g; ++r) sum += j[r];
+                            jover[b2] += sum > static_cast<double>(kCap18);
+                        }
+                    } else {
+                        for (int r = 0; r < 8; ++r) jover[b2] += j[r] / static_cast<double>(1 << (b2 - 3)) > kCap18;
+                    }
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1)
+                for (int b2 = 1; b2 <= 9; ++b2) jover[b2] += __shfl_xor(jover[b2], o);
+        }
         if (t == 0) {
             s_mtop = mtop, s_mt = mt, s_et = et, s_ef = ef, s_ht = ht, s_hf = hf;
-            for (int b2 = 1; b2 <= 9; ++b2) s_mg[b2] = mg[b2], s_mgn[b2] = mgn[b2];
+            for (int b2 = 1; b2 <= 9; ++b2) s_mg[b2] = mg[b2], s_mgn[b2] = mgn[b2], s_jover[b2] = jover[b2];
         }
         __syncthreads();
     }
@@ -417,8 +450,15 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
     if (mode == 18 && !has_val && stage == 0 && top_two) {
         // top 9 bits [8P - 9, 8P), field [8P - 18, 8P - 9): b2 <= 9 bits of the field
         const int fs = 8 * passes - 18;
+        bool futile = false;
         for (int b2 = 1; b2 <= 9; ++b2) {
             const double est = s_mtop * s_mg[b2] / dn;
+            // (r06) more cells over the segment than the bounded finish keeps:
+            // a wider field, or no 18-bit plan
+            if (fits(est, kCap18) && s_jover[b2] > kMaxBig) {
+                futile = true;
+                continue;
+            }
             if (fits(est, kCap18)) {
                 ctl[C_A9] = fs;
                 // r06: the padded second pass when its slots -- the estimated
@@ -435,6 +475,7 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
                 return plan(8 * passes - 9, fs + 9 - b2, b2, C_SEGC, 9);
             }
         }
+        if (futile) return lsd();  // (r06) the marginals fit, the joint histogram does not
         // r05: skew concentrated in a few buckets -- a few hot top-9 bins
         // whose excess keys sit in a few hot field bins (the same keys: the
         // excess masses match) -- is left to the bounded finish of the
@@ -747,7 +788,8 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     auto* segs = mode ? reinterpret_cast<seg_table*>(base + L.segs) : nullptr;
     auto* big = mode ? reinterpret_cast<uint32_t*>(base + L.big) : nullptr;
     hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, thist, bits, n, passes, first, mode,
-                       HAS_VAL ? 1 : 0, 0, ctl, segs, big, TS::tile, static_cast<uint64_t>(HPXHIP_SORT_PAD ? L.pad_keys : 0));
+                       HAS_VAL ? 1 : 0, 0, ctl, segs, big, TS::tile, static_cast<uint64_t>(HPXHIP_SORT_PAD ? L.pad_keys : 0),
+                       pre18 ? reinterpret_cast<const unsigned long long*>(base + L.joint) : nullptr);
     HPXHIP_CHECK_LAUNCH();
     if (first > 0) {
         if ((rc = count_rest(ctl + C_HIST_A))) return rc;

@@ -178,7 +178,7 @@ lease_h() {
 
 lease_i() {
   # round 6, lease i: sort_by_key in 512 x 9 pair segments (C_SEGD, two workgroups per CU) when the buckets
-  # fit: the sort tests (all pairs cases in every hybrid form, parity, 2^30 element-exact), then A/B against
+  # fit, and the planner's joint-histogram check (u64corr: no futile prefix passes; kv0 predates both): the sort tests (all pairs cases in every hybrid form, parity, 2^30 element-exact), then A/B against
   # kv0 (the 1024 x 9 segments only), 2^28 pairs, and a kernel trace
   cd $GRAFT_REPO_ROOT
   export TMPDIR=/tmp
@@ -189,6 +189,10 @@ lease_i() {
     for lib in hpx_amd/libhpxhip.so scripts/ubench/seglib/kv0/libhpxhip.so; do
       echo "== $lib pairs rep $rep" >> ${L}_ab.log
       HPXHIP_LIB=$lib SORT_ONLY=pairs timeout -k 10 200 python -u scripts/sort_probe.py 28 >> ${L}_ab.log 2>&1 || exit $?
+      for c in u64 u64corr u64hot; do
+        echo "== $lib $c rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 28 >> ${L}_ab.log 2>&1 || exit $?
+      done
     done
   done
   SORT_ONLY=pairs timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6i_prof_pairs -o run -- \
