@@ -371,9 +371,15 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
         int jover[10];
         for (int b2 = 1; b2 <= 9; ++b2) jover[b2] = 0;
         if (joint) {
+            // staged in LDS first (as the field histogram): 64 independent
+            // loads per thread instead of eight dependent rounds
+            __shared__ float s_joint[8 * kXBins];
+#pragma unroll 16
+            for (int i = t; i < 8 * kXBins; i += 64) s_joint[i] = static_cast<float>(joint[i]);
+            __syncthreads();
             for (int tt = t; tt < kXBins; tt += 64) {
                 double j[8];
-                for (int r = 0; r < 8; ++r) j[r] = static_cast<double>(joint[r * kXBins + tt]);
+                for (int r = 0; r < 8; ++r) j[r] = static_cast<double>(s_joint[r * kXBins + tt]);
                 for (int b2 = 1; b2 <= 9; ++b2) {
                     if (b2 <= 3) {
                         const int g = 1 << (3 - b2);
