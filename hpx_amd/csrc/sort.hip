@@ -75,20 +75,11 @@ constexpr uint64_t kTileChunk = 256;
 struct sort_layout {
     uint64_t ntiles;
     size_t alt_keys, alt_vals, hist, xhist, thist, joint, bits, start, xstart, tstart, bounds, ctl, counter, lb,
-        lb_bytes, tcount, csum, nchunks, segs, big, shist, sstart, segs2, bs2, pad, pad_keys, opt, cap1, total;
+        lb_bytes, tcount, csum, nchunks, segs, big, shist, sstart, segs2, bs2, pad, pad_keys, total;
     bool wide;  // 64-bit granules
 };
 
 bool takes_pre18(uint64_t n, size_t vsize, int tile);
-// r06: the optimistic first pass (k_slot_pass1 + k_opt_plan); 0: A/B builds
-#ifndef HPXHIP_SORT_OPT
-#define HPXHIP_SORT_OPT 1
-#endif
-// its scratch: slot counts, sampled joint histogram, slot tile starts
-constexpr uint64_t kOptScnt = 0, kOptJoint = 4 * 512, kOptTile0 = kOptJoint + 8 * 8 * 512,
-                   kOptBytes = kOptTile0 + 8 * 513;
-// field slot capacity: 1.25 x the mean field bin + 8192 keys, whole 64-key lines
-uint64_t opt_slot_cap(uint64_t n, size_t vsize, int tile);
 // r06: sort_by_key may plan 512 x 9 pair segments (k_bucket_sort C_SEGD); 0: A/B builds
 #ifndef HPXHIP_SORT_KV512
 #define HPXHIP_SORT_KV512 1
@@ -107,9 +98,7 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     L.wide = n >= (1ull << 31);
     size_t off = 0;
     L.alt_keys = off;
-    // r06: the optimistic first pass writes its 512 field slots here
-    L.cap1 = opt_slot_cap(n, vsize, tile);
-    off = align_up(off + std::max<uint64_t>(n, kXBins * L.cap1) * ksize, 256);
+    off = align_up(off + n * ksize, 256);
     L.alt_vals = off;
     off = align_up(off + n * vsize, 256);
     L.hist = off;
@@ -171,10 +160,6 @@ sort_layout make_layout(uint64_t n, size_t ksize, size_t vsize, int tile) {
     L.pad_keys = pre ? std::min<uint64_t>(n + n / 4 + kPadSlotMax, static_cast<uint64_t>(kMaxBuckets) * kPadSlotMax) : 0;
     L.pad = off;
     off = align_up(off + L.pad_keys * ksize, 256);
-    // r06: the optimistic first pass's slot counts (512 u32), sampled joint
-    // histogram (8 x 512 u64) and the slots' tile starts (513 u64)
-    L.opt = off;
-    off = align_up(off + (pre ? kOptBytes : 0), 256);
     L.total = off;
     return L;
 }
@@ -244,10 +229,6 @@ int hybrid_mode() {
 bool takes_pre18(uint64_t n, size_t vsize, int tile) {
     return vsize == 0 && n >= kHybridMin && n < (uint64_t(1) << 32) && tile == 8192 && hybrid_mode() == 18;
 }
-uint64_t opt_slot_cap(uint64_t n, size_t vsize, int tile) {
-    if (!HPXHIP_SORT_OPT || !takes_pre18(n, vsize, tile)) return 0;
-    return (n / kXBins + n / (4 * kXBins) + 8192 + 63) & ~uint64_t(63);
-}
 
 // ---------------------------------------------------------------- the plan
 // The sort is planned ON THE DEVICE: the host enqueues one fixed sequence of
@@ -281,10 +262,7 @@ enum : int {
     C_B9P = 48,        // ... its top-9 shift, -1 = not run
     C_PADOVF = 49,     // ... raised when a slot overflowed (the look-back pass runs instead)
     C_SEGD = 50,       // r06: {on, nb, top_single}: 512 x 9 pairs segment sort (sort_by_key, buckets <= 4608)
-    C_OPT = 53,        // r06: 1 = the optimistic first pass took the sort (the full path is skipped)
-    C_B9S = 54,        // ... the padded second pass over its slots: top-9 shift, -1 = not run
-    C_OPTOVF = 55,     // ... a field slot overflowed
-    C_WORDS = 56
+    C_WORDS = 53
 };
 static_assert(C_WORDS * 4 <= 256, "plan words fit their slot");
 
@@ -323,10 +301,8 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
                             const unsigned long long* __restrict__ bits, uint64_t n, int passes, int first, int mode,
                             int has_val, int stage, int32_t* __restrict__ ctl, seg_table* __restrict__ segs = nullptr,
                             uint32_t* __restrict__ big = nullptr, int tile = 0, uint64_t pad_keys = 0,
-                            const unsigned long long* __restrict__ joint = nullptr,
-                            const int32_t* __restrict__ opt = nullptr) {
+                            const unsigned long long* __restrict__ joint = nullptr) {
     if (blockIdx.x != 0) return;
-    if (stage == 0 && opt && *opt == 1) return;  // (r06) the optimistic first pass took the sort
     // 18-bit form: the statistics of the two 9-bit histograms, by the 64
     // threads of the launch (r05; one thread reading 9 x 512 bins took ~0.1
     // ms per plan): the largest top-9 bin; per field width b2 the largest
@@ -566,132 +542,6 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
     lsd();
 }
 
-// r06: the planner after the optimistic first pass (k_slot_pass1).  From the
-// keys' OR / AND (exact), the field histogram (the slot counts, exact) and the
-// sampled joint (field region x top-9) histogram: the same 18-bit plan
-// k_sort_plan makes -- fewest field bits b2 whose estimated largest bucket
-// fits, no more cells over a segment than the bounded finish keeps (the
-// joint lower bound, taken at 80 % for the sampling) -- with the padded
-// second pass over the slots.  Sizes from the sample get 3 % more room.
-// Takes the sort (ctl[C_OPT] = 1, every word the later kernels read) or
-// leaves it to the full path (ctl[C_OPT] = 0: k_hist_tiles and k_sort_plan
-// run from the keys, which the optimistic pass only read).  One block of 64.
-__global__ void k_opt_plan(const uint32_t* __restrict__ scnt, const unsigned long long* __restrict__ jsamp,
-                           const unsigned long long* __restrict__ bits, uint64_t n, int passes,
-                           int32_t* __restrict__ ctl, uint32_t* __restrict__ big, uint64_t* __restrict__ slot_tile0,
-                           uint64_t pad_keys, int tile) {
-    const int t = threadIdx.x;
-    __shared__ double s_x[kXBins], s_tt[kXBins];
-    __shared__ float s_j[8 * kXBins];
-    __shared__ double s_mg[10];
-    __shared__ int s_jover[10];
-    __shared__ double s_scale, s_mtop;
-    for (int i = t; i < kXBins; i += 64) s_x[i] = static_cast<double>(scnt[i]);
-#pragma unroll 16
-    for (int i = t; i < 8 * kXBins; i += 64) s_j[i] = static_cast<float>(jsamp[i]);
-    __syncthreads();
-    double tot = 0, mtop = 0;
-    for (int i = t; i < kXBins; i += 64) {
-        double v = 0;
-        for (int r = 0; r < 8; ++r) v += s_j[r * kXBins + i];
-        s_tt[i] = v;
-        tot += v;
-        mtop = v > mtop ? v : mtop;
-    }
-    // the slots' tile starts: thread t sums slots [8t, 8t + 8)
-    uint64_t mine = 0;
-    for (int i = 0; i < 8; ++i) mine += (static_cast<uint64_t>(s_x[8 * t + i]) + tile - 1) / tile;
-    const uint64_t incl = wave_inclusive_scan(mine, op_plus{});
-    uint64_t run = incl - mine;
-    for (int i = 0; i < 8; ++i) {
-        slot_tile0[8 * t + i] = run;
-        run += (static_cast<uint64_t>(s_x[8 * t + i]) + tile - 1) / tile;
-    }
-    if (t == 63) slot_tile0[kXBins] = run;
-    for (int o = 32; o > 0; o >>= 1) {
-        tot += __shfl_xor(tot, o);
-        const double m = __shfl_xor(mtop, o);
-        mtop = m > mtop ? m : mtop;
-    }
-    const double scale = tot > 0 ? static_cast<double>(n) / tot : 0.0;
-    // per field width b2: largest field group (exact) and the joint cells over a segment
-    for (int b2 = 1 + t; b2 <= 9; b2 += 64) {
-        const int g = 1 << (9 - b2);
-        double mg = 0;
-        for (int i = 0; i < kXBins; i += g) {
-            double sum = 0;
-            for (int k = 0; k < g; ++k) sum += s_x[i + k];
-            mg = sum > mg ? sum : mg;
-        }
-        int over = 0;
-        for (int tt = 0; tt < kXBins; ++tt) {
-            if (b2 <= 3) {
-                const int gr = 1 << (3 - b2);
-                for (int r0 = 0; r0 < 8; r0 += gr) {
-                    double sum = 0;
-                    for (int r = r0; r < r0 + gr; ++r) sum += s_j[r * kXBins + tt];
-                    over += 0.8 * scale * sum > static_cast<double>(kCap18);
-                }
-            } else {
-                for (int r = 0; r < 8; ++r)
-                    over += 0.8 * scale * s_j[r * kXBins + tt] / static_cast<double>(1 << (b2 - 3)) > kCap18;
-            }
-        }
-        s_mg[b2] = mg;
-        s_jover[b2] = over;
-    }
-    if (t == 0) {
-        s_scale = scale;
-        s_mtop = mtop * scale;
-    }
-    __syncthreads();
-    if (t != 0) return;
-    const int32_t slot_ovf = ctl[C_OPTOVF];
-    for (int i = 0; i < C_WORDS; ++i) ctl[i] = 0;
-    for (int i = 0; i < 11; ++i) ctl[i] = -1;
-    ctl[C_B9] = -1;
-    ctl[C_B9P] = -1;
-    ctl[C_B9S] = -1;
-    ctl[C_FIRST] = passes;
-    if (big) big[0] = 0;
-    const uint64_t diff = bits[0] ^ bits[1];
-    int live[8], nl = 0;
-    for (int p = passes - 1; p >= 0; --p)
-        if ((diff >> (8 * p)) & 0xffu) live[nl++] = p;
-    ctl[C_NLSD] = nl;
-    for (int i = 0; i < nl; ++i) ctl[C_DIGITS + i] = live[nl - 1 - i];
-    if (slot_ovf || nl < 3 || live[0] != passes - 1 || live[1] != passes - 2 || s_scale <= 0) return;  // C_OPT = 0
-    const double dn = static_cast<double>(n);
-    const int fs = 8 * passes - 18, s1 = 8 * passes - 9;
-    for (int b2 = 1; b2 <= 9; ++b2) {
-        const double est = 1.03 * s_mtop * s_mg[b2] / dn;
-        if (!fits(est, kCap18) || s_jover[b2] > kMaxBig) continue;
-        const uint32_t nb = 512u << b2;
-        uint32_t cap = (static_cast<uint32_t>(est + 7.0 * sqrt(est) + 64.0) + 63u) & ~63u;
-        cap = cap < kCap18 ? cap : static_cast<uint32_t>(kCap18);
-        if (static_cast<uint64_t>(nb) * cap > pad_keys) return;
-        const int s2 = fs + 9 - b2;
-        ctl[C_OPT] = 1;
-        ctl[C_B9S] = s1;
-        ctl[C_PAD] = static_cast<int32_t>(cap);
-        ctl[C_BOUNDS + 0] = 0;  // bounds from the slot counts (k_pad_bounds), not by search
-        ctl[C_BOUNDS + 1] = static_cast<int32_t>(nb);
-        ctl[C_BOUNDS + 2] = s1;
-        ctl[C_BOUNDS + 3] = s2;
-        ctl[C_BOUNDS + 4] = b2;
-        ctl[C_SEGC + 0] = 1;
-        ctl[C_SEGC + 1] = static_cast<int32_t>(nb);
-        ctl[C_SEGC + 2] = top_bit_d(diff & ((uint64_t(1) << s2) - 1));
-        return;
-    }
-}
-
-// After the padded second pass over the optimistic slots: a slot that
-// overflowed hands the sort to the full path (from the keys).
-__global__ void k_opt_check(int32_t* __restrict__ ctl) {
-    if (threadIdx.x == 0 && blockIdx.x == 0 && ctl[C_OPT] == 1 && ctl[C_PADOVF]) ctl[C_OPT] = 0;
-}
-
 // After the segment sorts: buckets over their LDS capacity (skewed keys)
 // were left unsorted.  Up to kMaxBig of them (the whole-array
 // LSD for one oversized bucket cost 2.5-2.9x) are finished by a segmented
@@ -907,57 +757,13 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     const bool pre18 = takes_pre18(n, HAS_VAL ? sizeof(VAL) : 0, TS::tile);
     auto* tcount = reinterpret_cast<uint32_t*>(base + L.tcount);
     auto* csum = reinterpret_cast<uint32_t*>(base + L.csum);
-    // r06: the optimistic path (keys, 18-bit form): the first prefix pass
-    // into field slots without a histogram read in front (k_slot_pass1), its
-    // planner, the padded second pass over the slots and its overflow check;
-    // the full path below runs iff ctl[C_OPT] == 0 afterwards
-    const bool opt18 = !HAS_VAL && pre18 && mode == 18 && L.cap1 > 0;
-    int32_t* opt_gate = opt18 ? ctl + C_OPT : nullptr;
-    if constexpr (!HAS_VAL) {
-        if (opt18) {
-            char* ob = base + L.opt;
-            auto* scnt = reinterpret_cast<uint32_t*>(ob + kOptScnt);
-            auto* jsamp = reinterpret_cast<unsigned long long*>(ob + kOptJoint);
-            auto* tile0 = reinterpret_cast<uint64_t*>(ob + kOptTile0);
-            HPXHIP_CHECK(hipMemsetAsync(ob, 0, kOptTile0, s));  // slot counts, sampled joint
-            HPXHIP_CHECK(hipMemsetAsync(ctl + C_OPTOVF, 0, 4, s));
-            HPXHIP_CHECK(hipMemsetAsync(counter, 0, 256, s));
-            hipLaunchKernelGGL((k_slot_pass1<U, X, TS::threads, TS::items>), dim3(static_cast<unsigned>(L.ntiles)),
-                               dim3(TS::threads), 0, s, kc, ka, n, L.ntiles, X{}, field18_shift<U>(), top9_shift<U>(),
-                               static_cast<uint64_t>(L.cap1), scnt, bits, jsamp, ctl + C_OPTOVF, counter);
-            HPXHIP_CHECK_LAUNCH();
-            hipLaunchKernelGGL(k_opt_plan, dim3(1), dim3(64), 0, s, static_cast<const uint32_t*>(scnt),
-                               static_cast<const unsigned long long*>(jsamp),
-                               static_cast<const unsigned long long*>(bits), n, passes, ctl,
-                               reinterpret_cast<uint32_t*>(base + L.big), tile0,
-                               static_cast<uint64_t>(HPXHIP_SORT_PAD ? L.pad_keys : 0), TS::tile);
-            HPXHIP_CHECK_LAUNCH();
-            auto* pcnt = reinterpret_cast<uint32_t*>(base + L.lb);
-            const uint64_t pz = align_up(256 + 4ull * kMaxBuckets, 16);
-            hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(pz / 16, 2048)), dim3(256), 0, s,
-                               reinterpret_cast<uint4*>(counter), pz / 16, ctl + C_B9S);
-            HPXHIP_CHECK_LAUNCH();
-            // (a slot adds at most one partial tile)
-            const uint64_t nt2 = L.ntiles + kXBins + 8;
-            hipLaunchKernelGGL((k_pad_scatter<U, X, TS::threads, TS::items>), dim3(static_cast<unsigned>(nt2)),
-                               dim3(TS::threads), 0, s, static_cast<const U*>(ka), reinterpret_cast<U*>(base + L.pad),
-                               ctl + C_B9S, ctl + C_BOUNDS, ctl + C_PAD,
-                               reinterpret_cast<const seg_table*>(base + L.segs2), counter, pcnt, ctl + C_PADOVF, X{},
-                               static_cast<const uint64_t*>(tile0), static_cast<const uint32_t*>(scnt),
-                               static_cast<uint64_t>(L.cap1));
-            HPXHIP_CHECK_LAUNCH();
-            hipLaunchKernelGGL(k_opt_check, dim3(1), dim3(64), 0, s, ctl);
-            HPXHIP_CHECK_LAUNCH();
-        }
-    }
     // (r05: tiles strided over 2 workgroups per CU; the chunk totals for the
     // offsets come from k_chunk_sums)
     if (pre18)
         hipLaunchKernelGGL((k_hist_tiles<U, X, 8192, kXBins>),
                            dim3(static_cast<unsigned>(std::min<uint64_t>(L.ntiles, 2ull * current_device_info().cus))),
                            dim3(kXBins), 0, s, kc, n, L.ntiles, X{}, field18_shift<U>(), top9_shift<U>(), tcount, xhist,
-                           thist, bits, reinterpret_cast<unsigned long long*>(base + L.joint),
-                           static_cast<const int32_t*>(opt_gate));
+                           thist, bits, reinterpret_cast<unsigned long long*>(base + L.joint));
     else if (mode == 18)  // the field and the top 9 bits; no byte digit
         hipLaunchKernelGGL((k_hist<U, X, kHistThreads, 4, 2, true>), dim3(hist_grid), dim3(kHistThreads), 0, s, kc, n,
                            first, passes, X{}, hist, bits, field18_shift<U>(), xhist,
@@ -989,8 +795,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
     auto* big = mode ? reinterpret_cast<uint32_t*>(base + L.big) : nullptr;
     hipLaunchKernelGGL(k_sort_plan, dim3(1), dim3(64), 0, s, hist, xhist, thist, bits, n, passes, first, mode,
                        HAS_VAL ? 1 : 0, 0, ctl, segs, big, TS::tile, static_cast<uint64_t>(HPXHIP_SORT_PAD ? L.pad_keys : 0),
-                       pre18 ? reinterpret_cast<const unsigned long long*>(base + L.joint) : nullptr,
-                       static_cast<const int32_t*>(opt_gate));
+                       pre18 ? reinterpret_cast<const unsigned long long*>(base + L.joint) : nullptr);
     HPXHIP_CHECK_LAUNCH();
     if (first > 0) {
         if ((rc = count_rest(ctl + C_HIST_A))) return rc;

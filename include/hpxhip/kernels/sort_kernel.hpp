@@ -235,10 +235,8 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
                                                          unsigned long long* __restrict__ xhist,
                                                          unsigned long long* __restrict__ thist,
                                                          unsigned long long* __restrict__ bits,
-                                                         unsigned long long* __restrict__ joint,
-                                                         const int32_t* __restrict__ skip = nullptr) {
+                                                         unsigned long long* __restrict__ joint) {
     static_assert(THREADS == kXBins, "one thread per field digit");
-    if (skip && *skip) return;  // (r06) the optimistic first pass took the sort
     constexpr int V = 16 / static_cast<int>(sizeof(U));
     constexpr int VPT = TILE / V / THREADS;  // 16-B vectors per thread per tile
     static_assert(VPT * V * THREADS == TILE, "tile of whole vectors");
@@ -1019,10 +1017,7 @@ __global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict_
                                                           const int32_t* __restrict__ g_cap,
                                                           const seg_table* __restrict__ segs,
                                                           uint32_t* __restrict__ counter, uint32_t* __restrict__ pcnt,
-                                                          int32_t* __restrict__ ovf, X xf,
-                                                          const uint64_t* __restrict__ slot_tile0 = nullptr,
-                                                          const uint32_t* __restrict__ scnt = nullptr,
-                                                          uint64_t cap1 = 0) {
+                                                          int32_t* __restrict__ ovf, X xf) {
     const int s1 = *g_s1;  // the top-9 digit's shift, -1: the plan does not take this pass
     if (s1 < 0) return;
     const int s2 = g_bounds[3], b2 = g_bounds[4];
@@ -1032,7 +1027,8 @@ __global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict_
     constexpr int WAVES = THREADS / kWave;
     constexpr uint32_t NL = 1024;  // local bins; bin NL: keys placed one by one
     static_assert(THREADS == 512, "one thread per two local bins");
-    __shared__ uint64_t s_base, s_end;
+    __shared__ uint32_t s_tile, s_seg;
+    __shared__ uint64_t s_sg[3 * kMaxBig + 2];
     __shared__ uint32_t s_cnt[NL + 1];
     __shared__ uint32_t s_adj[NL];
     __shared__ uint32_t s_wsum[WAVES];
@@ -1040,50 +1036,40 @@ __global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict_
     const int t = threadIdx.x;
     const int lane = lane_id();
     const int wave = t / kWave;
+    for (int i = t; i <= 8; i += THREADS) {
+        if (i < 8) {
+            s_sg[i] = segs->start[i];
+            s_sg[kMaxBig + i] = segs->len[i];
+        }
+        s_sg[2 * kMaxBig + i] = segs->tile0[i];
+    }
     if (t == 0) {
-        // the next tile of this XCD's region (see k_onesweep XREG): the 8
-        // field regions of a contiguous input (segs), or (r06, slot input:
-        // the optimistic first pass's field slots, slot f at f * cap1 holding
-        // scnt[f] keys) region x = slots [64 x, 64 x + 64), whose tiles are
-        // numbered slot by slot (slot_tile0)
+        s_sg[3 * kMaxBig + 1] = segs->nseg;
+        // the next tile of this XCD's region (see k_onesweep XREG)
         const uint32_t x = xcc_id();
-        uint64_t base = 0, end = 0;
-        bool got = false;
-        const uint32_t nseg = slot_tile0 ? 8u : segs->nseg;
-        for (uint32_t k = 0; k < 8 && !got; ++k) {
+        uint32_t tl = 0xffffffffu, sg = 0;
+        const uint32_t nseg = segs->nseg;
+        for (uint32_t k = 0; k < 8 && tl == 0xffffffffu; ++k) {
             const uint32_t xr = (x + k) & 7u;
             if (xr >= nseg) continue;
-            const uint64_t lo = slot_tile0 ? slot_tile0[64 * xr] : segs->tile0[xr];
-            const uint64_t cnt = (slot_tile0 ? slot_tile0[64 * xr + 64] : segs->tile0[xr + 1]) - lo;
+            const uint64_t lo = segs->tile0[xr], cnt = segs->tile0[xr + 1] - lo;
             if (cnt == 0) continue;
             const uint32_t c = __hip_atomic_fetch_add(counter + 8 * xr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (c >= cnt) continue;
-            got = true;
-            if (slot_tile0) {
-                // the slot holding region tile c: the last f with tile0[f] <= lo + c
-                const uint64_t g = lo + c;
-                uint32_t a = 64 * xr, b = 64 * xr + 64;
-                while (b - a > 1) {
-                    const uint32_t m = (a + b) / 2;
-                    if (slot_tile0[m] <= g) a = m;
-                    else b = m;
-                }
-                base = a * cap1 + (g - slot_tile0[a]) * TILE;
-                end = a * cap1 + scnt[a];
-            } else {
-                base = segs->start[xr] + c * TILE;
-                end = segs->start[xr] + segs->len[xr];
+            if (c < cnt) {
+                tl = static_cast<uint32_t>(lo + c);
+                sg = xr;
             }
         }
-        s_base = got ? base : ~0ull;
-        s_end = end;
+        s_tile = tl;
+        s_seg = sg;
     }
     for (uint32_t i = t; i <= NL; i += THREADS) s_cnt[i] = 0;
     __syncthreads();
-    const uint64_t tile_base = s_base;
-    if (tile_base == ~0ull) return;
-    const uint64_t end = s_end;
-    [[maybe_unused]] const uint32_t tile = static_cast<uint32_t>(tile_base / TILE);  // (the ablation's fixed claims only)
+    const uint32_t tile = s_tile;
+    if (tile == 0xffffffffu) return;
+    const uint32_t j = s_seg;
+    const uint64_t seg_lo = s_sg[j], end = seg_lo + s_sg[kMaxBig + j];
+    const uint64_t tile_base = seg_lo + (tile - s_sg[2 * kMaxBig + j]) * TILE;
     const bool full = tile_base + TILE <= end;
     const uint64_t wbase = tile_base + static_cast<uint64_t>(wave) * (TILE / WAVES);
     const uint32_t fb0 = static_cast<uint32_t>(xf(kin[tile_base]) >> s2) & bmask;
@@ -1229,144 +1215,6 @@ __global__ __launch_bounds__(256) void k_pad_bounds(const uint32_t* __restrict__
     reinterpret_cast<V2*>(off + v)[0] = V2{{run, run + c.x}};
     reinterpret_cast<V2*>(off + v)[1] = V2{{run + c.x + c.y, run + c.x + c.y + c.z}};
     if (v + 4 == nb) off[nb] = run + sum;
-}
-
-// ------------------------------------- optimistic first prefix pass (r06)
-// The 18-bit form's first pass without the histogram read in front of it.
-// The first pass only has to leave every field bin contiguous (its order
-// inside a bin is never relied on, see k_pad_scatter), so -- like the padded
-// second pass -- each field bin f gets a slot of cap1 keys at f * cap1 in the
-// alternate buffer, claimed per tile by one global atomic per bin (scnt[f]),
-// and no offsets need to be known before the pass: the 8 B/key histogram read
-// (k_hist_tiles, 1.57 ms at 2^30 u64) and the tile-offset scans go.  What the
-// planner needs that the histogram read gave it comes out of this pass: the
-// keys' OR / AND (exact: every key), the field histogram (exact: the slot
-// counts), and the top-9 histogram per field region (joint, from every 32nd
-// tile: estimates, as the planner's sizes are).  The sort.hip planner
-// (k_opt_plan) then takes the padded second pass over the slots, or -- a slot
-// overflowed (a field bin over 1.25 n / 512 + 8192 keys), fewer than two live
-// top digits, buckets that do not fit -- hands the sort to the full path from
-// the keys, which this pass only read.
-constexpr uint32_t kOptSample = 32;  // joint histogram from every 32nd tile
-template <typename U, typename X, int THREADS = 512, int ITEMS = 16>
-__global__ __launch_bounds__(THREADS, 4) void k_slot_pass1(const U* __restrict__ kin, U* __restrict__ slots,
-                                                          uint64_t n, uint64_t ntiles, X xf, int fs, int ts,
-                                                          uint64_t cap1, uint32_t* __restrict__ scnt,
-                                                          unsigned long long* __restrict__ bits,
-                                                          unsigned long long* __restrict__ jsamp,
-                                                          int32_t* __restrict__ ovf, uint32_t* __restrict__ counter) {
-    constexpr int TILE = THREADS * ITEMS;
-    constexpr int WAVES = THREADS / kWave;
-    static_assert(THREADS == kXBins, "one thread per field digit");
-    __shared__ uint32_t s_tile;
-    __shared__ uint32_t s_cnt[kXBins];
-    __shared__ uint64_t s_adj[kXBins];
-    __shared__ uint32_t s_wsum[WAVES];
-    __shared__ uint32_t s_j[8 * kXBins / 2];  // sampled tiles: (region, top-9) counts, 16-bit pairs
-    __shared__ U s_keys[TILE];
-    const int t = threadIdx.x;
-    const int lane = lane_id();
-    const int wave = t / kWave;
-    if (t == 0) {  // XCD regions of equal tile ranges (k_onesweep XREG)
-        const uint32_t x = xcc_id();
-        uint32_t tl = 0xffffffffu;
-        const uint64_t per = (ntiles + 7) / 8;
-        for (uint32_t k = 0; k < 8 && tl == 0xffffffffu; ++k) {
-            const uint32_t xr = (x + k) & 7u;
-            const uint64_t lo = xr * per;
-            const uint64_t cnt = lo < ntiles ? (ntiles - lo < per ? ntiles - lo : per) : 0;
-            if (cnt == 0) continue;
-            const uint32_t c = __hip_atomic_fetch_add(counter + 8 * xr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (c < cnt) tl = static_cast<uint32_t>(lo + c);
-        }
-        s_tile = tl;
-    }
-    s_cnt[t] = 0;
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    if (tile == 0xffffffffu) return;
-    const bool sampled = tile % kOptSample == 0;
-    if (sampled)
-        for (int i = t; i < 8 * kXBins / 2; i += THREADS) s_j[i] = 0;
-    const uint64_t tile_base = static_cast<uint64_t>(tile) * TILE;
-    const bool full = tile_base + TILE <= n;
-    const uint64_t wbase = tile_base + static_cast<uint64_t>(wave) * (TILE / WAVES);
-    U k[ITEMS];
-    {
-        const uint64_t last = n - 1;
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            const uint64_t i = wbase + r * kWave + lane;
-            k[r] = kin[(full || i < n) ? i : last];
-        }
-    }
-    __syncthreads();  // s_j zeroed
-    U any = 0, all = static_cast<U>(~U(0));
-    uint32_t rank[ITEMS];
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-        const uint64_t i = wbase + r * kWave + lane;
-        if (full || i < n) {
-            const U u = xf(k[r]);
-            any |= u;
-            all &= u;
-            const uint32_t f = static_cast<uint32_t>(u >> fs) & (kXBins - 1);
-            rank[r] = atomicAdd(&s_cnt[f], 1u);
-            if (sampled) {
-                const uint32_t cell = (f >> 6) * kXBins + (static_cast<uint32_t>(u >> ts) & (kXBins - 1));
-                atomicAdd(&s_j[cell >> 1], 1u << (16 * (cell & 1)));
-            }
-        }
-    }
-    any = wave_reduce(any, op_bit_or{});
-    all = wave_reduce(all, op_bit_and{});
-    if (lane == 0) {
-        atomicOr(&bits[0], static_cast<unsigned long long>(any));
-        atomicAnd(&bits[1], static_cast<unsigned long long>(all) | (sizeof(U) == 8 ? 0ull : ~0ull << 32));
-    }
-    __syncthreads();
-    {  // thread t owns field bin t: local start, and the bin's run of its slot
-        const uint32_t c = s_cnt[t];
-        const uint32_t incl = wave_inclusive_scan(c, op_plus{});
-        if (lane == kWave - 1) s_wsum[wave] = incl;
-        __syncthreads();
-        uint32_t ls = incl - c;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w)
-            if (w < wave) ls += s_wsum[w];
-        if (c) {
-            const uint32_t base = __hip_atomic_fetch_add(&scnt[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (base + c <= cap1) {
-                s_adj[t] = static_cast<uint64_t>(t) * cap1 + base - ls;
-            } else {
-                s_adj[t] = ~0ull;
-                __hip_atomic_store(ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        s_cnt[t] = ls;
-        if (sampled)
-            for (int i = t; i < 8 * kXBins; i += THREADS) {
-                const uint32_t v = (s_j[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-                if (v) atomicAdd(&jsamp[i], static_cast<unsigned long long>(v));
-            }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-        const uint64_t i = wbase + r * kWave + lane;
-        if (full || i < n) s_keys[s_cnt[static_cast<uint32_t>(xf(k[r]) >> fs) & (kXBins - 1)] + rank[r]] = k[r];
-    }
-    __syncthreads();
-    const uint32_t nvalid = full ? TILE : static_cast<uint32_t>(n - tile_base);
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-        const uint32_t i = r * THREADS + t;
-        if (i < nvalid) {
-            const U key = s_keys[i];
-            const uint64_t a = s_adj[static_cast<uint32_t>(xf(key) >> fs) & (kXBins - 1)];
-            if (a != ~0ull) slots[a + i] = key;
-        }
-    }
 }
 
 // off[v] = first index whose prefix is >= v (v = 0..nb): a lower_bound per
