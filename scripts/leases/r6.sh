@@ -224,4 +224,21 @@ lease_j() {
     python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j"; fi
+lease_k() {
+  # round 6, lease k: validation of the tree -- the whole GPU suite, smoke, bench, and the bench under
+  # rocprofv3 --kernel-trace --stats
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6k
+  timeout -k 10 1500 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > ${L}_tests.log 2>&1
+  rc=$?; echo "suite rc=$rc" >> ${L}_status.log
+  if [ $rc -gt 1 ]; then exit $rc; fi
+  timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > ${L}_smoke.log 2>&1 || exit $?
+  timeout -k 10 600 python -u bench.py > ${L}_bench.log 2>&1 || exit $?
+  echo "bench ok" >> ${L}_status.log
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d ${L}_prof -o run -- python3 bench.py --no-pmc \
+    --no-cpu > ${L}_bench_under_rocprof.log 2>&1 || exit $?
+  echo "rocprof ok" >> ${L}_status.log
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k"; fi
