@@ -831,7 +831,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                 // the check that hands a sort whose slots overflowed to the
                 // look-back pass below
                 const uint64_t nt = L.ntiles + 8;
-                auto* pcnt = reinterpret_cast<uint32_t*>(base + L.lb);
+                auto* pcnt = reinterpret_cast<unsigned long long*>(base + L.lb);
                 const uint64_t pz = align_up(256 + 4ull * kMaxBuckets, 16);
                 hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(pz / 16, 2048)), dim3(256), 0, s,
                                    reinterpret_cast<uint4*>(counter), pz / 16, ctl + C_B9P);
@@ -874,7 +874,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                            0, 0u, X{}, bounds, ctl + C_BOUNDS);
         HPXHIP_CHECK_LAUNCH();
         if (!HAS_VAL && mode == 18 && pre18) {  // the padded pass's bounds: a scan of its slot counts
-            const auto* pcnt = reinterpret_cast<const uint32_t*>(base + L.lb);
+            const auto* pcnt = reinterpret_cast<const unsigned long long*>(base + L.lb);
             auto* bsum = reinterpret_cast<uint64_t*>(base + L.lb + 4ull * kMaxBuckets);  // lb_bytes > 4 x 2^18 + 2 KiB
             const dim3 grid(kMaxBuckets / 1024);  // blocks past the plan's buckets leave
             hipLaunchKernelGGL(k_pad_sums, grid, dim3(256), 0, s, pcnt, ctl + C_BOUNDS, ctl + C_PAD, bsum);

@@ -1010,13 +1010,17 @@ __device__ __forceinline__ uint32_t bucket_of(U k, int s1, int s2, int b2, X xf,
 // parts: small or skewed field bins) claim their slot places one by one.  A
 // bucket whose slot overflows raises *ovf: sort.hip then runs the look-back
 // pass from the same input (left intact) instead.
+// the slot counter word of bucket (top-9 digit t9, field part fb): four
+// consecutive digits of one field part per 64-bit word (16-bit fields)
+__device__ __forceinline__ uint32_t pad_word(uint32_t t9, uint32_t fb) { return fb * 128u + (t9 >> 2); }
 template <typename U, typename X, int THREADS = 512, int ITEMS = 16>
 __global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict__ kin, U* __restrict__ pad,
                                                           const int32_t* __restrict__ g_s1,
                                                           const int32_t* __restrict__ g_bounds,
                                                           const int32_t* __restrict__ g_cap,
                                                           const seg_table* __restrict__ segs,
-                                                          uint32_t* __restrict__ counter, uint32_t* __restrict__ pcnt,
+                                                          uint32_t* __restrict__ counter,
+                                                          unsigned long long* __restrict__ pcnt,
                                                           int32_t* __restrict__ ovf, X xf) {
     const int s1 = *g_s1;  // the top-9 digit's shift, -1: the plan does not take this pass
     if (s1 < 0) return;
@@ -1095,11 +1099,21 @@ __global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict_
         if (full || i < end) rank[r] = atomicAdd(&s_cnt[local_bin(k[r])], 1u);
     }
     __syncthreads();
-    // local starts (thread t: bins 2t, 2t + 1; the one-by-one bin last) and
-    // each bin's run of its bucket's slot
+    // local starts (thread t < 256: bins 4t .. 4t + 3, four top-9 digits of
+    // one field part; the one-by-one bin last) and each bin's run of its
+    // bucket's slot.  r06: the slot counters are 16-bit fields, four buckets
+    // (four top-9 digits of one field part) per 64-bit word, so one atomic
+    // claims four runs: 128 atomics per tile instead of 512 (the counters'
+    // atomics were 27 % extra write traffic, profiles/r06_pmc_sort_e.txt).  A
+    // field can only carry into its neighbour past 65535 keys, long after
+    // its slot (<= 4608) overflowed and raised *ovf.
     {
-        const uint32_t c0 = s_cnt[2 * t], c1 = s_cnt[2 * t + 1];
-        const uint32_t sum = c0 + c1;
+        uint32_t c[4] = {0, 0, 0, 0};
+        if (t < 256) {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) c[h] = s_cnt[4 * t + h];
+        }
+        const uint32_t sum = c[0] + c[1] + c[2] + c[3];
         const uint32_t incl = wave_inclusive_scan(sum, op_plus{});
         if (lane == kWave - 1) s_wsum[wave] = incl;
         __syncthreads();
@@ -1107,28 +1121,34 @@ __global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict_
 #pragma unroll
         for (int w = 0; w < WAVES; ++w)
             if (w < wave) pre += s_wsum[w];
-        const uint32_t ls[2] = {pre, pre + c0}, cs[2] = {c0, c1};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t lb = 2 * t + h;
-            if (cs[h]) {
-                const uint32_t bucket = ((lb & 511u) << b2) | (fb0 + (lb >> 9));
-#if HPXHIP_PAD_ABL  // ablation (timing only, wrong output): no atomics, a spread of fixed claims
-                const uint32_t base = (tile * 16u) % (cap - 64u);
-#else
-                const uint32_t base = __hip_atomic_fetch_add(&pcnt[bucket], cs[h], __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT);
-#endif
-                if (base + cs[h] <= cap) {
-                    s_adj[lb] = bucket * cap + base - ls[h];  // mod 2^32: pad index of local position ls
-                } else {
-                    s_adj[lb] = 0xffffffffu;
-                    __hip_atomic_store(ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
+        if (t < 256) {
+            const uint32_t t9 = (4u * t) & 511u, fb = fb0 + ((4u * t) >> 9);
+            uint64_t old = 0;
+            if (sum) {
+                const uint64_t add = static_cast<uint64_t>(c[0]) | static_cast<uint64_t>(c[1]) << 16 |
+                                     static_cast<uint64_t>(c[2]) << 32 | static_cast<uint64_t>(c[3]) << 48;
+                old = __hip_atomic_fetch_add(&pcnt[pad_word(t9, fb)], add, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
             }
-            s_cnt[lb] = ls[h];
+            uint32_t ls = pre;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t lb = 4 * t + h;
+                if (c[h]) {
+                    const uint32_t base = static_cast<uint32_t>(old >> (16 * h)) & 0xffffu;
+                    const uint32_t bucket = ((t9 + h) << b2) | fb;
+                    if (base + c[h] <= cap) {
+                        s_adj[lb] = bucket * cap + base - ls;  // mod 2^32: pad index of local position ls
+                    } else {
+                        s_adj[lb] = 0xffffffffu;
+                        __hip_atomic_store(ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                s_cnt[lb] = ls;
+                ls += c[h];
+            }
+            if (t == 255) s_cnt[NL] = ls;
         }
-        if (t == THREADS - 1) s_cnt[NL] = pre + sum;
     }
     __syncthreads();
 #pragma unroll
@@ -1151,8 +1171,11 @@ __global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict_
                 const U u = xf(key);
                 const uint32_t bucket = ((static_cast<uint32_t>(u >> s1) & 511u) << b2) |
                                         (static_cast<uint32_t>(u >> s2) & bmask);
-                const uint32_t base = __hip_atomic_fetch_add(&pcnt[bucket], 1u, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t t9 = static_cast<uint32_t>(u >> s1) & 511u;
+                const uint64_t old = __hip_atomic_fetch_add(&pcnt[pad_word(t9, static_cast<uint32_t>(u >> s2) & bmask)],
+                                                            uint64_t(1) << (16 * (t9 & 3u)), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t base = static_cast<uint32_t>(old >> (16 * (t9 & 3u))) & 0xffffu;
                 if (base < cap) pad[bucket * cap + base] = key;
                 else __hip_atomic_store(ovf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -1167,25 +1190,34 @@ __global__ __launch_bounds__(THREADS, 4) void k_pad_scatter(const U* __restrict_
 // pass ran and no slot overflowed).  g_bounds = {on, nb, ...}; nb is a power
 // of two >= 1024.  (A one-workgroup scan walking 256 buckets per thread took
 // 0.21 ms, profiles/r06_sort_kernel_stats_u64_d.csv.)
-__global__ __launch_bounds__(256) void k_pad_sums(const uint32_t* __restrict__ pcnt,
+__device__ __forceinline__ uint32_t pad_count(const unsigned long long* pcnt, uint32_t bucket, int b2) {
+    const uint32_t t9 = bucket >> b2, fb = bucket & ((1u << b2) - 1u);
+    return static_cast<uint32_t>(pcnt[pad_word(t9, fb)] >> (16 * (t9 & 3u))) & 0xffffu;
+}
+__global__ __launch_bounds__(256) void k_pad_sums(const unsigned long long* __restrict__ pcnt,
                                                    const int32_t* __restrict__ g_bounds,
                                                    const int32_t* __restrict__ g_cap, uint64_t* __restrict__ bsum) {
     if (*g_cap <= 0) return;
     const uint32_t nb = static_cast<uint32_t>(g_bounds[1]);
+    const int b2 = g_bounds[4];
     if (blockIdx.x * 1024u >= nb) return;
     __shared__ uint64_t s_w[4];
-    const uint4 c = reinterpret_cast<const uint4*>(pcnt)[blockIdx.x * 256u + threadIdx.x];
-    const uint64_t x = wave_reduce(static_cast<uint64_t>(c.x) + c.y + c.z + c.w, op_plus{});
+    const uint32_t v = blockIdx.x * 1024u + 4u * threadIdx.x;
+    uint64_t x = 0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) x += pad_count(pcnt, v + h, b2);
+    x = wave_reduce(x, op_plus{});
     if (lane_id() == 0) s_w[threadIdx.x / kWave] = x;
     __syncthreads();
     if (threadIdx.x == 0) bsum[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
-__global__ __launch_bounds__(256) void k_pad_bounds(const uint32_t* __restrict__ pcnt,
+__global__ __launch_bounds__(256) void k_pad_bounds(const unsigned long long* __restrict__ pcnt,
                                                      const int32_t* __restrict__ g_bounds,
                                                      const int32_t* __restrict__ g_cap,
                                                      const uint64_t* __restrict__ bsum, uint64_t* __restrict__ off) {
     if (*g_cap <= 0) return;
     const uint32_t nb = static_cast<uint32_t>(g_bounds[1]);
+    const int b2 = g_bounds[4];
     const uint32_t b = blockIdx.x;
     if (b * 1024u >= nb) return;
     const int t = threadIdx.x, lane = lane_id(), wave = t / kWave;
@@ -1201,8 +1233,11 @@ __global__ __launch_bounds__(256) void k_pad_bounds(const uint32_t* __restrict__
         x = wave_reduce(x, op_plus{});
         if (lane == 0) s_base = x;
     }
-    const uint4 c = reinterpret_cast<const uint4*>(pcnt)[b * 256u + t];
-    const uint64_t sum = static_cast<uint64_t>(c.x) + c.y + c.z + c.w;
+    const uint32_t v = b * 1024u + 4u * t;
+    uint32_t c[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) c[h] = pad_count(pcnt, v + h, b2);
+    const uint64_t sum = static_cast<uint64_t>(c[0]) + c[1] + c[2] + c[3];
     const uint64_t incl = wave_inclusive_scan(sum, op_plus{});
     if (lane == kWave - 1) s_w[wave] = incl;
     __syncthreads();
@@ -1210,10 +1245,9 @@ __global__ __launch_bounds__(256) void k_pad_bounds(const uint32_t* __restrict__
 #pragma unroll
     for (int w = 0; w < 4; ++w)
         if (w < wave) run += s_w[w];
-    const uint32_t v = b * 1024u + 4u * t;
     using V2 = vec<uint64_t, 2>;
-    reinterpret_cast<V2*>(off + v)[0] = V2{{run, run + c.x}};
-    reinterpret_cast<V2*>(off + v)[1] = V2{{run + c.x + c.y, run + c.x + c.y + c.z}};
+    reinterpret_cast<V2*>(off + v)[0] = V2{{run, run + c[0]}};
+    reinterpret_cast<V2*>(off + v)[1] = V2{{run + c[0] + c[1], run + c[0] + c[1] + c[2]}};
     if (v + 4 == nb) off[nb] = run + sum;
 }
 

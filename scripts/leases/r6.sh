@@ -241,4 +241,29 @@ lease_k() {
   echo "rocprof ok" >> ${L}_status.log
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k"; fi
+lease_l() {
+  # round 6, lease l: the padded pass's slot counters packed four per 64-bit word (128 claims per tile
+  # instead of 512): sort tests, A/B against pad32 (one 32-bit counter per bucket), kernel trace, and a
+  # WRITE_SIZE pass over the u64 sort
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6l
+  timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sort_hybrid.py \
+    tests/test_gpu_fullsize.py -k "sort" > ${L}_tests.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for lib in hpx_amd/libhpxhip.so scripts/ubench/seglib/pad32/libhpxhip.so; do
+      for c in u64 u32; do
+        echo "== $lib $c rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 30 >> ${L}_ab.log 2>&1 || exit $?
+      done
+      echo "== $lib u64hot rep $rep" >> ${L}_ab.log
+      HPXHIP_LIB=$lib SORT_ONLY=u64hot timeout -k 10 200 python -u scripts/sort_probe.py 28 >> ${L}_ab.log 2>&1 || exit $?
+    done
+  done
+  SORT_ONLY=u64 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6l_prof_u64 -o run -- \
+    python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
+  SORT_ONLY=u64 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/r6l_pmc_w -o run -- \
+    python3 scripts/sort_probe.py 30 > ${L}_pmc_w.log 2>&1 || exit 1
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l"; fi
