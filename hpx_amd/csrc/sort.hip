@@ -318,18 +318,12 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
     if (mode == 18 && !has_val && stage == 0 && thist) {
         const int t = threadIdx.x;
         for (int i = t; i < kXBins; i += 64) s_x[i] = static_cast<double>(xhist[i]);
-        // r06: the top-9 (and joint) histograms may be a sample (k_hist_tiles
-        // counts them on every kJointSample-th tile): scaled to n keys
-        double tsum = 0;
-        for (int i = t; i < kXBins; i += 64) tsum += static_cast<double>(thist[i]);
-        for (int o = 32; o > 0; o >>= 1) tsum += __shfl_xor(tsum, o);
-        const double tscale = tsum > 0 ? static_cast<double>(n) / tsum : 1.0;
         __syncthreads();
         const double mean = static_cast<double>(n) / kXBins;
         double mtop = 0, mt = mean, et = 0, ef = 0;
         int ht = 0, hf = 0;
         for (int i = t; i < kXBins; i += 64) {
-            const double a = tscale * static_cast<double>(thist[i]), b = s_x[i];
+            const double a = static_cast<double>(thist[i]), b = s_x[i];
             mtop = a > mtop ? a : mtop;
             if (a > 2 * mean) ++ht, et += a - mean;
             else mt = a > mt ? a : mt;
@@ -381,7 +375,7 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
             // loads per thread instead of eight dependent rounds
             __shared__ float s_joint[8 * kXBins];
 #pragma unroll 16
-            for (int i = t; i < 8 * kXBins; i += 64) s_joint[i] = static_cast<float>(tscale * static_cast<double>(joint[i]));
+            for (int i = t; i < 8 * kXBins; i += 64) s_joint[i] = static_cast<float>(joint[i]);
             __syncthreads();
             for (int tt = t; tt < kXBins; tt += 64) {
                 double j[8];
@@ -476,8 +470,7 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
                 // r06: the padded second pass when its slots -- the estimated
                 // largest bucket + 7 sigma, whole 64-key lines -- fit the scratch
                 const uint32_t nb = 512u << b2;
-                // (+ 1 % + 32 keys for the sampled top-9 histogram)
-                uint32_t cap = (static_cast<uint32_t>(1.01 * est + 7.0 * sqrt(est) + 33.0) + 63u) & ~63u;
+                uint32_t cap = (static_cast<uint32_t>(est + 7.0 * sqrt(est) + 1.0) + 63u) & ~63u;
                 cap = cap < kCap18 ? cap : static_cast<uint32_t>(kCap18);
                 if (pad_keys > 0 && static_cast<uint64_t>(nb) * cap <= pad_keys) {
                     ctl[C_B9P] = 8 * passes - 9;
@@ -698,10 +691,7 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                     bool persist, const unsigned long long* bs9 = nullptr, const uint32_t* pre = nullptr) -> int {
         const unsigned long long* b9 = bs9 ? bs9 : xstart;  // a 9-bit pass's bin starts
         const uint64_t nt = L.ntiles;
-        // the look-back state; the PRE pass (no look-back) only claims tiles
-        // from the counter (r06: it had zeroed all 268 MB of granules at 2^30,
-        // 38 us per sort)
-        const uint64_t zbytes = pre ? 256 : align_up(256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), 16);
+        const uint64_t zbytes = align_up(256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), 16);
         {  // (the PRE pass too: its tiles are claimed from the counter, which this zeroes)
             hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
                                reinterpret_cast<uint4*>(counter), zbytes / 16, word);
@@ -788,12 +778,11 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
         hipLaunchKernelGGL(k_bin_offsets<kXBins>, dim3(1), dim3(kXBins), 0, s, xhist, xstart);
         HPXHIP_CHECK_LAUNCH();
     }
-    if (mode == 18 && !pre18) {  // (pre18: k_hist_tiles samples the top-9 histogram; see the second pass)
+    if (mode == 18) {
         hipLaunchKernelGGL(k_bin_offsets<kXBins>, dim3(1), dim3(kXBins), 0, s, thist, tstart);
         HPXHIP_CHECK_LAUNCH();
     }
-    if (pre18) {  // the second prefix pass's field regions (segs2, from the exact field histogram; the
-                  // region bin starts bs2 are recomputed from exact counts iff the look-back pass runs)
+    if (pre18) {  // the second prefix pass's field regions
         hipLaunchKernelGGL(k_region_plan, dim3(1), dim3(kXBins), 0, s, xstart, tstart,
                            reinterpret_cast<const unsigned long long*>(base + L.joint), n, TS::tile,
                            reinterpret_cast<seg_table*>(base + L.segs2),
@@ -853,25 +842,6 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                                    counter, pcnt, ctl + C_PADOVF, X{});
                 HPXHIP_CHECK_LAUNCH();
                 hipLaunchKernelGGL(k_pad_check, dim3(1), dim3(64), 0, s, ctl);
-                HPXHIP_CHECK_LAUNCH();
-                // r06: the look-back pass's region bin starts need the exact
-                // joint and top-9 histograms, which k_hist_tiles only samples:
-                // recounted iff the plan takes that pass (a skewed plan, or a
-                // padded pass whose slot overflowed)
-                hipLaunchKernelGGL(k_zero_gated, dim3(grid_for((9 * kXBins * 8) / 16, 64)), dim3(256), 0, s,
-                                   reinterpret_cast<uint4*>(thist), static_cast<uint64_t>((9 * kXBins * 8) / 16),
-                                   ctl + C_B9);
-                HPXHIP_CHECK_LAUNCH();
-                hipLaunchKernelGGL((k_joint_exact<U, X>), dim3(2 * current_device_info().cus), dim3(512), 0, s, kc, n,
-                                   X{}, field18_shift<U>(), top9_shift<U>(), thist,
-                                   reinterpret_cast<unsigned long long*>(base + L.joint), ctl + C_B9);
-                HPXHIP_CHECK_LAUNCH();
-                hipLaunchKernelGGL(k_bin_offsets<kXBins>, dim3(1), dim3(kXBins), 0, s, thist, tstart);
-                HPXHIP_CHECK_LAUNCH();
-                hipLaunchKernelGGL(k_region_plan, dim3(1), dim3(kXBins), 0, s, xstart, tstart,
-                                   reinterpret_cast<const unsigned long long*>(base + L.joint), n, TS::tile,
-                                   reinterpret_cast<seg_table*>(base + L.segs2),
-                                   reinterpret_cast<unsigned long long*>(base + L.bs2));
                 HPXHIP_CHECK_LAUNCH();
                 // r05: the top-9 pass over the field-ordered keys in 8 field
                 // regions, one per XCD, each with its own look-back and bin

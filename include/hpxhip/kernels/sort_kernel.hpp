@@ -229,7 +229,6 @@ __global__ __launch_bounds__(THREADS) void k_hist(const U* __restrict__ keys, ui
 // exclusive prefixes (from the digits' bin starts), k_tile_offsets the tile
 // counts into each tile's destination offsets, which the pass reads instead
 // of walking back (k_onesweep PRE).  Offsets are 32-bit: n < 2^32.
-constexpr uint32_t kJointSample = 8;
 template <typename U, typename X, int TILE = 8192, int THREADS = 512>
 __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ keys, uint64_t n, uint64_t ntiles,
                                                          X xf, int xshift, int tshift, uint32_t* __restrict__ tcount,
@@ -269,16 +268,9 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
     // one readlane + compare + ballot per key (peeling the first two lanes'
     // cells unconditionally had cost them 4x: 1.75 ms at 2^28).
     uint32_t cc0 = ~0u, cc1 = ~0u, cn0 = 0, cn1 = 0;
-    // r06: the joint (region, top-9) cells are counted on every kJointSample-th
-    // tile of each workgroup only (the field's per-tile counts on every tile):
-    // one LDS atomic per key instead of two.  The planner scales the sample
-    // (its sizes are estimates), and the one consumer that needs the exact
-    // joint histogram -- the look-back second pass's region bin starts --
-    // gets it from k_joint_exact, run only when the plan takes that pass.
-    bool sj = true;
     auto add_cell = [&](uint32_t c, uint32_t v, uint32_t* ct) {
         atomicAdd(&ct[c >> 12], v);
-        if (sj) atomicAdd(&hj[c & 0xfffu], v);
+        atomicAdd(&hj[c & 0xfffu], v);
     };
     auto count = [&](U b, uint32_t* ct) {
         any |= b;
@@ -329,8 +321,7 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
     uint64_t t = blockIdx.x;
     if (t < ntiles && full_tile(t)) load(x, t);
     int buf = 0;
-    for (uint32_t it = 0; t < ntiles; t += gridDim.x, ++it) {
-        sj = (it + blockIdx.x) % kJointSample == 0;  // (balanced over the workgroups)
+    for (; t < ntiles; t += gridDim.x) {
         const uint64_t base = t * TILE;
         const uint64_t tn = t + gridDim.x;
         const bool pf = tn < ntiles && full_tile(tn);
@@ -379,36 +370,6 @@ __global__ __launch_bounds__(THREADS) void k_hist_tiles(const U* __restrict__ ke
     if (lane_id() == 0) {
         atomicOr(&bits[0], static_cast<unsigned long long>(any));
         atomicAnd(&bits[1], static_cast<unsigned long long>(all) | (sizeof(U) == 8 ? 0ull : ~0ull << 32));
-    }
-}
-
-// r06: the exact joint (field region x top-9) and top-9 histograms, for the
-// look-back second pass's region bin starts (k_region_plan) -- k_hist_tiles
-// samples them; runs iff *gate >= 0 (the plan takes the look-back pass).
-template <typename U, typename X, int THREADS = 512>
-__global__ __launch_bounds__(THREADS) void k_joint_exact(const U* __restrict__ keys, uint64_t n, X xf, int xshift,
-                                                          int tshift, unsigned long long* __restrict__ thist,
-                                                          unsigned long long* __restrict__ joint,
-                                                          const int32_t* __restrict__ gate) {
-    if (*gate < 0) return;
-    __shared__ uint32_t hj[8 * kXBins];
-    for (int i = threadIdx.x; i < 8 * kXBins; i += THREADS) hj[i] = 0;
-    __syncthreads();
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * THREADS;
-    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * THREADS + threadIdx.x; i < n; i += stride) {
-        const U u = xf(keys[i]);
-        const uint32_t f = static_cast<uint32_t>(u >> xshift) & (kXBins - 1);
-        atomicAdd(&hj[(f >> 6) * kXBins + (static_cast<uint32_t>(u >> tshift) & (kXBins - 1))], 1u);
-    }
-    __syncthreads();
-    for (int d = threadIdx.x; d < kXBins; d += THREADS) {
-        uint32_t tc = 0;
-        for (int x = 0; x < 8; ++x) {
-            const uint32_t c = hj[x * kXBins + d];
-            tc += c;
-            if (c) atomicAdd(&joint[x * kXBins + d], static_cast<unsigned long long>(c));
-        }
-        if (tc) atomicAdd(&thist[d], static_cast<unsigned long long>(tc));
     }
 }
 
