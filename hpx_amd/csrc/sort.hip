@@ -691,7 +691,9 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                     bool persist, const unsigned long long* bs9 = nullptr, const uint32_t* pre = nullptr) -> int {
         const unsigned long long* b9 = bs9 ? bs9 : xstart;  // a 9-bit pass's bin starts
         const uint64_t nt = L.ntiles;
-        const uint64_t zbytes = align_up(256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), 16);
+        // the look-back state; the PRE pass (no look-back) only claims tiles
+        // from the counter (r06: it had zeroed all 268 MB of granules at 2^30)
+        const uint64_t zbytes = pre ? 256 : align_up(256 + nt * (uint64_t(1) << rb) * (L.wide ? 8 : 4), 16);
         {  // (the PRE pass too: its tiles are claimed from the counter, which this zeroes)
             hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
                                reinterpret_cast<uint4*>(counter), zbytes / 16, word);
