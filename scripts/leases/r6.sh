@@ -229,7 +229,7 @@ lease_k() {
   # rocprofv3 --kernel-trace --stats
   cd $GRAFT_REPO_ROOT
   export TMPDIR=/tmp
-  L=gpurun_out/r6k
+  L=${LEASE_OUT:-gpurun_out/r6k}
   timeout -k 10 1500 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > ${L}_tests.log 2>&1
   rc=$?; echo "suite rc=$rc" >> ${L}_status.log
   if [ $rc -gt 1 ]; then exit $rc; fi
@@ -292,4 +292,16 @@ lease_m() {
     python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m"; fi
+lease_n() {
+  # round 6, lease n: final validation (as lease k) of the round's last tree, plus a 2^30 u64 / u32 sort
+  # kernel trace and one sort probe sweep
+  LEASE_OUT=gpurun_out/r6n lease_k || exit $?
+  cd $GRAFT_REPO_ROOT
+  L=gpurun_out/r6n
+  for c in u64 u32; do
+    SORT_ONLY=$c timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6n_prof_$c -o run -- \
+      python3 -u scripts/sort_probe.py 30 > ${L}_sort_$c.log 2>&1 || exit $?
+  done
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n"; fi
