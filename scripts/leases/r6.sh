@@ -302,6 +302,9 @@ lease_n() {
     SORT_ONLY=$c timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6n_prof_$c -o run -- \
       python3 -u scripts/sort_probe.py 30 > ${L}_sort_$c.log 2>&1 || exit $?
   done
+  # the N > 1 rows on one GPU over a real one-rank RCCL group (segmented reduce's per-call overhead)
+  HPXHIP_RCCL_SELF=1 timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+    --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --no-cpu --no-pmc > ${L}_rccl_self.log 2>&1 || exit $?
 }
 
 if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n"; fi
