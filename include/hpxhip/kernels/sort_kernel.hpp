@@ -603,9 +603,6 @@ __global__ __launch_bounds__(256) void k_seg_copy(const E* __restrict__ src, E* 
 #ifndef HPXHIP_REGION_ATOM
 #define HPXHIP_REGION_ATOM 1
 #endif
-#ifndef HPXHIP_XREG_STATIC
-#define HPXHIP_XREG_STATIC 1
-#endif
 template <typename U, typename VAL, bool HAS_VAL, typename G, typename X, int THREADS = 512, int ITEMS = 16,
           int LBB = 8, int RB = 8, bool STAGE = true, bool DYN_ID = HPXHIP_TILE_DYN_ID, bool PERSIST = false,
           bool SEG = false, bool XREG = false>
@@ -689,24 +686,7 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
         // a region that is done sends its XCD's workgroups to the next ones
         const uint32_t x = xcc_id();
         uint32_t tl = 0xffffffffu, sg = 0;
-        if constexpr (!SEG && HPXHIP_XREG_STATIC) {
-            // r06: the equal-range regions (the offset-fed first pass) taken
-            // without the counter: workgroup b -> region b % 8 -- the XCD the
-            // dispatcher deals it to -- tile b / 8 of it, region r holding
-            // the ceil((ntiles - r) / 8) tiles of its workgroups.  Every
-            // claim on a region's counter had been one device atomic on one
-            // address: 16384 of them per region at 2^30 keys, serialised
-            // (~180 ns each, profiles/r06_sort_opt_slot_pass1_rejected.log)
-            // against a 3.9 ms pass.  Any dealing covers every tile once; only
-            // the L2 sharing of neighbouring tiles depends on it.
-            const uint32_t r = blockIdx.x & 7u, c = blockIdx.x >> 3;
-            uint64_t lo = 0;
-            for (uint32_t q = 0; q < r; ++q) lo += ntiles > q ? (ntiles - q + 7) / 8 : 0;
-            const uint64_t cnt = ntiles > r ? (ntiles - r + 7) / 8 : 0;
-            if (c < cnt) tl = static_cast<uint32_t>(lo + c);
-            (void)x;
-        }
-        for (uint32_t k = 0; k < 8 && tl == 0xffffffffu && !(!SEG && HPXHIP_XREG_STATIC); ++k) {
+        for (uint32_t k = 0; k < 8 && tl == 0xffffffffu; ++k) {
             const uint32_t xr = (x + k) & 7u;
             uint64_t lo, cnt;
             if constexpr (SEG) {
