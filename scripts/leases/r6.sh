@@ -307,4 +307,26 @@ lease_n() {
     --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --no-cpu --no-pmc > ${L}_rccl_self.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n"; fi
+lease_o() {
+  # round 6, lease o: the offset-fed first pass deals its tiles to the XCD regions statically (no claim
+  # counter): sort tests, A/B against xdyn (claims from the per-region counters), kernel trace
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6o
+  timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sort_hybrid.py \
+    tests/test_gpu_fullsize.py -k "sort" > ${L}_tests.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for lib in hpx_amd/libhpxhip.so scripts/ubench/seglib/xdyn/libhpxhip.so; do
+      for c in u64 u32; do
+        echo "== $lib $c rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 30 >> ${L}_ab.log 2>&1 || exit $?
+      done
+      echo "== $lib u64 2^28 rep $rep" >> ${L}_ab.log
+      HPXHIP_LIB=$lib SORT_ONLY=u64 timeout -k 10 200 python -u scripts/sort_probe.py 28 >> ${L}_ab.log 2>&1 || exit $?
+    done
+  done
+  SORT_ONLY=u64 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6o_prof_u64 -o run -- \
+    python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o"; fi
