@@ -107,6 +107,26 @@ def test_cxx_program(prog, args):
     assert f"{prog}: all tests passed" in r.stdout
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("targets", [1, 3])
+def test_cxx_drop_in_bench_program(targets):
+    """tests/cxx/bench_targets (bench.py's `cxx_drop_in` row) at small sizes:
+    the step (triad + reduce + inclusive_scan under par(task)) and the heat
+    ring over a partitioned_vector of `targets` HIP targets on one device,
+    its own checks (reduce == scan's last == n, triad == 7, the heat ring's
+    sum conserved) and one JSON line."""
+    import json
+    exe = os.path.join(BIN, "bench_targets")
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} not built (run `make cxxtests` / __graft_entry__.build())")
+    r = subprocess.run([exe, "--targets", str(targets), "--logn", "20", "--heat-logn", "14", "--steps", "3",
+                        "--warmup", "1", "--heat-steps", "37"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    row = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"cxx_drop_in"')][-1])["cxx_drop_in"]
+    assert row["checks_ok"] and row["heat"]["sum_conserved"], row
+    assert row["targets"] == targets and row["elements_per_target"] == 1 << 20 and row["ms_per_step"] > 0
+
+
 def test_futures_compose_on_host():
     """hpx::future / shared_future / dataflow / unwrapping / when_all /
     wait_all / sliding_semaphore on host values (the restated lcos unit
