@@ -342,3 +342,22 @@ def test_direct_path_and_fallback(pol, gpu_target, kdt):
     v = np.arange(n, dtype=np.uint64)
     check_kv(pol, gpu_target, k, v)
     check_kv(pol, gpu_target, k, v, True)
+
+
+def test_one_pass_segment_sort_mixed_bins(pol, gpu_target):
+    """r06, the one-pass segment sort (k_bucket_sort ONEB = 13): most buckets
+    of random keys take it; in every 16th bucket (top 11 bits) the 13 bits
+    under the bucket's top take 4 values, so its bins hold ~1000 keys, over
+    kOneBinMax -- those buckets are listed and sorted by the two-pass form in
+    the third launch -- with duplicates and keys differing only in the low
+    bits inside them."""
+    rng = np.random.default_rng(0x0E13)
+    n = 1 << 23
+    h = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    top = h >> np.uint64(53)
+    sel = (top % np.uint64(16)) == 0
+    low = rng.integers(0, 4, int(sel.sum()), dtype=np.uint64) << np.uint64(40)
+    h[sel] = (h[sel] & ~(np.uint64((1 << 53) - 1))) | low | (h[sel] & np.uint64((1 << 20) - 1))
+    h[: 1000] = h[1000]  # a run of equal keys
+    check(pol, gpu_target, h)
+    check(pol, gpu_target, h, True)
