@@ -329,4 +329,46 @@ lease_o() {
     python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o"; fi
+lease_p() {
+  # round 6, lease p: the pairs segment sort in the one-pass form (HPXHIP_SEG_ONE_KV): sort tests (with the
+  # new pairs mixed-bins case), the C++ drop-in program test, A/B against kv1off (two-pass pairs), kernel trace
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6p
+  timeout -k 10 800 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sort_hybrid.py \
+    tests/test_gpu_parity.py tests/test_gpu_fullsize.py -k "sort" > ${L}_tests.log 2>&1 || exit $?
+  timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_cxx_api.py \
+    -k "drop_in" > ${L}_cxx.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for lib in hpx_amd/libhpxhip.so scripts/ubench/seglib/kv1off/libhpxhip.so; do
+      for lg in 28 26; do
+        echo "== $lib pairs 2^$lg rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=pairs timeout -k 10 200 python -u scripts/sort_probe.py $lg >> ${L}_ab.log 2>&1 || exit $?
+      done
+    done
+  done
+  SORT_ONLY=pairs timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6p_prof_pairs -o run -- \
+    python3 -u scripts/sort_probe.py 28 > ${L}_prof.log 2>&1 || exit $?
+}
+
+lease_q() {
+  # round 6, lease q: lease p's steps after its sort tests (green there): the C++ drop-in program test
+  # (the one-target check index fixed), the pairs A/B against kv1off, kernel trace
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6q
+  timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_cxx_api.py \
+    -k "drop_in" > ${L}_cxx.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for lib in hpx_amd/libhpxhip.so scripts/ubench/seglib/kv1off/libhpxhip.so; do
+      for lg in 28 26; do
+        echo "== $lib pairs 2^$lg rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=pairs timeout -k 10 200 python -u scripts/sort_probe.py $lg >> ${L}_ab.log 2>&1 || exit $?
+      done
+    done
+  done
+  SORT_ONLY=pairs timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6q_prof_pairs -o run -- \
+    python3 -u scripts/sort_probe.py 28 > ${L}_prof.log 2>&1 || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q"; fi

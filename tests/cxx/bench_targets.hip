@@ -118,10 +118,12 @@ int hpx_main(int, char**) {
         hpx::parallel::inclusive_scan(ex::par, x.begin(), x.end(), y.begin(), std::plus<int64_t>(), int64_t(0));
     });
 
-    // checks: reduce == n, scan's last == n, a few triad values == 7
+    // checks: reduce == n, scan's last == n (and across the first partition
+    // boundary), a few triad values == 7
     ok = r == static_cast<int64_t>(n) && int64_t(y[n - 1]) == static_cast<int64_t>(n) &&
-         int64_t(y[per]) == static_cast<int64_t>(per + 1) && double(a[0]) == 7.0 && double(a[n - 1]) == 7.0 &&
-         double(a[n / 2]) == 7.0;
+         int64_t(y[per - 1]) == static_cast<int64_t>(per) &&
+         (n == per || int64_t(y[per]) == static_cast<int64_t>(per + 1)) && double(a[0]) == 7.0 &&
+         double(a[n - 1]) == 7.0 && double(a[n / 2]) == 7.0;
     }
 
     // 1d_stencil_8 heat ring over the targets

@@ -361,3 +361,25 @@ def test_one_pass_segment_sort_mixed_bins(pol, gpu_target):
     h[: 1000] = h[1000]  # a run of equal keys
     check(pol, gpu_target, h)
     check(pol, gpu_target, h, True)
+
+
+def test_one_pass_pairs_segment_sort_mixed_bins(pol, gpu_target):
+    """sort_by_key over the keys of the test above (sort_by_key's 512 x 9
+    segments; buckets whose 13 bits under the top take 4 values), plus 5000
+    keys each copied to ~10 scattered places: equal keys inside one segment,
+    whose values must keep their input order.  (r06: it also covered the
+    rejected one-pass form with values, profiles/r06_sort_pairs_onepass_rejected.log.)"""
+    rng = np.random.default_rng(0x0E14)
+    n = 1 << 23
+    h = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    top = h >> np.uint64(53)
+    sel = (top % np.uint64(16)) == 0
+    low = rng.integers(0, 4, int(sel.sum()), dtype=np.uint64) << np.uint64(40)
+    h[sel] = (h[sel] & ~(np.uint64((1 << 53) - 1))) | low | (h[sel] & np.uint64((1 << 20) - 1))
+    h[: 1000] = h[1000]
+    src = h[rng.integers(0, n, 5000)]
+    h[rng.choice(n, 50000, replace=False)] = src[rng.integers(0, 5000, 50000)]
+    v = np.arange(n, dtype=np.uint64)
+    check_kv(pol, gpu_target, h, v)
+    check_kv(pol, gpu_target, h, v, True)
+    check_kv(pol, gpu_target, h, v.astype(np.uint32))
