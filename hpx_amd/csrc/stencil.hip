@@ -65,7 +65,7 @@ __global__ __launch_bounds__(kThreads) void k_heat_scalar(const double* __restri
 }
 
 // ------------------------------------------------------ temporal blocking
-// S fused steps per pass (S even, 2..16): each wave owns a window of WIN = 512
+// S fused steps per pass (S even, 2..16): each wave owns a window of WIN = 1024
 // consecutive points held in registers as ROWS rows x 64 lanes x P points
 // (row r, lane l -> window points r*64P + l*P .. +P-1; loads and stores are
 // 16-B vectors), steps it S times with the neighbours taken from the
@@ -73,19 +73,30 @@ __global__ __launch_bounds__(kThreads) void k_heat_scalar(const double* __restri
 // the WIN - 2S points that are still exact (a point's value after S steps
 // depends on the S points each side).  Window w starts at out_lo + w*OUT - S,
 // OUT = WIN - 2S, so consecutive windows overlap by 2S points.  P = 4 halves
-// the cross-lane moves per point of P = 2 (the pass is FP64-VALU bound at
-// S = 8).
+// the cross-lane moves per point of P = 2.  r06: the pass is bound by each
+// wave's serial per-step chain (profiles/r06_heat_valu_pmc_g.txt), so ROWS =
+// 4 (independent rows: twice the chains per wave, 1024-point windows) against
+// 2: 2^30 points x 100 steps 26.7-27.6 -> 25.5-26.2 ms (ramp), 30.5-31.5 ->
+// 29.1-29.8 (random); 2 x 8, 4 x 8 (138 VGPRs) and 1 x 8 were no better
+// (profiles/r06_heat_window_ab_r.log).
 // HBM traffic per pass: 8 B read x WIN/OUT + 8 B written per point, i.e.
-// 16.26 B per point for S = 8 steps (16.55 B for S = 16) instead of 16 B per
+// 16.13 B per point for S = 8 steps (16.26 B for S = 16) instead of 16 B per
 // point per step.
 // Every point sees exactly the single-step arithmetic (heat() above, same
 // association, -ffp-contract=off), so results are bit-identical to S single
 // steps.  Points outside [0, n) come from the halos: cur[-j] = lh[S - j],
 // cur[n + j] = rh[j] (j < S; for one periodic partition lh = cur + n - S,
 // rh = cur).
-constexpr int kFusedPts = 4;                                // points per lane per row
-constexpr int kFusedRows = 2;
-constexpr int kFusedWin = kFusedRows * kFusedPts * kWave;  // 512 points
+#ifndef HPXHIP_HEAT_PTS
+#define HPXHIP_HEAT_PTS 4
+#endif
+#ifndef HPXHIP_HEAT_ROWS
+#define HPXHIP_HEAT_ROWS 4
+#endif
+constexpr int kFusedPts = HPXHIP_HEAT_PTS;                  // points per lane per row
+constexpr int kFusedRows = HPXHIP_HEAT_ROWS;
+static_assert(kFusedPts % 2 == 0 && kFusedRows * kFusedPts * kWave > 2 * 16, "16-B vectors; a window wider than its halos");
+constexpr int kFusedWin = kFusedRows * kFusedPts * kWave;  // 1024 points (hpx_amd/stencil.py FUSED_WINDOW)
 
 template <int S>
 __global__ __launch_bounds__(kThreads) void k_heat_fused(const double* __restrict__ cur, double* __restrict__ next,

@@ -20,7 +20,7 @@ from .compute import target, vector
 
 K, DT, DX = 0.5, 1.0, 1.0  # 1d_stencil_1.cpp:25-28
 MAX_FUSED = L.STENCIL_MAX_FUSED   # steps per HBM pass (hpxhip_stencil_heat_steps)
-FUSED_WINDOW = 512                # points per wave window of the fused kernel
+FUSED_WINDOW = 1024               # points per wave window of the fused kernel (stencil.hip kFusedWin)
 FUSED_MIN_POINTS = 2 * FUSED_WINDOW
 
 
@@ -54,8 +54,8 @@ def fused_passes(n: int, nt: int, match_parity: bool = False) -> list:
 
 
 def pass_hbm_bytes(n: int, steps: int) -> float:
-    """HBM bytes of one pass over n points: every wave window of 512 points
-    is read once and its 512 - 2*steps exact points written (a single step
+    """HBM bytes of one pass over n points: every wave window of FUSED_WINDOW points
+    is read once and its FUSED_WINDOW - 2*steps exact points written (a single step
     reads and writes each point once)."""
     if steps == 1:
         return 16.0 * n

@@ -371,4 +371,24 @@ lease_q() {
     python3 -u scripts/sort_probe.py 28 > ${L}_prof.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q"; fi
+lease_r() {
+  # round 6, lease r: the fused heat kernel's window shape (rows x points per lane; shipped 2 x 4): stencil
+  # probe at 2^30 for each build, twice, then the stencil tests under the 4 x 4 and 2 x 8 builds
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6r
+  for rep in 1 2; do
+    for v in main r4p4 r2p8 r4p8 r1p8; do
+      lib=scripts/ubench/seglib/$v/libhpxhip.so
+      [ $v = main ] && lib=hpx_amd/libhpxhip.so
+      echo "== $v rep $rep" >> ${L}_ab.log
+      HPXHIP_LIB=$lib timeout -k 10 200 python -u scripts/stencil_probe.py 30 >> ${L}_ab.log 2>&1 || exit $?
+    done
+  done
+  for v in r4p4 r2p8; do
+    HPXHIP_LIB=scripts/ubench/seglib/$v/libhpxhip.so timeout -k 10 400 python -u -m pytest -x -v --timeout 200 \
+      --timeout-method thread tests -m gpu -k "stencil or heat" > ${L}_tests_$v.log 2>&1 || exit $?
+  done
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r"; fi
