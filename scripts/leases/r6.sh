@@ -391,4 +391,15 @@ lease_r() {
   done
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r"; fi
+lease_s() {
+  # round 6, lease s: final validation (as lease k) of the tree with the 4-row heat windows, then the
+  # stencil probe at 2^30 and a kernel trace of the 2^28 pairs sort
+  LEASE_OUT=gpurun_out/r6s lease_k || exit $?
+  cd $GRAFT_REPO_ROOT
+  L=gpurun_out/r6s
+  timeout -k 10 200 python -u scripts/stencil_probe.py 30 > ${L}_stencil.log 2>&1 || exit $?
+  SORT_ONLY=pairs timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6s_prof_pairs -o run -- \
+    python3 -u scripts/sort_probe.py 28 > ${L}_sort_pairs.log 2>&1 || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s"; fi
