@@ -93,6 +93,9 @@ __global__ __launch_bounds__(kThreads) void k_heat_scalar(const double* __restri
 #ifndef HPXHIP_HEAT_ROWS
 #define HPXHIP_HEAT_ROWS 4
 #endif
+#ifndef HPXHIP_HEAT_LANERUN
+#define HPXHIP_HEAT_LANERUN 1
+#endif
 constexpr int kFusedPts = HPXHIP_HEAT_PTS;                  // points per lane per row
 constexpr int kFusedRows = HPXHIP_HEAT_ROWS;
 static_assert(kFusedPts % 2 == 0 && kFusedRows * kFusedPts * kWave > 2 * 16, "16-B vectors; a window wider than its halos");
@@ -144,6 +147,67 @@ __global__ __launch_bounds__(kThreads) void k_heat_fused(const double* __restric
             }
     }
 
+#if HPXHIP_HEAT_LANERUN
+    // r06, lane runs: the window passes through the wave's own LDS slice once
+    // after the loads and once before the stores, so that during the steps
+    // lane l holds the Q = ROWS x P consecutive points [lQ, lQ + Q): a step then
+    // needs two wave shifts (the run's two ends) instead of per-row shifts,
+    // row-crossing readlanes and their moves (124 -> 86 VALU instructions per
+    // step at 4 x 4; the kernel is VALU-issue bound).  LDS granules of 16 B
+    // are rotated by the run index (two-way bank conflicts at most on the
+    // run-wise reads).  2^30 points x 100 steps 25.2-25.6 -> 23.3-23.8 ms
+    // (ramp), 28.4-29.0 -> 27.0-27.2 (random), bit-identical; 2 x 4 runs
+    // (8 points per lane) 24.8-25.0 (profiles/r06_heat_lanerun_ab_t.log).
+    // The 32 KiB of LDS per block hold it to 5 waves per SIMD.
+    constexpr int Q = kFusedRows * P;
+    constexpr int QG = Q / 2;  // 16-B granules per run
+    __shared__ alignas(16) double s_win[kThreads / kWave][kFusedWin];
+    double* sw = s_win[threadIdx.x / kWave];
+    auto gpos = [](int pnt) {  // LDS slot (in doubles) of window point pnt (even)
+        const int run = pnt / Q, g = (pnt % Q) / 2;
+        return run * Q + ((g + run) % QG) * 2;
+    };
+#pragma unroll
+    for (int r = 0; r < kFusedRows; ++r)
+#pragma unroll
+        for (int h = 0; h < P / 2; ++h)
+            *reinterpret_cast<V2*>(sw + gpos(r * ROW + lane * P + 2 * h)) = V2{{x[r][2 * h], x[r][2 * h + 1]}};
+    __builtin_amdgcn_wave_barrier();
+    double y[Q];
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+        const V2 v = *reinterpret_cast<const V2*>(sw + lane * Q + ((g + lane) % QG) * 2);
+        y[2 * g] = v.v[0];
+        y[2 * g + 1] = v.v[1];
+    }
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+        // the window's outer neighbours (lane 0's left, lane 63's right) are
+        // 0.0: they feed only the 2S points that are not written
+        const double lft = dpp<DPP_WAVE_SHR1>(0.0, y[Q - 1]);
+        const double rgt = dpp<DPP_WAVE_SHL1>(0.0, y[0]);
+        double prev = lft;
+#pragma unroll
+        for (int e = 0; e < Q; ++e) {
+            const double m = y[e];
+            y[e] = heat(prev, m, e + 1 < Q ? y[e + 1] : rgt, c);
+            prev = m;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int g = 0; g < QG; ++g)
+        *reinterpret_cast<V2*>(sw + lane * Q + ((g + lane) % QG) * 2) = V2{{y[2 * g], y[2 * g + 1]}};
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < kFusedRows; ++r)
+#pragma unroll
+        for (int h = 0; h < P / 2; ++h) {
+            const V2 v = *reinterpret_cast<const V2*>(sw + gpos(r * ROW + lane * P + 2 * h));
+            x[r][2 * h] = v.v[0];
+            x[r][2 * h + 1] = v.v[1];
+        }
+#else
 #pragma unroll
     for (int t = 0; t < S; ++t) {
         double L[kFusedRows], R[kFusedRows];
@@ -168,6 +232,7 @@ __global__ __launch_bounds__(kThreads) void k_heat_fused(const double* __restric
             }
         }
     }
+#endif
 
 #pragma unroll
     for (int r = 0; r < kFusedRows; ++r)

@@ -402,4 +402,23 @@ lease_s() {
     python3 -u scripts/sort_probe.py 28 > ${L}_sort_pairs.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s"; fi
+lease_t() {
+  # round 6, lease t: the fused heat kernel with lane runs (HPXHIP_HEAT_LANERUN: each lane steps 16 / 8
+  # consecutive points, the window transposed through LDS): stencil tests under it, then the stencil probe
+  # at 2^30 for main (4 x 4 rows), lanerun (4 x 4) and lr2 (2 x 4), twice
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6t
+  HPXHIP_LIB=scripts/ubench/seglib/lanerun/libhpxhip.so timeout -k 10 400 python -u -m pytest -x -v --timeout 200 \
+    --timeout-method thread tests -m gpu -k "stencil or heat" > ${L}_tests_lanerun.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for v in main lanerun lr2; do
+      lib=scripts/ubench/seglib/$v/libhpxhip.so
+      [ $v = main ] && lib=hpx_amd/libhpxhip.so
+      echo "== $v rep $rep" >> ${L}_ab.log
+      HPXHIP_LIB=$lib timeout -k 10 200 python -u scripts/stencil_probe.py 30 >> ${L}_ab.log 2>&1 || exit $?
+    done
+  done
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t"; fi
