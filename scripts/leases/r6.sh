@@ -421,4 +421,13 @@ lease_t() {
   done
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t"; fi
+lease_u() {
+  # round 6, lease u: final validation (as lease k) of the tree with the lane-run heat kernel, then the
+  # stencil probe at 2^30 and the C++ drop-in program at the bench's 1-GPU size
+  LEASE_OUT=gpurun_out/r6u lease_k || exit $?
+  cd $GRAFT_REPO_ROOT
+  L=gpurun_out/r6u
+  timeout -k 10 200 python -u scripts/stencil_probe.py 30 > ${L}_stencil.log 2>&1 || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u"; fi
