@@ -200,6 +200,11 @@ constexpr uint64_t kCap18 = static_cast<uint64_t>(kSegThreads17) * kSegItems18;
 static_assert(kCap18 == kPadSlotMax, "padded slots hold a segment");
 // r06: the one-pass segment sort (k_bucket_sort ONEB) bound to three
 // workgroups per CU (6 waves per SIMD: <= 80 VGPRs); unbounded it took 119
+// r06: the look-back second pass (the padded pass's fallback) as a
+// persistent grid; 0: one workgroup per tile (A/B builds)
+#ifndef HPXHIP_XREG_PERSIST
+#define HPXHIP_XREG_PERSIST 1
+#endif
 #ifndef HPXHIP_SEG_MINW18
 #define HPXHIP_SEG_MINW18 6
 #endif
@@ -389,7 +394,11 @@ __global__ void k_sort_plan(const unsigned long long* __restrict__ hist, const u
                             jover[b2] += sum > static_cast<double>(kCap18);
                         }
                     } else {
-                        for (int r = 0; r < 8; ++r) jover[b2] += j[r] / static_cast<double>(1 << (b2 - 3)) > kCap18;
+                        // (j / 2^k > cap as j > cap * 2^k: exact, and no f64
+                        // division -- 384 of them per thread had been most of
+                        // the plan's ~50 us)
+                        const double lim = static_cast<double>(kCap18) * static_cast<double>(1 << (b2 - 3));
+                        for (int r = 0; r < 8; ++r) jover[b2] += j[r] > lim;
                     }
                 }
             }
@@ -853,11 +862,17 @@ int run_sort(void* keys, void* vals, uint64_t n, hipStream_t s, void* scratch, s
                 hipLaunchKernelGGL(k_zero_gated, dim3(grid_for(zbytes / 16, 2048)), dim3(256), 0, s,
                                    reinterpret_cast<uint4*>(counter), zbytes / 16, ctl + C_B9);
                 HPXHIP_CHECK_LAUNCH();
+                // r06: a persistent grid (two workgroups per CU claiming the
+                // regions' tiles in order), since the padded pass leaves this
+                // pass to its rare overflow: a skipped launch of one workgroup
+                // per tile had dispatched 131080 workgroups that only read the
+                // gate (~60 us per 2^30 sort)
+                const unsigned gx = static_cast<unsigned>(std::min<uint64_t>(nt, 2ull * current_device_info().cus));
                 auto launch = [&](auto gtag) {
                     using G = decltype(gtag);
                     hipLaunchKernelGGL((k_onesweep<U, VAL, false, G, X, TS::threads, TS::items, TS::lbb, 9, true, false,
-                                                   false, true, true>),
-                                       dim3(static_cast<unsigned>(nt)), dim3(TS::threads), 0, s, ka, kc,
+                                                   HPXHIP_XREG_PERSIST != 0, true, true>),
+                                       dim3(HPXHIP_XREG_PERSIST ? gx : static_cast<unsigned>(nt)), dim3(TS::threads), 0, s, ka, kc,
                                        static_cast<const VAL*>(nullptr), static_cast<VAL*>(nullptr), n, 0,
                                        reinterpret_cast<const unsigned long long*>(base + L.bs2),
                                        reinterpret_cast<G*>(base + L.lb), counter, err, X{}, ctl + C_B9, nt,

@@ -618,7 +618,11 @@ __global__ __launch_bounds__(THREADS) void k_onesweep(const U* __restrict__ kin,
                                                        const unsigned long long* __restrict__ prev_starts = nullptr) {
     static_assert(!PERSIST || STAGE, "the persistent form keeps the LDS-staged write-out");
     static_assert(!SEG || ((PERSIST || XREG) && LBB > 0), "segmented passes: look-back passes, persistent or XREG");
-    static_assert(!XREG || !PERSIST, "XCD regions: one tile per block");
+    // XREG + PERSIST (r06, SEG only): workgroups claim tiles from the region
+    // counters until every region is done (the claim returns no tile); a
+    // claimed tile's predecessors were claimed earlier by running workgroups,
+    // so the look-back always finds them published
+    static_assert(!XREG || !PERSIST || SEG, "XCD regions, persistent: the segmented (region) pass");
     static_assert(!XREG || SEG || LBB < 0, "XCD regions of equal tile ranges: the offset-fed pass (no look-back)");
     // segment table entries a workgroup loads (XREG: the 8 regions)
     constexpr int NS = XREG ? 8 : kMaxBig;

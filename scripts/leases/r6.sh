@@ -430,4 +430,21 @@ lease_u() {
   timeout -k 10 200 python -u scripts/stencil_probe.py 30 > ${L}_stencil.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u"; fi
+lease_v() {
+  # round 6, lease v: the planner without f64 divisions and the padded pass's look-back fallback as a
+  # persistent grid: sort tests (with the new forced-overflow cases), 2^30 u64 / u32 probes, u64 kernel trace
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6v
+  timeout -k 10 800 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sort_hybrid.py \
+    tests/test_gpu_parity.py tests/test_gpu_fullsize.py -k "sort" > ${L}_tests.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for c in u64 u32; do
+      SORT_ONLY=$c timeout -k 10 200 python -u scripts/sort_probe.py 30 >> ${L}_probe.log 2>&1 || exit $?
+    done
+  done
+  SORT_ONLY=u64 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r6v_prof_u64 -o run -- \
+    python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v"; fi

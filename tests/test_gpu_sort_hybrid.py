@@ -363,6 +363,29 @@ def test_one_pass_segment_sort_mixed_bins(pol, gpu_target):
     check(pol, gpu_target, h, True)
 
 
+@pytest.mark.parametrize("kdt", [np.uint64, np.uint32])
+@pytest.mark.parametrize("extra", [1000, 3000])
+def test_padded_pass_overflow_fallback(pol, gpu_target, kdt, extra):
+    """r06, the padded second prefix pass's fallback: `extra` keys share one
+    (top-9, 4-bit field) cell of a 2^24-key sort, which the planner's
+    marginal estimate (largest top-9 bin x largest field group / n, ~2100
+    keys per bucket, slots of ~2500) cannot see.  The cell's slot overflows
+    (k_pad_scatter raises C_PADOVF), k_pad_check hands the sort to the
+    look-back pass (the persistent XREG form) from the same input; with
+    3000 extra keys the bucket (~5000) is also over the 4608-key segment and
+    is finished by the oversized-bucket LSD."""
+    rng = np.random.default_rng(0x0F10 + extra)
+    n = 1 << 24
+    bits = np.dtype(kdt).itemsize * 8
+    h = rng.integers(0, 2**bits - 1, n, dtype=kdt, endpoint=True)
+    low = bits - 13
+    cell = kdt(int(rng.integers(0, 1 << 13)) << low)
+    h[:extra] = cell | rng.integers(0, 1 << low, extra, dtype=kdt)
+    rng.shuffle(h)
+    check(pol, gpu_target, h)
+    check(pol, gpu_target, h, True)
+
+
 def test_one_pass_pairs_segment_sort_mixed_bins(pol, gpu_target):
     """sort_by_key over the keys of the test above (sort_by_key's 512 x 9
     segments; buckets whose 13 bits under the top take 4 values), plus 5000
