@@ -447,4 +447,9 @@ lease_v() {
     python3 -u scripts/sort_probe.py 30 > ${L}_prof.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v"; fi
+lease_w() {
+  # round 6, lease w: final validation (as lease k) of the round's last tree
+  LEASE_OUT=gpurun_out/r6w lease_k || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v w"; fi
