@@ -62,9 +62,15 @@ constexpr int kHistBlocksPerCU = 4;  // 4 lane copies x 8 KiB per pass histogram
 // 8 and 5.48 at 16; rocPRIM's radix_sort_keys takes 50.2 ms for the whole
 // 2^30 u64 sort on the same GPU, the plain LSD here 40 ms, the hybrid 21 ms).
 template <bool HAS_VAL>
+#ifndef HPXHIP_KV_THREADS
+#define HPXHIP_KV_THREADS 256
+#endif
+#ifndef HPXHIP_KV_ITEMS
+#define HPXHIP_KV_ITEMS 16
+#endif
 struct tile_shape {
-    static constexpr int threads = HAS_VAL ? 256 : 512;
-    static constexpr int items = 16;
+    static constexpr int threads = HAS_VAL ? HPXHIP_KV_THREADS : 512;
+    static constexpr int items = HAS_VAL ? HPXHIP_KV_ITEMS : 16;
     static constexpr int lbb = 4;
     static constexpr int tile = threads * items;
 };

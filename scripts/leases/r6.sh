@@ -452,4 +452,26 @@ lease_w() {
   LEASE_OUT=gpurun_out/r6w lease_k || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v w"; fi
+lease_x() {
+  # round 6, lease x: sort_by_key's prefix-pass tile (HPXHIP_KV_THREADS x HPXHIP_KV_ITEMS; shipped 256 x 16,
+  # 2 workgroups = 8 waves per CU): sort_by_key tests under 512 x 8, then pairs 2^28 / 2^26 for main,
+  # kv512x8 and kv512x6, twice
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6x
+  HPXHIP_LIB=scripts/ubench/seglib/kv512x8/libhpxhip.so timeout -k 10 600 python -u -m pytest -x -v --timeout 300 \
+    --timeout-method thread tests/test_gpu_sort_hybrid.py tests/test_gpu_parity.py -k "by_key or pairs" \
+    > ${L}_tests_kv512x8.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for v in main kv512x8 kv512x6; do
+      lib=scripts/ubench/seglib/$v/libhpxhip.so
+      [ $v = main ] && lib=hpx_amd/libhpxhip.so
+      for lg in 28 26; do
+        echo "== $v pairs 2^$lg rep $rep" >> ${L}_ab.log
+        HPXHIP_LIB=$lib SORT_ONLY=pairs timeout -k 10 200 python -u scripts/sort_probe.py $lg >> ${L}_ab.log 2>&1 || exit $?
+      done
+    done
+  done
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v w x"; fi
