@@ -474,4 +474,18 @@ lease_x() {
   done
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v w x"; fi
+lease_y() {
+  # round 6, lease y: the library rebuilt from the committed tree (the tile knob only): smoke, the sort and
+  # stencil GPU tests, and the one-rank RCCL rehearsal of the N > 1 rows (segmented reduce / scan / sort,
+  # the 2^32 stencil) with the lane-run heat kernel
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6y
+  timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > ${L}_smoke.log 2>&1 || exit $?
+  timeout -k 10 800 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu \
+    -k "sort or stencil or heat" > ${L}_tests.log 2>&1 || exit $?
+  HPXHIP_RCCL_SELF=1 timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+    --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --no-cpu --no-pmc > ${L}_rccl_self.log 2>&1 || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v w x y"; fi
