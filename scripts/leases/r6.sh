@@ -488,4 +488,23 @@ lease_y() {
     --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --no-cpu --no-pmc > ${L}_rccl_self.log 2>&1 || exit $?
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v w x y"; fi
+lease_z() {
+  # round 6, lease z: the lane-run heat kernel's LDS transpose in two halves (HPXHIP_HEAT_LDS_HALF: 16 KiB
+  # per block, 6 waves per SIMD instead of 5): stencil tests under it, then the stencil probe at 2^30 for
+  # main and half, twice
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6z
+  HPXHIP_LIB=scripts/ubench/seglib/half/libhpxhip.so timeout -k 10 400 python -u -m pytest -x -v --timeout 200 \
+    --timeout-method thread tests -m gpu -k "stencil or heat" > ${L}_tests_half.log 2>&1 || exit $?
+  for rep in 1 2; do
+    for v in main half; do
+      lib=scripts/ubench/seglib/$v/libhpxhip.so
+      [ $v = main ] && lib=hpx_amd/libhpxhip.so
+      echo "== $v rep $rep" >> ${L}_ab.log
+      HPXHIP_LIB=$lib timeout -k 10 200 python -u scripts/stencil_probe.py 30 >> ${L}_ab.log 2>&1 || exit $?
+    done
+  done
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v w x y z"; fi
