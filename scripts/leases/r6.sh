@@ -507,4 +507,13 @@ lease_z() {
   done
 }
 
-if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v w x y z"; fi
+lease_fin() {
+  # round 6, last lease: the whole GPU suite and smoke on the round's final tree (library relinked after z)
+  cd $GRAFT_REPO_ROOT
+  export TMPDIR=/tmp
+  L=gpurun_out/r6fin
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > ${L}_tests.log 2>&1 || exit $?
+  timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > ${L}_smoke.log 2>&1 || exit $?
+}
+
+if [ $# -eq 1 ]; then "lease_$1"; else echo "leases: a b c d e f g h i j k l m n o p q r s t u v w x y z fin"; fi
